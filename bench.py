@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""LM-BA iterations/sec + final reprojection RMSE on the synthetic 1k-camera / 200k-point / 2M-observation scene
+(BASELINE.json configs[2]; configs[3] when run on N GPUs: the same scene track-sharded, strong scaling).
+
+A "step" is one LM step (bae.optim.LM.step semantics: linearize, damped Schur solve with block-Jacobi PCG, trial,
+TrustRegion accept/reject) over the whole scene.  Inputs are resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL all-reduce of the camera system)
+
+Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) is the build's C/OpenMP restatement of the same LM
+(oracle/ba_oracle.c; the reference has no CPU BA) run to convergence on the same scene.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(kernel, C, P, N, D, nnzb):
+    """Compulsory HBM bytes of one launch (every input byte read once, every output byte written once)."""
+    if kernel == "k_schur":
+        return (N * D * 3 * 8          # W_o
+                + N * 4 * 3            # cam_obs, ptl, cam
+                + (P + 1) * 4          # pt_ptr
+                + P * 9 * 8            # V^-1 (6) + y (3)
+                + C * (D * D + D) * 8  # U, g_c
+                + nnzb * D * D * 8     # S (upper blocks) written
+                + C * D * 8)           # b written
+    if kernel == "k_cg_iter":
+        nlo = nnzb - C
+        return (nnzb * D * D * 8       # S~ upper blocks (diag blocks are I and never read)
+                - C * D * D * 8
+                + C * D * D * 8        # L_i (true-residual norm)
+                + (C + 1) * 4 * 2 + (nnzb - C) * 4 + nlo * 8   # row_ptr/lo_ptr, col, lo_col+lo_blk
+                + 10 * C * D * 8)      # r, w, s, p, x read + written
+    raise ValueError(kernel)
+
+
+def cpu_baseline(prob, max_steps):
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    t0 = time.perf_counter()
+    cams, pts, hist, rmse = O.solve_to_convergence(prob, max_iters=max_steps, threads=threads)
+    dt = time.perf_counter() - t0
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return dict(value=len(hist) / dt, unit="LM it/s", cores=threads, kind="port",
+                sample=f"oracle/ba_oracle.c (C/OpenMP f64 restatement of the same LM), same scene, {len(hist)} LM steps "
+                       f"to the reference stop rule in {dt:.2f} s incl. setup; CPU: {model}",
+                final_rmse_px=rmse, steps=len(hist))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-max-steps", type=int, default=30)
+    ap.add_argument("--deterministic", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from instantsfm_amd.engine import BundleAdjuster
+    from instantsfm_amd.shard import shard_ranges
+    from instantsfm_amd.synth import CONFIGS, make_config
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    prob = make_config(args.config, seed=args.seed)
+    shards = shard_ranges(prob.pt_idx, prob.n_points, world)
+    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
+                         deterministic=args.deterministic, world_size=world, rank=rank, shard=shards[rank])
+    cams0 = torch.from_numpy(prob.cams_init).to(dev)
+    pts0 = torch.from_numpy(prob.points_init).to(dev)
+    cams, pts = cams0.clone(), pts0.clone()
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.step(cams, pts)
+    eng.reset()
+    cams.copy_(cams0)
+    pts.copy_(pts0)
+    barrier()
+    t0 = time.perf_counter()
+    stats = []
+    losses = []
+    for _ in range(args.steps):
+        loss, st = eng.step(cams, pts)
+        losses.append(loss)
+        stats.append(st)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    final_loss, rmse = eng.cost(cams, pts)
+
+    # stop rule of bundle_adjustment.py:134-141 applied to the timed loss history
+    conv_step = None
+    for k in range(8, len(losses) + 1):
+        h = losses[:k]
+        a, b = np.mean(h[-4:]), np.mean(h[-8:-4])
+        if abs((b - a) / b) < 5e-4 or h[-1] == h[-2]:
+            conv_step = k
+            break
+
+    C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
+    Pl = shards[rank][1] - shards[rank][0]
+    Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
+    nnzb = eng.nnzb()
+    ph = np.sum([s["time_ms"] for s in stats], axis=0)
+    trials = sum(s["trials"] for s in stats)
+    cg_launches = sum(s["cg_launches"] for s in stats)
+    kern = {
+        "k_schur": (ph[1], trials, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb)),
+        "k_cg_iter": (ph[5], cg_launches, algorithmic_bytes("k_cg_iter", C, Pl, Nl, D, nnzb)),
+    }
+    name = max(kern, key=lambda k: kern[k][0])
+    tot_ms, launches, nbytes = kern[name]
+    avg_s = tot_ms / 1e3 / max(launches, 1)
+    achieved = nbytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    roof = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": int(nbytes), "launches": int(launches)}
+
+    out = {
+        "metric": "LM-BA iterations/sec (+ final reprojection RMSE)",
+        "value": round(args.steps / dt, 4),
+        "unit": "LM it/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded scene generator instantsfm_amd/synth.py, SURVEY.md 8(d))",
+        "config": {"workload": f"config {args.config}: synthetic {C}-cam / {P}-point / {N}-obs SIMPLE_RADIAL BA, "
+                               f"LM steps of the full scene" + (", track-sharded" if world > 1 else ""),
+                   "cams": C, "points": P, "obs": N, "camera_block_dim": D, "schur_blocks": nnzb,
+                   "parallelism": f"track-shard x{world}" if world > 1 else "single GPU"},
+        "final_loss": final_loss,
+        "final_rmse_px": rmse,
+        "converged_at_step": conv_step,
+        "pcg_iters": [s["pcg_iters"] for s in stats],
+        "trials": trials,
+        "phase_ms_per_step": {k: round(float(v) / args.steps, 3) for k, v in
+                              zip(["linearize", "k_schur", "linear_solve", "backsub_update", "trial_cost", "k_cg_iter"], ph)},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(prob, args.cpu_max_steps)
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["cpu_final_rmse_px"] = cb["final_rmse_px"]
+        out["cpu_steps_to_converge"] = cb["steps"]
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * insfm_ba.h -- C ABI of the MI355X-native sparse bundle-adjustment core.
+ *
+ * This library replaces the engine row under InstantSfM's TorchBA processor:
+ *   - the per-step call  `loss = optimizer.step(input)`  of  `bae.optim.LM(model, strategy=TrustRegion(...),
+ *     solver=PCG(tol=1e-5), kernel=Huber(thres), reject=30)`   (instantsfm/processors/bundle_adjustment.py:115-119, :132)
+ *     -> insfm_ba_step();
+ *   - the residual model `ReprojNonBatched.forward` = `reproject_funcs[model](points_3d[pi], pose[ci], pp[ci]) - points_2d`
+ *     (bundle_adjustment.py:51-64, cost_function.py:32-208) and its TrackingTensor sparse Jacobian
+ *     (bae.autograd.function, un-vendored)  -> fused into the library's linearize kernels;
+ *   - `bae.utils.pysolvers.PCG` and the cuDSS sparse solve (un-vendored)  -> Schur complement + block-Jacobi PCG kernels;
+ *   - `model.loss(input)` (pypose RobustModel, Huber kernel)  -> insfm_ba_cost().
+ * Creation corresponds to the LM/model construction at bundle_adjustment.py:115-119 (packed inputs of :98-113).
+ *
+ * Plain C types only.  Device pointers are HIP device memory (e.g. the data_ptr() of a torch ROCm tensor).
+ * All functions return INSFM_BA_OK (0) or a negative error code; insfm_ba_last_error() gives text.
+ * One handle per device and stream; calls on a handle must be serialised by the caller.
+ */
+#ifndef INSFM_BA_H
+#define INSFM_BA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define INSFM_BA_OK 0
+#define INSFM_BA_EINVAL (-22)   /* bad descriptor / inputs (e.g. obs not track-major, unsupported model) */
+#define INSFM_BA_ENOMEM (-12)   /* device or host allocation failed */
+#define INSFM_BA_EHIP (-100)    /* HIP runtime error (message in insfm_ba_last_error) */
+#define INSFM_BA_ECOMM (-101)   /* cross-rank all-reduce callback failed */
+#define INSFM_BA_ESOLVER (-102) /* linear solver breakdown: params unchanged, loss == previous loss
+                                   (mirrors "Linear solver failed. Breaking optimization step..." in the LM) */
+
+typedef struct insfm_ba insfm_ba;
+
+/* Sum `count` doubles starting at `dev_buf` across ranks, in place, ordered after all work the library
+ * has queued on its stream (a torch.distributed all_reduce on the current stream satisfies this). */
+typedef int (*insfm_ba_allreduce_fn)(void* ctx, double* dev_buf, int64_t count);
+
+typedef struct {
+    int32_t n_cams;        /* C: rows of camera_params (registered, observed images after compaction) */
+    int32_t n_points;      /* P: rows of points_3d */
+    int32_t n_obs;         /* N: observations (after the cheirality filter, bundle_adjustment.py:102-107) */
+    int32_t cam_model;     /* CameraModelId value (defs.py:101-113); 7 (FOV) and 10 (THIN_PRISM) -> EINVAL */
+    int32_t optimize_poses;/* 0: cameras frozen, points-only solve (track_retriangulation.py:247-249) */
+    int32_t deterministic; /* 1: fixed-order reductions everywhere (bitwise reproducible Schur build) */
+    double huber_delta;    /* BUNDLE_ADJUSTER_OPTIONS['thres_loss_function'] */
+    double tr_radius, tr_max, tr_min, tr_up, tr_down, tr_factor, tr_high, tr_low; /* TrustRegion(1e4, 1e10, .., 2, 1/16, ..) */
+    double clamp_min, clamp_max;   /* A.diagonal().clamp_(1e-6, 1e32) */
+    int32_t max_rejects;           /* LM(reject=30) */
+    int32_t pcg_max_iter;          /* PCG iteration cap */
+    double pcg_tol;                /* PCG(tol=1e-5): ||b - S x|| <= tol ||b|| */
+    int32_t world_size, rank;      /* track-sharded multi-GPU; 1 / 0 for a single GPU */
+    int32_t shard_point_begin;     /* points [begin, end) (and their observations) belong to this rank */
+    int32_t shard_point_end;
+    insfm_ba_allreduce_fn allreduce;  /* required when world_size > 1 */
+    void* allreduce_ctx;
+} insfm_ba_desc;
+
+typedef struct {
+    double loss;            /* robust (Huber) loss after the step, == LM.step() return value */
+    double loss_before;     /* loss at the start of the step */
+    double damping;         /* 1 / TrustRegion radius after the step */
+    int32_t trials;         /* linear solves this step (1 + rejected trials) */
+    int32_t rejects;
+    int32_t pcg_iters_last; /* PCG iterations of the final trial */
+    int32_t pcg_iters_total;
+    int32_t solver_failed;
+    int32_t cg_launches;    /* k_cg_iter launches this step (incl. the cheap early-exit ones after convergence) */
+    double time_ms[8];      /* device time per phase (hipEvent on the library stream), filled when stats != NULL:
+                               [0] linearize  [1] k_schur  [2] whole linear solve (point prep .. CG finish, incl. the
+                               host polls of the CG status)  [3] back-substitution + update  [4] trial cost
+                               [5] k_cg_iter launches only (back-to-back chunks, no host gaps)  [6..7] 0 */
+} insfm_ba_stats;
+
+/* Fill `desc` with the reference's defaults (TorchBA + BUNDLE_ADJUSTER_OPTIONS, config/colmap.py:47-54). */
+void insfm_ba_default_desc(insfm_ba_desc* desc);
+
+/* Create a solver.  obs_uv [N,2] f64, cam_idx [N] i32 (compacted camera row), pt_idx [N] i32 (compacted point row,
+ * nondecreasing = track-major as TorchBA packs them), pp [C,2] f64: HOST pointers, copied.  `stream` is a hipStream_t
+ * (NULL = default stream).  Device memory is allocated here and freed by insfm_ba_destroy. */
+int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32_t* cam_idx, const int32_t* pt_idx,
+                    const double* pp, void* stream, insfm_ba** out);
+
+/* One LM step (bae.optim.LM.step semantics).  cam_params [C, 7+n_intr] ([t, q_xyzw, intrinsics without pp]) and
+ * points [P,3] are DEVICE pointers, read at the start and updated in place at the end (on a multi-rank run each
+ * rank updates only its shard's points).  `stats` may be NULL.  Blocks for one 64-byte device->host copy per trial. */
+int insfm_ba_step(insfm_ba* h, double* cam_params, double* points, insfm_ba_stats* stats);
+
+/* Robust loss and raw reprojection RMSE (sqrt(sum ||r||^2 / N)) at the given DEVICE parameters. */
+int insfm_ba_cost(insfm_ba* h, const double* cam_params, const double* points, double* loss, double* rmse);
+
+/* Multi-rank runs: the reduced system [S | b | U | g_c | scalars] must live in a caller-owned DEVICE buffer that the
+ * allreduce callback can reach (e.g. a torch tensor).  Query the size after create, then hand the buffer over before
+ * the first step.  The callback is then only ever called with sub-ranges of this buffer. */
+int64_t insfm_ba_exchange_count(const insfm_ba* h);
+int insfm_ba_set_exchange(insfm_ba* h, double* dev_buf, int64_t count);
+
+/* Forget the cached loss/damping state (a fresh LM, as TorchBA builds one per Solve). */
+int insfm_ba_reset(insfm_ba* h);
+
+void insfm_ba_destroy(insfm_ba* h);
+const char* insfm_ba_last_error(const insfm_ba* h);
+
+/* ---- introspection used by the parity tests (not needed by TorchBA) -------------------------------------- */
+/* Linearize at DEVICE params (fills W, V, g_p, U, g_c). */
+int insfm_ba_debug_linearize(insfm_ba* h, const double* cam_params, const double* points);
+/* Build and solve the damped system for cumulative damping factor f; returns PCG iterations or a negative code. */
+int insfm_ba_debug_solve(insfm_ba* h, double f);
+/* Copy an internal buffer to HOST memory: 0 W[N,D,3] 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
+ * solve)[nnzb,D,D] 6 b[C,D] 7 dc[C,D] 8 dp[P,3].  Returns the number of doubles copied or a negative code. */
+int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
+/* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */
+int64_t insfm_ba_nnzb(const insfm_ba* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* INSFM_BA_H */

@@ -1,0 +1,116 @@
+"""ctypes binding of the C ABI in include/insfm_ba.h (libinsfm_ba.so, built in-tree for gfx950).
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible, every entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libinsfm_ba.so")
+
+INSFM_BA_OK = 0
+INSFM_BA_EINVAL = -22
+INSFM_BA_ENOMEM = -12
+INSFM_BA_EHIP = -100
+INSFM_BA_ECOMM = -101
+INSFM_BA_ESOLVER = -102
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [
+        ("n_cams", ctypes.c_int32), ("n_points", ctypes.c_int32), ("n_obs", ctypes.c_int32),
+        ("cam_model", ctypes.c_int32), ("optimize_poses", ctypes.c_int32), ("deterministic", ctypes.c_int32),
+        ("huber_delta", ctypes.c_double),
+        ("tr_radius", ctypes.c_double), ("tr_max", ctypes.c_double), ("tr_min", ctypes.c_double),
+        ("tr_up", ctypes.c_double), ("tr_down", ctypes.c_double), ("tr_factor", ctypes.c_double),
+        ("tr_high", ctypes.c_double), ("tr_low", ctypes.c_double),
+        ("clamp_min", ctypes.c_double), ("clamp_max", ctypes.c_double),
+        ("max_rejects", ctypes.c_int32), ("pcg_max_iter", ctypes.c_int32),
+        ("pcg_tol", ctypes.c_double),
+        ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32),
+        ("shard_point_begin", ctypes.c_int32), ("shard_point_end", ctypes.c_int32),
+        ("allreduce", ALLREDUCE_FN), ("allreduce_ctx", ctypes.c_void_p),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("loss", ctypes.c_double), ("loss_before", ctypes.c_double), ("damping", ctypes.c_double),
+        ("trials", ctypes.c_int32), ("rejects", ctypes.c_int32), ("pcg_iters_last", ctypes.c_int32),
+        ("pcg_iters_total", ctypes.c_int32), ("solver_failed", ctypes.c_int32), ("cg_launches", ctypes.c_int32),
+        ("time_ms", ctypes.c_double * 8),
+    ]
+
+    def as_dict(self):
+        return dict(loss=self.loss, loss_before=self.loss_before, damping=self.damping, trials=self.trials,
+                    rejects=self.rejects, pcg_iters=self.pcg_iters_last, pcg_total=self.pcg_iters_total,
+                    failed=self.solver_failed, cg_launches=self.cg_launches, time_ms=list(self.time_ms)[:6])
+
+
+# exported symbols (every one declared in include/insfm_ba.h)
+SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
+           "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
+           "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange")
+
+_lib = None
+
+
+class BAError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"insfm_ba error {code}: {msg}")
+        self.code = code
+
+
+def load(path=LIB_PATH):
+    """Load the HIP library (no GPU needed to load it).  Raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(path)
+    vp, dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
+    L.insfm_ba_default_desc.argtypes = [ctypes.POINTER(Desc)]
+    L.insfm_ba_default_desc.restype = None
+    L.insfm_ba_create.argtypes = [ctypes.POINTER(Desc), dp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                  dp, vp, ctypes.POINTER(vp)]
+    L.insfm_ba_create.restype = ctypes.c_int
+    L.insfm_ba_step.argtypes = [vp, vp, vp, ctypes.POINTER(Stats)]
+    L.insfm_ba_step.restype = ctypes.c_int
+    L.insfm_ba_cost.argtypes = [vp, vp, vp, dp, dp]
+    L.insfm_ba_cost.restype = ctypes.c_int
+    L.insfm_ba_reset.argtypes = [vp]
+    L.insfm_ba_reset.restype = ctypes.c_int
+    L.insfm_ba_destroy.argtypes = [vp]
+    L.insfm_ba_destroy.restype = None
+    L.insfm_ba_last_error.argtypes = [vp]
+    L.insfm_ba_last_error.restype = ctypes.c_char_p
+    L.insfm_ba_debug_linearize.argtypes = [vp, vp, vp]
+    L.insfm_ba_debug_linearize.restype = ctypes.c_int
+    L.insfm_ba_debug_solve.argtypes = [vp, ctypes.c_double]
+    L.insfm_ba_debug_solve.restype = ctypes.c_int
+    L.insfm_ba_debug_get.argtypes = [vp, ctypes.c_int32, dp]
+    L.insfm_ba_debug_get.restype = ctypes.c_int64
+    L.insfm_ba_nnzb.argtypes = [vp]
+    L.insfm_ba_nnzb.restype = ctypes.c_int64
+    L.insfm_ba_exchange_count.argtypes = [vp]
+    L.insfm_ba_exchange_count.restype = ctypes.c_int64
+    L.insfm_ba_set_exchange.argtypes = [vp, vp, ctypes.c_int64]
+    L.insfm_ba_set_exchange.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def default_desc():
+    d = Desc()
+    load().insfm_ba_default_desc(ctypes.byref(d))
+    return d
+
+
+def check(h, rc):
+    if rc < 0:
+        msg = load().insfm_ba_last_error(h).decode() if h else ""
+        raise BAError(rc, msg)
+    return rc

@@ -1,0 +1,1391 @@
+// MI355X (gfx950) sparse bundle-adjustment core: HIP kernels + host LM driver behind include/insfm_ba.h.
+//
+// One LM step (bae.optim.LM.step as reconstructed in SURVEY.md 3.3, options of bundle_adjustment.py:115-119):
+//   linearize (per step)   k_lin_points  : per track, residual + analytic J + Huber/Triggs weight  -> W_o, V_p, g_p
+//                          k_lin_cams    : per camera, J~c^T J~c and -J~c^T r~ (LDS-staged batch)  -> U_c, g_c
+//   per trial (damping f)  k_point_prep  : V_p clamp/damp + 3x3 SPD inverse                          -> V^-1, y = V^-1 g_p
+//                          k_schur       : per camera row, LDS-resident row of S (upper blocks), b
+//                          k_cg_factor / k_cg_scale : S_ii = L L^T, S~ = L^-1 S L^-T, r0 = L^-1 b
+//                          k_cg_iter x k : Chronopoulos-Gear CG on S~, ONE launch per iteration
+//                          k_cg_finish   : dc = L^-T x~
+//                          k_backsub     : dp = V^-1 (g_p - W^T dc), trial points, gain terms
+//                          k_update_cams : SE3 left retraction, intrinsics +=, gain terms
+//                          k_cost        : Huber loss + sum ||r||^2 at the trial parameters
+//                          k_final       : fixed-order reduction of all partials -> 64 B to the host
+// Every cross-workgroup reduction is a fixed-order partial sum (no float atomics in global memory), so a step is
+// bitwise reproducible when desc.deterministic = 1 (the Schur row accumulation then uses one wave per row).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/insfm_ba.h"
+#include "ba_device.h"
+
+using namespace insfm;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgroup
+
+// ------------------------------------------------------------------------------------------------------------
+// reductions
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Fixed-order block reduction of NV values per thread; result valid in thread 0 (and returned to all).
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= kThreads*NV doubles */) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sh[k * kThreads + t] = v[k];
+    __syncthreads();
+    for (int s = kThreads / 2; s >= 1; s >>= 1) {
+        if (t < s) {
+#pragma unroll
+            for (int k = 0; k < NV; ++k) sh[k * kThreads + t] += sh[k * kThreads + t + s];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = sh[k * kThreads];
+    __syncthreads();
+}
+
+// Sum n partial records of NV doubles (record-major) in a fixed order; every thread gets the result.
+template <int NV>
+__device__ __forceinline__ void sum_partials(const double* __restrict__ part, int n, double (&out)[NV], double* sh) {
+    double v[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = 0.0;
+    for (int i = threadIdx.x; i < n; i += kThreads)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) v[k] += part[(size_t)i * NV + k];
+    block_sum<NV>(v, sh);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) out[k] = v[k];
+}
+
+__device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
+    const double rs = sqrt(s);
+    const double w = rs < delta ? 1.0 : delta / rs;
+    return sqrt(w);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// linearization
+// ------------------------------------------------------------------------------------------------------------
+// One thread per (local) track: every observation's weighted J gives W_o = J~c^T J~p (stored [o][D][3]); the track
+// reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~ in registers.
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lin_points(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+                                                         const double* __restrict__ uv, const double* __restrict__ pp,
+                                                         const double* __restrict__ cams, const double* __restrict__ pts,
+                                                         double delta, double* __restrict__ W, double* __restrict__ V,
+                                                         double* __restrict__ gp) {
+    constexpr int D = kD<M>, ST = kStride<M>;
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= Pl) return;
+    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+    double Vs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+    const int ob = pt_ptr[p], oe = pt_ptr[p + 1];
+    for (int o = ob; o < oe; ++o) {
+        const int c = cam[o];
+        const double2 z = reinterpret_cast<const double2*>(uv)[o];
+        const double uvo[2] = {z.x, z.y};
+        const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+        double r[2], Jc[2][D], Jp[2][3];
+        eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
+        const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+        r[0] *= sw; r[1] *= sw;
+#pragma unroll
+        for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
+        double* Wo = W + (size_t)o * D * 3;
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) Wo[a * 3 + k] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+        Vs[0] += Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
+        Vs[1] += Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
+        Vs[2] += Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
+        Vs[3] += Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
+        Vs[4] += Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
+        Vs[5] += Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) g[k] -= Jp[0][k] * r[0] + Jp[1][k] * r[1];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) V[6 * (size_t)p + k] = Vs[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gp[3 * (size_t)p + k] = g[k];
+}
+
+// One workgroup per camera: 256 observations at a time are evaluated (one per thread) into an LDS batch
+// [obs][J~c row0 | J~c row1 | r~0 r~1]; then thread e owns entry e of [U (DxD) | g_c (D)] and sums the batch in
+// observation order (the oracle's order).
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ cam_ptr, const int* __restrict__ cam_obs,
+                                                       const int* __restrict__ ptl, const double* __restrict__ uv,
+                                                       const double* __restrict__ pp, const double* __restrict__ cams,
+                                                       const double* __restrict__ pts, double delta, double* __restrict__ U,
+                                                       double* __restrict__ gc) {
+    constexpr int D = kD<M>, ST = kStride<M>;
+    constexpr int RW = 2 * D + 2;
+    constexpr int E = D * D + D;
+    constexpr int EPT = (E + kThreads - 1) / kThreads;
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    const int c = blockIdx.x, t = threadIdx.x;
+    const int eb = cam_ptr[c], ee = cam_ptr[c + 1];
+    double camv[ST];
+#pragma unroll
+    for (int k = 0; k < ST; ++k) camv[k] = cams[(size_t)c * ST + k];
+    const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+    double acc[EPT];
+#pragma unroll
+    for (int m = 0; m < EPT; ++m) acc[m] = 0.0;
+    for (int base = eb; base < ee; base += kThreads) {
+        const int e = base + t;
+        double* row = sh + (size_t)t * RW;
+        if (e < ee) {
+            const int o = cam_obs[e];
+            const int p = ptl[o];
+            const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+            const double2 z = reinterpret_cast<const double2*>(uv)[o];
+            const double uvo[2] = {z.x, z.y};
+            double r[2], Jc[2][D], Jp[2][3];
+            eval_obs<M, true>(camv, X, ppc, uvo, r, Jc, Jp);
+            const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+#pragma unroll
+            for (int a = 0; a < D; ++a) { row[a] = Jc[0][a] * sw; row[D + a] = Jc[1][a] * sw; }
+            row[2 * D] = r[0] * sw;
+            row[2 * D + 1] = r[1] * sw;
+        }
+        __syncthreads();
+        const int n = min(kThreads, ee - base);
+#pragma unroll
+        for (int m = 0; m < EPT; ++m) {
+            const int ent = t + m * kThreads;
+            if (ent < D * D) {
+                const int a = ent / D, b = ent % D;
+                double s = acc[m];
+                for (int i = 0; i < n; ++i) {
+                    const double* rw = sh + (size_t)i * RW;
+                    s += rw[a] * rw[b] + rw[D + a] * rw[D + b];
+                }
+                acc[m] = s;
+            } else if (ent < E) {
+                const int a = ent - D * D;
+                double s = acc[m];
+                for (int i = 0; i < n; ++i) {
+                    const double* rw = sh + (size_t)i * RW;
+                    s -= rw[a] * rw[2 * D] + rw[D + a] * rw[2 * D + 1];
+                }
+                acc[m] = s;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int m = 0; m < EPT; ++m) {
+        const int ent = t + m * kThreads;
+        if (ent < D * D) U[(size_t)c * D * D + ent] = acc[m];
+        else if (ent < E) gc[(size_t)c * D + (ent - D * D)] = acc[m];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// per-trial point preparation
+// ------------------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* __restrict__ V, const double* __restrict__ gp,
+                                                         double f, double cmin, double cmax, double* __restrict__ Vinv,
+                                                         double* __restrict__ y, int* __restrict__ flags) {
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= Pl) return;
+    double s[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[k] = V[6 * (size_t)p + k];
+    s[0] = clampd(s[0], cmin, cmax) * f;
+    s[3] = clampd(s[3], cmin, cmax) * f;
+    s[5] = clampd(s[5], cmin, cmax) * f;
+    double o[6];
+    if (!spd3_inverse(s, o)) {
+        atomicOr(flags, 1);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) Vinv[6 * (size_t)p + k] = o[k];
+    const double g0 = gp[3 * (size_t)p], g1 = gp[3 * (size_t)p + 1], g2 = gp[3 * (size_t)p + 2];
+    y[3 * (size_t)p + 0] = o[0] * g0 + o[1] * g1 + o[2] * g2;
+    y[3 * (size_t)p + 1] = o[1] * g0 + o[3] * g1 + o[4] * g2;
+    y[3 * (size_t)p + 2] = o[2] * g0 + o[4] * g1 + o[5] * g2;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Schur complement: one workgroup per (camera row i, chunk of its upper blocks).  The chunk of S's row lives in LDS;
+// each wave walks camera i's observations o (camera-major list), forms W^_o = W_o V_p^-1 per lane-entry, and for every
+// partner q of track p with camera j >= i in the chunk adds -W^_o W_q^T into slot(j).  Lane <-> block entry (a, b):
+// 64 lanes cover an 8x8 block.  WAVES = 1 gives a fixed accumulation order (deterministic mode).
+// ------------------------------------------------------------------------------------------------------------
+template <int D, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
+                                                      const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
+                                                      const int* __restrict__ cam_obs, const int* __restrict__ ptl,
+                                                      const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+                                                      const double* __restrict__ W, const double* __restrict__ Vinv,
+                                                      const double* __restrict__ y, const double* __restrict__ U,
+                                                      const double* __restrict__ gc, double f, double cmin, double cmax,
+                                                      int add_diag, double* __restrict__ S, double* __restrict__ b) {
+    constexpr int DD = D * D;
+    constexpr int ENT = (DD + 63) / 64;
+    constexpr int NT = WAVES * 64;
+    extern __shared__ __attribute__((aligned(16))) double sh[];
+    const int4 wk = work[blockIdx.x];
+    const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
+    double* acc = sh;
+    double* bacc = acc + (size_t)nb * DD;
+    int* slot = reinterpret_cast<int*>(bacc + D);
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    for (int k = t; k < nb * DD; k += NT) acc[k] = 0.0;
+    for (int k = t; k < C; k += NT) slot[k] = -1;
+    if (t < D) bacc[t] = 0.0;
+    __syncthreads();
+    for (int e = kb + t; e < ke; e += NT) slot[col[e]] = e - kb;
+    __syncthreads();
+    const bool diag_chunk = (kb == row_ptr[i]);
+    int ea[ENT], ebv[ENT];
+#pragma unroll
+    for (int m = 0; m < ENT; ++m) {
+        const int ent = lane + 64 * m;
+        ea[m] = ent < DD ? ent / D : 0;
+        ebv[m] = ent < DD ? ent % D : 0;
+    }
+    double breg = 0.0;
+    const int ob = cam_ptr[i], oe = cam_ptr[i + 1];
+    for (int e = ob + wv; e < oe; e += WAVES) {
+        const int o = cam_obs[e];
+        const int p = ptl[o];
+        const double* vi = Vinv + 6 * (size_t)p;
+        const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
+        const double* Wo = W + (size_t)o * D * 3;
+        double wh[ENT][3];
+#pragma unroll
+        for (int m = 0; m < ENT; ++m) {
+            const double w0 = Wo[ea[m] * 3 + 0], w1 = Wo[ea[m] * 3 + 1], w2 = Wo[ea[m] * 3 + 2];
+            wh[m][0] = w0 * v00 + w1 * v01 + w2 * v02;
+            wh[m][1] = w0 * v01 + w1 * v11 + w2 * v12;
+            wh[m][2] = w0 * v02 + w1 * v12 + w2 * v22;
+        }
+        if (diag_chunk && lane < D) {
+            const double* yp = y + 3 * (size_t)p;
+            breg -= Wo[lane * 3 + 0] * yp[0] + Wo[lane * 3 + 1] * yp[1] + Wo[lane * 3 + 2] * yp[2];
+        }
+        const int qb = pt_ptr[p], qe = pt_ptr[p + 1];
+        for (int q = qb; q < qe; ++q) {
+            const int j = cam[q];
+            if (j < i) continue;
+            const int s = slot[j];
+            if (s < 0) continue;
+            const double* Wq = W + (size_t)q * D * 3;
+            double* blk = acc + (size_t)s * DD;
+#pragma unroll
+            for (int m = 0; m < ENT; ++m) {
+                const int ent = lane + 64 * m;
+                if (ent < DD) {
+                    const double* wq = Wq + ebv[m] * 3;
+                    const double v = wh[m][0] * wq[0] + wh[m][1] * wq[1] + wh[m][2] * wq[2];
+                    if constexpr (WAVES == 1) blk[ent] -= v;
+                    else atomicAdd(blk + ent, -v);
+                }
+            }
+        }
+    }
+    if (diag_chunk && lane < D) {
+        if constexpr (WAVES == 1) bacc[lane] += breg;
+        else atomicAdd(bacc + lane, breg);
+    }
+    __syncthreads();
+    double* Sout = S + (size_t)kb * DD;
+    const double* Ui = U + (size_t)i * DD;
+    for (int k = t; k < nb * DD; k += NT) {
+        double v = acc[k];
+        if (diag_chunk && add_diag && k < DD) {
+            const int a = k / D, bb = k % D;
+            double u = Ui[k];
+            if (a == bb) u = clampd(u, cmin, cmax) * f;
+            v += u;
+        }
+        Sout[k] = v;
+    }
+    if (diag_chunk && t < D) b[(size_t)i * D + t] = (add_diag ? gc[(size_t)i * D + t] : 0.0) + bacc[t];
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// PCG on the reduced camera system
+// ------------------------------------------------------------------------------------------------------------
+struct CgBufs {
+    double* r[2];
+    double* w[2];
+    double* s[2];
+    double* p;
+    double* x;
+    double* part[2];  // [nwg][3]: gamma, delta, rho
+    double* hist;     // [maxit + 2][2]: alpha_i, gamma_i ; hist_bb at the end
+    int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
+};
+
+// One wave per camera: Cholesky S_ii = L L^T and L^-1 (lane 0 on an LDS copy), r0 = L^-1 b, zero p/x/s.
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, const double* __restrict__ S,
+                                                        const double* __restrict__ b, double* __restrict__ Lf,
+                                                        double* __restrict__ Li, CgBufs cg) {
+    constexpr int DD = D * D;
+    __shared__ double A[kWaves][DD];
+    __shared__ double L[kWaves][DD];
+    __shared__ double I[kWaves][DD];
+    __shared__ int bad[kWaves];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * kWaves + wv;
+    if (i >= C) return;
+    const double* blk = S + (size_t)row_ptr[i] * DD;
+    for (int k = lane; k < DD; k += 64) { A[wv][k] = blk[k]; L[wv][k] = 0.0; I[wv][k] = 0.0; }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (lane == 0) {
+        int ok = 1;
+        for (int r = 0; r < D && ok; ++r)
+            for (int c = 0; c <= r; ++c) {
+                double s = A[wv][r * D + c];
+                for (int k = 0; k < c; ++k) s -= L[wv][r * D + k] * L[wv][c * D + k];
+                if (r == c) {
+                    if (!(s > 0.0)) { ok = 0; break; }
+                    L[wv][r * D + r] = sqrt(s);
+                } else {
+                    L[wv][r * D + c] = s / L[wv][c * D + c];
+                }
+            }
+        if (ok) {
+            for (int r = 0; r < D; ++r) {
+                I[wv][r * D + r] = 1.0 / L[wv][r * D + r];
+                for (int c = 0; c < r; ++c) {
+                    double s = 0.0;
+                    for (int k = c; k < r; ++k) s -= L[wv][r * D + k] * I[wv][k * D + c];
+                    I[wv][r * D + c] = s / L[wv][r * D + r];
+                }
+            }
+        } else {
+            atomicMax(cg.status, 2);
+        }
+        bad[wv] = !ok;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < DD; k += 64) { Lf[(size_t)i * DD + k] = L[wv][k]; Li[(size_t)i * DD + k] = I[wv][k]; }
+    if (lane < D) {
+        const int a = lane;
+        double s = 0.0;
+        for (int k = 0; k <= a; ++k) s += I[wv][a * D + k] * b[(size_t)i * D + k];
+        const size_t idx = (size_t)i * D + a;
+        cg.r[0][idx] = bad[wv] ? 0.0 : s;
+        cg.r[1][idx] = 0.0;
+        cg.w[0][idx] = 0.0; cg.w[1][idx] = 0.0;
+        cg.s[0][idx] = 0.0; cg.s[1][idx] = 0.0;
+        cg.p[idx] = 0.0; cg.x[idx] = 0.0;
+    }
+}
+
+// One wave per upper block: S~_ij = L_i^-1 S_ij L_j^-T (diagonal blocks -> I).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __restrict__ blk_row, const int* __restrict__ col,
+                                                       const int* __restrict__ row_ptr, const double* __restrict__ Li,
+                                                       double* __restrict__ S) {
+    constexpr int DD = D * D;
+    __shared__ double T[kWaves][DD];
+    __shared__ double Sb[kWaves][DD];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int e = blockIdx.x * kWaves + wv;
+    if (e >= nnzb) return;
+    const int i = blk_row[e], j = col[e];
+    double* blk = S + (size_t)e * DD;
+    if (e == row_ptr[i]) {
+        for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
+        return;
+    }
+    const double* Lii = Li + (size_t)i * DD;
+    const double* Ljj = Li + (size_t)j * DD;
+    for (int k = lane; k < DD; k += 64) Sb[wv][k] = blk[k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < DD; k += 64) {
+        const int a = k / D, bb = k % D;
+        double s = 0.0;
+        for (int m = 0; m <= a; ++m) s += Lii[a * D + m] * Sb[wv][m * D + bb];
+        T[wv][k] = s;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k = lane; k < DD; k += 64) {
+        const int a = k / D, bb = k % D;
+        double s = 0.0;
+        for (int m = 0; m <= bb; ++m) s += T[wv][a * D + m] * Ljj[bb * D + m];
+        blk[k] = s;
+    }
+}
+
+// CG iteration kernel `it` (Chronopoulos-Gear on S~; diagonal blocks of S~ are I).  it = 0 computes w0 = S~ r0 and
+// the first dots.  it >= 1 performs recurrence step i = it-1: reads dots_i (partials of kernel it-1), decides
+// convergence on the true residual rho_i = ||L r~_i||^2 <= tol^2 ||b||^2, then per row
+//   p = r + beta p; s = w + beta s; x += alpha p; r' = r - alpha s; w' = S~ r'
+// where every neighbour's r'_j is recomputed from its previous-iteration (r, w, s) so that the whole iteration is
+// ONE launch.  Lane (g, col) of a wave handles column `col` of neighbour block g (D lanes per block, 64/D blocks
+// in flight per wave); the D row sums are butterfly-reduced across the wave.
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_iter(int it, int C, int nwg, int maxit, double tol2_rel,
+                                                      const int* __restrict__ row_ptr, const int* __restrict__ col,
+                                                      const int* __restrict__ lo_ptr, const int* __restrict__ lo_col,
+                                                      const int* __restrict__ lo_blk, const double* __restrict__ S,
+                                                      const double* __restrict__ Lf, CgBufs cg) {
+    constexpr int DD = D * D;
+    constexpr int NG = 64 / D;
+    __shared__ double red[3 * kThreads];
+    __shared__ double rsh[kWaves][D];
+    __shared__ double wpart[kWaves][3];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (cg.status[0] != 0) return;
+    double alpha = 0.0, beta = 0.0;
+    const int pin = (it + 1) & 1;  // parity of index it-1 (r_{it-1}, w_{it-1}, s_{it-1})
+    const int pout = it & 1;       // parity of index it   (r_it, w_it, s_{it-2} read, part_it)
+    if (it > 0) {
+        const int i = it - 1;
+        double d3[3];
+        sum_partials<3>(cg.part[pin], nwg, d3, red);
+        const double gam = d3[0], del = d3[1], rho = d3[2];
+        const double bb = (i == 0) ? rho : cg.hist[2 * (maxit + 1)];
+        if (rho <= tol2_rel * bb || i >= maxit) {
+            if (blockIdx.x == 0 && t == 0) { cg.status[0] = 1; cg.status[1] = i; }
+            return;
+        }
+        double den;
+        if (i == 0) { beta = 0.0; den = del; }
+        else {
+            const double alpha_prev = cg.hist[2 * (i - 1)], gam_prev = cg.hist[2 * (i - 1) + 1];
+            beta = gam / gam_prev;
+            den = del - beta * gam / alpha_prev;
+        }
+        if (!(den > 0.0)) {
+            if (blockIdx.x == 0 && t == 0) { cg.status[0] = 2; cg.status[1] = i; }
+            return;
+        }
+        alpha = gam / den;
+        if (blockIdx.x == 0 && t == 0) {
+            cg.hist[2 * i] = alpha;
+            cg.hist[2 * i + 1] = gam;
+            if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
+        }
+    }
+    const int row = blockIdx.x * kWaves + wv;
+    const double* r_old = cg.r[it == 0 ? 0 : pin];
+    const double* w_old = cg.w[pin];
+    const double* s_old = cg.s[pout];  // s_{it-2}
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (row < C) {
+        // own row update (lanes < D)
+        if (lane < D) {
+            const size_t idx = (size_t)row * D + lane;
+            double rn;
+            if (it == 0) {
+                rn = r_old[idx];
+            } else {
+                const double sn = w_old[idx] + beta * s_old[idx];
+                const double pn = r_old[idx] + beta * cg.p[idx];
+                cg.x[idx] += alpha * pn;
+                cg.p[idx] = pn;
+                cg.s[pin][idx] = sn;
+                rn = r_old[idx] - alpha * sn;
+                cg.r[pout][idx] = rn;
+            }
+            rsh[wv][lane] = rn;
+        }
+        // neighbour blocks
+        const int ub = row_ptr[row] + 1, ue = row_ptr[row + 1];
+        const int lb = lo_ptr[row], le = lo_ptr[row + 1];
+        const int nup = ue - ub, nbr = nup + (le - lb);
+        const int g = lane / D, cidx = lane % D;
+        double acc[D];
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[a] = 0.0;
+        if (g < NG) {
+            for (int n = g; n < nbr; n += NG) {
+                int blk, j;
+                const bool up = n < nup;
+                if (up) { blk = ub + n; j = col[blk]; }
+                else { const int k = lb + (n - nup); blk = lo_blk[k]; j = lo_col[k]; }
+                const size_t jx = (size_t)j * D + cidx;
+                const double rj = (it == 0) ? r_old[jx] : r_old[jx] - alpha * (w_old[jx] + beta * s_old[jx]);
+                const double* Sb = S + (size_t)blk * DD;
+                if (up) {
+#pragma unroll
+                    for (int a = 0; a < D; ++a) acc[a] += Sb[a * D + cidx] * rj;
+                } else {
+#pragma unroll
+                    for (int a = 0; a < D; ++a) acc[a] += Sb[cidx * D + a] * rj;
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[a] = wave_sum(acc[a]);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < D) {
+            const int a = lane;
+            double tot = acc[0];
+#pragma unroll
+            for (int k = 1; k < D; ++k) tot = (a == k) ? acc[k] : tot;
+            const double rn = rsh[wv][a];
+            const double wn = rn + tot;
+            const size_t idx = (size_t)row * D + a;
+            cg.w[pout][idx] = wn;
+            const double* L = Lf + (size_t)row * DD;
+            double lr = 0.0;
+            for (int k = 0; k <= a; ++k) lr += L[a * D + k] * rsh[wv][k];
+            g0 = rn * rn;
+            g1 = wn * rn;
+            g2 = lr * lr;
+        }
+    }
+    g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+    if (lane == 0) { wpart[wv][0] = g0; wpart[wv][1] = g1; wpart[wv][2] = g2; }
+    __syncthreads();
+    if (t == 0) {
+        double a0 = 0, a1 = 0, a2 = 0;
+        for (int k = 0; k < kWaves; ++k) { a0 += wpart[k][0]; a1 += wpart[k][1]; a2 += wpart[k][2]; }
+        double* pp = cg.part[pout] + 3 * (size_t)blockIdx.x;
+        pp[0] = a0; pp[1] = a1; pp[2] = a2;
+    }
+}
+
+// dc = L^-T x~
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __restrict__ Li, const double* __restrict__ xt,
+                                                        double* __restrict__ dc) {
+    const int k = blockIdx.x * kThreads + threadIdx.x;
+    if (k >= C * D) return;
+    const int i = k / D, a = k % D;
+    const double* L = Li + (size_t)i * D * D;
+    double s = 0.0;
+    for (int m = a; m < D; ++m) s += L[m * D + a] * xt[(size_t)i * D + m];
+    dc[k] = s;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// back-substitution, parameter update, cost
+// ------------------------------------------------------------------------------------------------------------
+// dp = V^-1 (g_p - sum_o W_o^T dc_c(o)); trial points; gain part  2 t.dp - dp^T V dp  (block partial).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_backsub(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+                                                      const double* __restrict__ W, const double* __restrict__ dc,
+                                                      const double* __restrict__ V, const double* __restrict__ Vinv,
+                                                      const double* __restrict__ gp, const double* __restrict__ pts,
+                                                      double* __restrict__ dp, double* __restrict__ pts_new,
+                                                      double* __restrict__ part) {
+    __shared__ double red[kThreads];
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    double gain[1] = {0.0};
+    if (p < Pl) {
+        double t0 = gp[3 * (size_t)p], t1 = gp[3 * (size_t)p + 1], t2 = gp[3 * (size_t)p + 2];
+        if (dc) {
+            for (int o = pt_ptr[p]; o < pt_ptr[p + 1]; ++o) {
+                const double* Wo = W + (size_t)o * D * 3;
+                const double* d = dc + (size_t)cam[o] * D;
+                double s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) {
+                    s0 += Wo[a * 3 + 0] * d[a];
+                    s1 += Wo[a * 3 + 1] * d[a];
+                    s2 += Wo[a * 3 + 2] * d[a];
+                }
+                t0 -= s0; t1 -= s1; t2 -= s2;
+            }
+        }
+        const double* vi = Vinv + 6 * (size_t)p;
+        const double d0 = vi[0] * t0 + vi[1] * t1 + vi[2] * t2;
+        const double d1 = vi[1] * t0 + vi[3] * t1 + vi[4] * t2;
+        const double d2 = vi[2] * t0 + vi[4] * t1 + vi[5] * t2;
+        dp[3 * (size_t)p] = d0; dp[3 * (size_t)p + 1] = d1; dp[3 * (size_t)p + 2] = d2;
+        pts_new[3 * (size_t)p] = pts[3 * (size_t)p] + d0;
+        pts_new[3 * (size_t)p + 1] = pts[3 * (size_t)p + 1] + d1;
+        pts_new[3 * (size_t)p + 2] = pts[3 * (size_t)p + 2] + d2;
+        const double* v = V + 6 * (size_t)p;
+        const double Vd0 = v[0] * d0 + v[1] * d1 + v[2] * d2;
+        const double Vd1 = v[1] * d0 + v[3] * d1 + v[4] * d2;
+        const double Vd2 = v[2] * d0 + v[4] * d1 + v[5] * d2;
+        gain[0] = 2.0 * (t0 * d0 + t1 * d1 + t2 * d2) - (d0 * Vd0 + d1 * Vd1 + d2 * Vd2);
+    }
+    block_sum<1>(gain, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
+}
+
+// Cameras: X <- Exp(dc_pose) X, intrinsics += dc_intr; gain part 2 g_c.dc - dc^T U dc (rank 0 only).
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_update_cams(int C, const double* __restrict__ cams, const double* __restrict__ dc,
+                                                          const double* __restrict__ U, const double* __restrict__ gc,
+                                                          int with_gain, double* __restrict__ cams_new,
+                                                          double* __restrict__ part) {
+    constexpr int D = kD<M>, ST = kStride<M>, NI = Model<M>::NI;
+    __shared__ double red[kThreads];
+    const int c = blockIdx.x * kThreads + threadIdx.x;
+    double gain[1] = {0.0};
+    if (c < C) {
+        const double* x = cams + (size_t)c * ST;
+        double* o = cams_new + (size_t)c * ST;
+        if (dc) {
+            const double* d = dc + (size_t)c * D;
+            retract_pose(x, d, o);
+#pragma unroll
+            for (int k = 0; k < NI; ++k) o[7 + k] = x[7 + k] + d[6 + k];
+            if (with_gain) {
+                const double* Uc = U + (size_t)c * D * D;
+                double quad = 0.0, lin = 0.0;
+                for (int a = 0; a < D; ++a) {
+                    double s = 0.0;
+                    for (int bb = 0; bb < D; ++bb) s += Uc[a * D + bb] * d[bb];
+                    quad += d[a] * s;
+                    lin += gc[(size_t)c * D + a] * d[a];
+                }
+                gain[0] = 2.0 * lin - quad;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < ST; ++k) o[k] = x[k];
+        }
+    }
+    block_sum<1>(gain, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
+}
+
+// Huber loss and sum ||r||^2 (block partials).
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
+                                                   const double* __restrict__ uv, const double* __restrict__ pp,
+                                                   const double* __restrict__ cams, const double* __restrict__ pts,
+                                                   double delta, double* __restrict__ part) {
+    constexpr int ST = kStride<M>;
+    __shared__ double red[2 * kThreads];
+    const int o = blockIdx.x * kThreads + threadIdx.x;
+    double v[2] = {0.0, 0.0};
+    if (o < Nl) {
+        const int c = cam[o], p = ptl[o];
+        const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+        const double2 z = reinterpret_cast<const double2*>(uv)[o];
+        const double uvo[2] = {z.x, z.y};
+        const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+        double r[2];
+        eval_obs<M, false>(cams + (size_t)c * ST, X, ppc, uvo, r, nullptr, nullptr);
+        const double s = r[0] * r[0] + r[1] * r[1];
+        const double rs = sqrt(s);
+        v[0] = rs < delta ? s : 2.0 * delta * rs - delta * delta;
+        v[1] = s;
+    }
+    block_sum<2>(v, red);
+    if (threadIdx.x == 0) { part[2 * (size_t)blockIdx.x] = v[0]; part[2 * (size_t)blockIdx.x + 1] = v[1]; }
+}
+
+// result[0..3] = {loss, sum ||r||^2, gain_points, gain_cams}; fixed-order sums of the partial arrays.
+__global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ cost_part, int ncost,
+                                                    const double* __restrict__ gp_part, int ngp,
+                                                    const double* __restrict__ gc_part, int ngc, double* __restrict__ result) {
+    __shared__ double red[2 * kThreads];
+    double c2[2];
+    sum_partials<2>(cost_part, ncost, c2, red);
+    double a[1], b[1];
+    if (gp_part) sum_partials<1>(gp_part, ngp, a, red); else a[0] = 0.0;
+    if (gc_part) sum_partials<1>(gc_part, ngc, b, red); else b[0] = 0.0;
+    if (threadIdx.x == 0) { result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0]; }
+}
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace
+
+// ============================================================================================================
+// host side
+// ============================================================================================================
+struct insfm_ba {
+    insfm_ba_desc d{};
+    int model = 0, ni = 0, D = 0, stride = 0;
+    int C = 0, P = 0, N = 0;
+    int p0 = 0, p1 = 0, Pl = 0, o0 = 0, Nl = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // structure (device)
+    double *uv = nullptr, *pp = nullptr;
+    int *cam = nullptr, *ptl = nullptr, *pt_ptr = nullptr, *cam_ptr = nullptr, *cam_obs = nullptr;
+    int *row_ptr = nullptr, *col = nullptr, *lo_ptr = nullptr, *lo_col = nullptr, *lo_blk = nullptr, *blk_row = nullptr;
+    int4* work = nullptr;
+    int nwork = 0, nnzb = 0, max_chunk = 0;
+    size_t schur_lds = 0;
+    // numeric (device)
+    double *W = nullptr, *V = nullptr, *gp = nullptr, *Vinv = nullptr, *y = nullptr, *dp = nullptr;
+    double *xbuf = nullptr;  // [S | b | U | gc | scal]
+    double *S = nullptr, *b = nullptr, *U = nullptr, *gc = nullptr, *scal = nullptr;
+    int64_t xcount = 0;
+    double *Lf = nullptr, *Li = nullptr, *dc = nullptr;
+    double* cgmem = nullptr;
+    CgBufs cg{};
+    int cg_nwg = 0;
+    double *cams_cur = nullptr, *cams_new = nullptr, *pts_cur = nullptr, *pts_new = nullptr;
+    double *part_cost = nullptr, *part_gp = nullptr, *part_gc = nullptr;
+    int n_cost = 0, n_gp = 0, n_gc = 0;
+    double* result = nullptr;
+    int* flags = nullptr;
+    double* host_res = nullptr;  // pinned 128 B: result[0..3] | flags (ints, slot 4-5) | cg status (ints, slot 8)
+    std::vector<void*> allocs;
+    // LM state
+    double damping = 0.0, down = 0.0, loss = 0.0;
+    bool have_loss = false;
+    int last_cg_iters = 16;
+    hipEvent_t ev[12]{};
+    bool timing = false;
+    // device time of the current step, accumulated per phase (ms): see insfm_ba_stats.time_ms
+    double tms[8]{};
+    int cg_launches = 0;
+};
+
+namespace {
+
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) {                                                                   \
+            h->err = std::string(#expr) + " failed: " + hipGetErrorString(e_);                    \
+            return INSFM_BA_EHIP;                                                                 \
+        }                                                                                         \
+    } while (0)
+
+int dalloc(insfm_ba* h, void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        h->err = std::string("hipMalloc(") + std::to_string(bytes) + ") failed: " + hipGetErrorString(e);
+        return INSFM_BA_ENOMEM;
+    }
+    h->allocs.push_back(*p);
+    return 0;
+}
+
+template <typename T>
+int upload(insfm_ba* h, T** dst, const T* src, size_t n) {
+    int rc = dalloc(h, (void**)dst, n * sizeof(T));
+    if (rc) return rc;
+    if (n) HIPCHK(hipMemcpyAsync(*dst, src, n * sizeof(T), hipMemcpyHostToDevice, h->stream));
+    return 0;
+}
+
+int model_ni(int m) {
+    switch (m) {
+        case 0: return 1; case 1: return 2; case 2: return 2; case 3: return 3; case 4: return 6;
+        case 5: return 6; case 6: return 10; case 8: return 2; case 9: return 3;
+        default: return -1;
+    }
+}
+
+// ---- model / D dispatch ----------------------------------------------------------------------------------------
+template <typename F>
+int with_model(int m, F&& f) {
+    switch (m) {
+        case 0: return f(std::integral_constant<int, 0>{});
+        case 1: return f(std::integral_constant<int, 1>{});
+        case 2: return f(std::integral_constant<int, 2>{});
+        case 3: return f(std::integral_constant<int, 3>{});
+        case 4: return f(std::integral_constant<int, 4>{});
+        case 5: return f(std::integral_constant<int, 5>{});
+        case 6: return f(std::integral_constant<int, 6>{});
+        case 8: return f(std::integral_constant<int, 8>{});
+        case 9: return f(std::integral_constant<int, 9>{});
+        default: return INSFM_BA_EINVAL;
+    }
+}
+template <typename F>
+int with_D(int D, F&& f) {
+    switch (D) {
+        case 7: return f(std::integral_constant<int, 7>{});
+        case 8: return f(std::integral_constant<int, 8>{});
+        case 9: return f(std::integral_constant<int, 9>{});
+        case 12: return f(std::integral_constant<int, 12>{});
+        case 16: return f(std::integral_constant<int, 16>{});
+        default: return INSFM_BA_EINVAL;
+    }
+}
+
+int launch_err(insfm_ba* h, const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        h->err = std::string(what) + ": " + hipGetErrorString(e);
+        return INSFM_BA_EHIP;
+    }
+    return 0;
+}
+
+int allreduce(insfm_ba* h, double* buf, int64_t n) {
+    if (h->d.world_size <= 1) return 0;
+    if (!h->d.allreduce) { h->err = "world_size > 1 needs an allreduce callback"; return INSFM_BA_ECOMM; }
+    int rc = h->d.allreduce(h->d.allreduce_ctx, buf, n);
+    if (rc) { h->err = "allreduce callback failed (" + std::to_string(rc) + ")"; return INSFM_BA_ECOMM; }
+    return 0;
+}
+
+void rec(insfm_ba* h, int k) {
+    if (h->timing) (void)hipEventRecord(h->ev[k], h->stream);
+}
+
+// after a stream sync: add the device time between events a and b to phase `slot`
+void acc_time(insfm_ba* h, int a, int b, int slot) {
+    if (!h->timing) return;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) == hipSuccess) h->tms[slot] += ms;
+}
+
+// ---- phases --------------------------------------------------------------------------------------------------
+int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
+    int rc = with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        constexpr int D = kD<M>;
+        if (h->Pl > 0)
+            k_lin_points<M><<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->uv, h->pp, cams,
+                                                                              pts_local, h->d.huber_delta, h->W, h->V, h->gp);
+        const size_t lds = sizeof(double) * kThreads * (2 * D + 2);
+        k_lin_cams<M><<<h->C, kThreads, lds, h->stream>>>(h->cam_ptr, h->cam_obs, h->ptl, h->uv, h->pp, cams, pts_local,
+                                                          h->d.huber_delta, h->U, h->gc);
+        return launch_err(h, "linearize");
+    });
+    if (rc) return rc;
+    return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
+}
+
+// Build S/b for factor f, solve, back-substitute and form the trial parameters.  Returns PCG iterations (>= 0),
+// INSFM_BA_ESOLVER on breakdown, or another negative code.
+int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
+    const int D = h->D;
+    HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
+    if (h->Pl > 0)
+        k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
+                                                                       h->Vinv, h->y, h->flags);
+    int iters = 0;
+    const double* dcp = nullptr;
+    if (h->d.optimize_poses) {
+        rec(h, 6);
+        int rc = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            if (h->d.deterministic)
+                k_schur<DV, 1><<<h->nwork, 64, h->schur_lds, h->stream>>>(
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->cam, h->W, h->Vinv, h->y,
+                    h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+            else
+                k_schur<DV, 4><<<h->nwork, 256, h->schur_lds, h->stream>>>(
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->cam, h->W, h->Vinv, h->y,
+                    h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+            return launch_err(h, "k_schur");
+        });
+        if (rc) return rc;
+        rec(h, 7);
+        rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
+        if (rc) return rc;
+        HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+        rc = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg);
+            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr, h->Li, h->S);
+            return launch_err(h, "k_cg_factor/scale");
+        });
+        if (rc) return rc;
+        const int maxit = h->d.pcg_max_iter;
+        const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
+        int it = 0;
+        int* st = reinterpret_cast<int*>(h->host_res + 8);
+        for (;;) {
+            const int chunk = (it == 0) ? std::max(8, h->last_cg_iters + 2) : 8;
+            const int stop = std::min(it + chunk, maxit + 2);
+            const int first = it;
+            rec(h, 8);
+            rc = with_D(D, [&](auto dc_) -> int {
+                constexpr int DV = decltype(dc_)::value;
+                for (int k = it; k < stop; ++k)
+                    k_cg_iter<DV><<<h->cg_nwg, kThreads, 0, h->stream>>>(k, h->C, h->cg_nwg, maxit, tol2, h->row_ptr, h->col,
+                                                                       h->lo_ptr, h->lo_col, h->lo_blk, h->S, h->Lf, h->cg);
+                return launch_err(h, "k_cg_iter");
+            });
+            if (rc) return rc;
+            rec(h, 9);
+            it = stop;
+            HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            acc_time(h, 8, 9, 5);
+            h->cg_launches += stop - first;
+            if (st[0] != 0 || it >= maxit + 2) break;
+        }
+        if (st[0] != 1) return INSFM_BA_ESOLVER;
+        iters = st[1];
+        h->last_cg_iters = iters;
+        rc = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x, h->dc);
+            return launch_err(h, "k_cg_finish");
+        });
+        if (rc) return rc;
+        dcp = h->dc;
+    }
+    rec(h, 3);
+    int rc = with_D(D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        if (h->Pl > 0)
+            k_backsub<DV><<<h->n_gp, kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->W, dcp, h->V, h->Vinv, h->gp,
+                                                               pts_local, h->dp, h->pts_new, h->part_gp);
+        return launch_err(h, "k_backsub");
+    });
+    if (rc) return rc;
+    rc = with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        k_update_cams<M><<<h->n_gc, kThreads, 0, h->stream>>>(h->C, cams, dcp, h->U, h->gc, h->d.rank == 0, h->cams_new,
+                                                               h->part_gc);
+        return launch_err(h, "k_update_cams");
+    });
+    if (rc) return rc;
+    return iters;
+}
+
+// cost at (cams, pts_local) -> h->result[0..1]; with gain partials when `gains` (after a solve).
+int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gains) {
+    int rc = with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        if (h->Nl > 0)
+            k_cost<M><<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
+                                                             h->d.huber_delta, h->part_cost);
+        k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
+                                               h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->result);
+        return launch_err(h, "k_cost/k_final");
+    });
+    if (rc) return rc;
+    rc = allreduce(h, h->result, 4);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(h->host_res + 4, h->flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+}  // namespace
+
+// ============================================================================================================
+// C ABI
+// ============================================================================================================
+extern "C" {
+
+void insfm_ba_default_desc(insfm_ba_desc* d) {
+    std::memset(d, 0, sizeof(*d));
+    d->cam_model = 2;
+    d->optimize_poses = 1;
+    d->deterministic = 0;
+    d->huber_delta = 1.0;
+    d->tr_radius = 1e4; d->tr_max = 1e10; d->tr_min = 1e-6; d->tr_up = 2.0; d->tr_down = 1.0 / 16.0;
+    d->tr_factor = 0.5; d->tr_high = 0.5; d->tr_low = 1e-3;
+    d->clamp_min = 1e-6; d->clamp_max = 1e32;
+    d->max_rejects = 30;
+    d->pcg_max_iter = 500;
+    d->pcg_tol = 1e-5;
+    d->world_size = 1; d->rank = 0;
+    d->shard_point_begin = 0; d->shard_point_end = -1;
+}
+
+const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() : "null handle"; }
+
+void insfm_ba_destroy(insfm_ba* h) {
+    if (!h) return;
+    for (void* p : h->allocs) (void)hipFree(p);
+    if (h->host_res) (void)hipHostFree(h->host_res);
+    for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete h;
+}
+
+int64_t insfm_ba_nnzb(const insfm_ba* h) { return h ? h->nnzb : -1; }
+
+int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32_t* cam_idx, const int32_t* pt_idx,
+                    const double* pp, void* stream, insfm_ba** out) {
+    if (!desc || !out) return INSFM_BA_EINVAL;
+    *out = nullptr;
+    insfm_ba* h = new insfm_ba();
+    h->d = *desc;
+    h->stream = reinterpret_cast<hipStream_t>(stream);
+    auto fail = [&](int rc, const std::string& msg) {
+        if (!msg.empty()) h->err = msg;
+        *out = h;  // handle returned so the caller can read the error; caller destroys it
+        return rc;
+    };
+    h->model = desc->cam_model;
+    h->ni = model_ni(h->model);
+    if (h->ni < 0) return fail(INSFM_BA_EINVAL, "unsupported camera model " + std::to_string(h->model));
+    h->D = 6 + h->ni;
+    h->stride = 7 + h->ni;
+    h->C = desc->n_cams; h->P = desc->n_points; h->N = desc->n_obs;
+    if (h->C <= 0 || h->P <= 0 || h->N < 0) return fail(INSFM_BA_EINVAL, "empty problem");
+    if (!obs_uv || !cam_idx || !pt_idx || !pp) return fail(INSFM_BA_EINVAL, "null input pointer");
+    if (desc->world_size < 1 || desc->rank < 0 || desc->rank >= desc->world_size) return fail(INSFM_BA_EINVAL, "bad rank");
+    if (desc->world_size > 1 && !desc->allreduce) return fail(INSFM_BA_EINVAL, "world_size > 1 needs allreduce");
+    if (h->C > 30000) return fail(INSFM_BA_EINVAL, "n_cams > 30000 not supported (LDS slot table)");
+    const int C = h->C, P = h->P, N = h->N, D = h->D;
+    for (int i = 0; i < N; ++i) {
+        if (cam_idx[i] < 0 || cam_idx[i] >= C) return fail(INSFM_BA_EINVAL, "cam_idx out of range");
+        if (pt_idx[i] < 0 || pt_idx[i] >= P) return fail(INSFM_BA_EINVAL, "pt_idx out of range");
+        if (i && pt_idx[i] < pt_idx[i - 1]) return fail(INSFM_BA_EINVAL, "observations must be track-major (pt_idx nondecreasing)");
+    }
+    h->p0 = std::max(0, desc->shard_point_begin);
+    h->p1 = desc->shard_point_end < 0 ? P : std::min(P, desc->shard_point_end);
+    if (h->p1 < h->p0) return fail(INSFM_BA_EINVAL, "bad shard range");
+    h->Pl = h->p1 - h->p0;
+    // global track pointers
+    std::vector<int> gptr(P + 1, 0);
+    for (int i = 0; i < N; ++i) gptr[pt_idx[i] + 1]++;
+    for (int p = 0; p < P; ++p) gptr[p + 1] += gptr[p];
+    h->o0 = gptr[h->p0];
+    h->Nl = gptr[h->p1] - h->o0;
+    const int o0 = h->o0, Nl = h->Nl, Pl = h->Pl;
+    // local arrays
+    std::vector<int> lptr(Pl + 1), lptl(Nl), lcam(Nl);
+    for (int p = 0; p <= Pl; ++p) lptr[p] = gptr[h->p0 + p] - o0;
+    for (int o = 0; o < Nl; ++o) { lptl[o] = pt_idx[o0 + o] - h->p0; lcam[o] = cam_idx[o0 + o]; }
+    std::vector<int> cptr(C + 1, 0), cobs(Nl);
+    for (int o = 0; o < Nl; ++o) cptr[lcam[o] + 1]++;
+    for (int c = 0; c < C; ++c) cptr[c + 1] += cptr[c];
+    {
+        std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+        for (int o = 0; o < Nl; ++o) cobs[fill[lcam[o]]++] = o;
+    }
+    // global upper pattern (identical on every rank)
+    std::vector<int> gcptr(C + 1, 0), gcobs(N);
+    for (int i = 0; i < N; ++i) gcptr[cam_idx[i] + 1]++;
+    for (int c = 0; c < C; ++c) gcptr[c + 1] += gcptr[c];
+    {
+        std::vector<int> fill(gcptr.begin(), gcptr.end() - 1);
+        for (int i = 0; i < N; ++i) gcobs[fill[cam_idx[i]]++] = i;
+    }
+    std::vector<int> rptr(C + 1, 0), cols;
+    cols.reserve((size_t)C * 8);
+    {
+        std::vector<int> mark(C, -1), buf;
+        for (int i = 0; i < C; ++i) {
+            buf.clear();
+            buf.push_back(i);
+            mark[i] = i;
+            for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
+                const int p = pt_idx[gcobs[e]];
+                for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
+                    const int j = cam_idx[q];
+                    if (j > i && mark[j] != i) { mark[j] = i; buf.push_back(j); }
+                }
+            }
+            std::sort(buf.begin(), buf.end());
+            cols.insert(cols.end(), buf.begin(), buf.end());
+            rptr[i + 1] = (int)cols.size();
+        }
+    }
+    h->nnzb = rptr[C];
+    std::vector<int> brow(h->nnzb);
+    for (int i = 0; i < C; ++i)
+        for (int e = rptr[i]; e < rptr[i + 1]; ++e) brow[e] = i;
+    std::vector<int> lop(C + 1, 0);
+    for (int i = 0; i < C; ++i)
+        for (int e = rptr[i] + 1; e < rptr[i + 1]; ++e) lop[cols[e] + 1]++;
+    for (int c = 0; c < C; ++c) lop[c + 1] += lop[c];
+    std::vector<int> locol(std::max(1, lop[C])), loblk(std::max(1, lop[C]));
+    {
+        std::vector<int> fill(lop.begin(), lop.end() - 1);
+        for (int i = 0; i < C; ++i)
+            for (int e = rptr[i] + 1; e < rptr[i + 1]; ++e) {
+                const int k = fill[cols[e]]++;
+                locol[k] = i;
+                loblk[k] = e;
+            }
+    }
+    // Schur work items: split long rows so a chunk fits the LDS budget
+    const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + 64;
+    if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
+    const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * D * D));
+    std::vector<int4> work;
+    int maxc = 1;
+    for (int i = 0; i < C; ++i) {
+        if (gcptr[i + 1] == gcptr[i] && rptr[i + 1] - rptr[i] == 1) {
+            work.push_back(make_int4(i, rptr[i], rptr[i + 1], 0));
+            continue;
+        }
+        for (int kb = rptr[i]; kb < rptr[i + 1]; kb += cap) {
+            const int ke = std::min(kb + cap, rptr[i + 1]);
+            work.push_back(make_int4(i, kb, ke, 0));
+            maxc = std::max(maxc, ke - kb);
+        }
+    }
+    h->nwork = (int)work.size();
+    h->max_chunk = maxc;
+    h->schur_lds = sizeof(double) * ((size_t)maxc * D * D + D) + sizeof(int) * (size_t)C;
+    h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
+
+    int rc;
+    std::vector<double> uvl((size_t)2 * Nl);
+    std::memcpy(uvl.data(), obs_uv + 2 * (size_t)o0, sizeof(double) * 2 * Nl);
+    if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->pp, pp, (size_t)2 * C))) return fail(rc, "");
+    if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->ptl, lptl.data(), lptl.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->cam_ptr, cptr.data(), cptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->cam_obs, cobs.data(), cobs.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->row_ptr, rptr.data(), rptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->col, cols.data(), cols.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->blk_row, brow.data(), brow.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->lo_ptr, lop.data(), lop.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->lo_col, locol.data(), locol.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->lo_blk, loblk.data(), loblk.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
+    auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
+    if ((rc = dd(&h->W, (size_t)Nl * D * 3))) return fail(rc, "");
+    if ((rc = dd(&h->V, (size_t)Pl * 6))) return fail(rc, "");
+    if ((rc = dd(&h->gp, (size_t)Pl * 3))) return fail(rc, "");
+    if ((rc = dd(&h->Vinv, (size_t)Pl * 6))) return fail(rc, "");
+    if ((rc = dd(&h->y, (size_t)Pl * 3))) return fail(rc, "");
+    if ((rc = dd(&h->dp, (size_t)Pl * 3))) return fail(rc, "");
+    h->xcount = (int64_t)h->nnzb * D * D + (int64_t)C * D + (int64_t)C * D * D + (int64_t)C * D + 8;
+    if ((rc = dd(&h->xbuf, (size_t)h->xcount))) return fail(rc, "");
+    h->S = h->xbuf;
+    h->b = h->S + (size_t)h->nnzb * D * D;
+    h->U = h->b + (size_t)C * D;
+    h->gc = h->U + (size_t)C * D * D;
+    h->scal = h->gc + (size_t)C * D;
+    if ((rc = dd(&h->Lf, (size_t)C * D * D))) return fail(rc, "");
+    if ((rc = dd(&h->Li, (size_t)C * D * D))) return fail(rc, "");
+    if ((rc = dd(&h->dc, (size_t)C * D))) return fail(rc, "");
+    h->cg_nwg = cdiv(C, kWaves);
+    const size_t cd = (size_t)C * D;
+    const size_t cgn = 8 * cd + 2 * 3 * (size_t)h->cg_nwg + 2 * ((size_t)desc->pcg_max_iter + 2) + 8;
+    if ((rc = dd(&h->cgmem, cgn))) return fail(rc, "");
+    {
+        double* m = h->cgmem;
+        h->cg.r[0] = m; m += cd; h->cg.r[1] = m; m += cd;
+        h->cg.w[0] = m; m += cd; h->cg.w[1] = m; m += cd;
+        h->cg.s[0] = m; m += cd; h->cg.s[1] = m; m += cd;
+        h->cg.p = m; m += cd; h->cg.x = m; m += cd;
+        h->cg.part[0] = m; m += 3 * (size_t)h->cg_nwg; h->cg.part[1] = m; m += 3 * (size_t)h->cg_nwg;
+        h->cg.hist = m; m += 2 * ((size_t)desc->pcg_max_iter + 2);
+    }
+    if ((rc = dalloc(h, (void**)&h->cg.status, sizeof(int) * 4))) return fail(rc, "");
+    const int ST = h->stride;
+    if ((rc = dd(&h->cams_cur, (size_t)C * ST))) return fail(rc, "");
+    if ((rc = dd(&h->cams_new, (size_t)C * ST))) return fail(rc, "");
+    if ((rc = dd(&h->pts_cur, (size_t)std::max(Pl, 1) * 3))) return fail(rc, "");
+    if ((rc = dd(&h->pts_new, (size_t)std::max(Pl, 1) * 3))) return fail(rc, "");
+    h->n_cost = std::max(1, cdiv(Nl, kThreads));
+    h->n_gp = std::max(1, cdiv(Pl, kThreads));
+    h->n_gc = std::max(1, cdiv(C, kThreads));
+    if ((rc = dd(&h->part_cost, 2 * (size_t)h->n_cost))) return fail(rc, "");
+    if ((rc = dd(&h->part_gp, (size_t)h->n_gp))) return fail(rc, "");
+    if ((rc = dd(&h->part_gc, (size_t)h->n_gc))) return fail(rc, "");
+    h->result = h->scal;  // the 4 result scalars are all-reduced in place with the exchange buffer
+    if ((rc = dalloc(h, (void**)&h->flags, sizeof(int) * 4))) return fail(rc, "");
+    {
+        hipError_t e = hipHostMalloc((void**)&h->host_res, 128, hipHostMallocDefault);
+        if (e != hipSuccess) return fail(INSFM_BA_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    for (auto& e : h->ev) {
+        hipError_t x = hipEventCreate(&e);
+        if (x != hipSuccess) return fail(INSFM_BA_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(x));
+    }
+    {
+        hipError_t e = hipMemsetAsync(h->part_gp, 0, sizeof(double) * h->n_gp, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->part_gc, 0, sizeof(double) * h->n_gc, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("init: ") + hipGetErrorString(e));
+    }
+    // the Schur kernels may need more than the default dynamic-LDS limit
+    with_D(D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
+        return 0;
+    });
+    h->damping = 1.0 / desc->tr_radius;
+    h->down = desc->tr_down;
+    *out = h;
+    return INSFM_BA_OK;
+}
+
+int64_t insfm_ba_exchange_count(const insfm_ba* h) { return h ? h->xcount : -1; }
+
+int insfm_ba_set_exchange(insfm_ba* h, double* buf, int64_t count) {
+    if (!h || !buf || count < h->xcount) return INSFM_BA_EINVAL;
+    const int C = h->C, D = h->D;
+    h->xbuf = buf;
+    h->S = h->xbuf;
+    h->b = h->S + (size_t)h->nnzb * D * D;
+    h->U = h->b + (size_t)C * D;
+    h->gc = h->U + (size_t)C * D * D;
+    h->scal = h->gc + (size_t)C * D;
+    h->result = h->scal;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_reset(insfm_ba* h) {
+    if (!h) return INSFM_BA_EINVAL;
+    h->damping = 1.0 / h->d.tr_radius;
+    h->down = h->d.tr_down;
+    h->have_loss = false;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* loss, double* rmse) {
+    if (!h || !cams || !pts) return INSFM_BA_EINVAL;
+    int rc = run_cost(h, cams, pts + 3 * (size_t)h->p0, false);
+    if (rc) return rc;
+    if (loss) *loss = h->host_res[0];
+    if (rmse) *rmse = h->N > 0 ? std::sqrt(h->host_res[1] / h->N) : 0.0;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_stats* st) {
+    if (!h || !cams_user || !pts_user) return INSFM_BA_EINVAL;
+    const int C = h->C, ST = h->stride;
+    const size_t cam_bytes = sizeof(double) * (size_t)C * ST;
+    const size_t pt_bytes = sizeof(double) * (size_t)h->Pl * 3;
+    h->timing = st != nullptr;
+    for (auto& v : h->tms) v = 0.0;
+    h->cg_launches = 0;
+    HIPCHK(hipMemcpyAsync(h->cams_cur, cams_user, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
+    if (pt_bytes) HIPCHK(hipMemcpyAsync(h->pts_cur, pts_user + 3 * (size_t)h->p0, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
+    int rc;
+    if (!h->have_loss) {
+        if ((rc = run_cost(h, h->cams_cur, h->pts_cur, false))) return rc;
+        h->loss = h->host_res[0];
+        h->have_loss = true;
+    }
+    const double last = h->loss;
+    rec(h, 0);
+    if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
+    rec(h, 1);
+    double f = 1.0;
+    int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
+    for (;;) {
+        f *= (1.0 + h->damping);
+        ++trials;
+        const int it = run_solve(h, f, h->cams_cur, h->pts_cur);
+        if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
+        if (it < 0) return it;
+        rec(h, 4);
+        if ((rc = run_cost(h, h->cams_new, h->pts_new, true))) return rc;  // synchronizes
+        rec(h, 5);
+        if (h->timing) {
+            (void)hipEventSynchronize(h->ev[5]);
+            if (trials == 1) acc_time(h, 0, 1, 0);
+            if (h->d.optimize_poses) {
+                acc_time(h, 6, 7, 1);
+                acc_time(h, 1, 3, 2);
+            }
+            acc_time(h, 3, 4, 3);
+            acc_time(h, 4, 5, 4);
+            rec(h, 1);  // the next trial starts here
+        }
+        const int* flags = reinterpret_cast<const int*>(h->host_res + 4);
+        if (flags[0]) { failed = 1; h->loss = last; break; }
+        pcg_last = it;
+        pcg_total += it;
+        const double loss_new = h->host_res[0];
+        const double denom = h->host_res[2] + h->host_res[3];
+        const double quality = (last - loss_new) / denom;
+        double radius = 1.0 / h->damping;
+        if (quality > h->d.tr_high) { radius = h->d.tr_up * radius; h->down = h->d.tr_down; }
+        else if (quality > h->d.tr_low) { h->down = h->d.tr_down; }
+        else { radius = radius * h->down; h->down = h->down * h->d.tr_factor; }
+        radius = std::min(std::max(radius, h->d.tr_min), h->d.tr_max);
+        h->damping = 1.0 / radius;
+        if (last < loss_new && rejects < h->d.max_rejects) {
+            ++rejects;
+            h->loss = last;
+            continue;
+        }
+        std::swap(h->cams_cur, h->cams_new);
+        std::swap(h->pts_cur, h->pts_new);
+        h->loss = loss_new;
+        break;
+    }
+    HIPCHK(hipMemcpyAsync(cams_user, h->cams_cur, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
+    if (pt_bytes) HIPCHK(hipMemcpyAsync(pts_user + 3 * (size_t)h->p0, h->pts_cur, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (st) {
+        st->loss = h->loss;
+        st->loss_before = last;
+        st->damping = h->damping;
+        st->trials = trials;
+        st->rejects = rejects;
+        st->pcg_iters_last = pcg_last;
+        st->pcg_iters_total = pcg_total;
+        st->solver_failed = failed;
+        for (int k = 0; k < 8; ++k) st->time_ms[k] = h->tms[k];
+        st->cg_launches = h->cg_launches;
+    }
+    h->timing = false;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts) {
+    if (!h || !cams || !pts) return INSFM_BA_EINVAL;
+    HIPCHK(hipMemcpyAsync(h->cams_cur, cams, sizeof(double) * (size_t)h->C * h->stride, hipMemcpyDeviceToDevice, h->stream));
+    if (h->Pl)
+        HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * (size_t)h->Pl * 3, hipMemcpyDeviceToDevice,
+                              h->stream));
+    int rc = run_linearize(h, h->cams_cur, h->pts_cur);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int insfm_ba_debug_solve(insfm_ba* h, double f) {
+    if (!h) return INSFM_BA_EINVAL;
+    // solves around the parameters last passed to insfm_ba_debug_linearize
+    int it = run_solve(h, f, h->cams_cur, h->pts_cur);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return it;
+}
+
+int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
+    if (!h || !host) return INSFM_BA_EINVAL;
+    const size_t C = h->C, Pl = h->Pl, Nl = h->Nl, D = h->D;
+    const double* src = nullptr;
+    size_t n = 0;
+    switch (which) {
+        case 0: src = h->W; n = Nl * D * 3; break;
+        case 1: src = h->V; n = Pl * 6; break;
+        case 2: src = h->gp; n = Pl * 3; break;
+        case 3: src = h->U; n = C * D * D; break;
+        case 4: src = h->gc; n = C * D; break;
+        case 5: src = h->S; n = (size_t)h->nnzb * D * D; break;
+        case 6: src = h->b; n = C * D; break;
+        case 7: src = h->dc; n = C * D; break;
+        case 8: src = h->dp; n = Pl * 3; break;
+        default: return INSFM_BA_EINVAL;
+    }
+    HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return (int64_t)n;
+}
+
+}  // extern "C"

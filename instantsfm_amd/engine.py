@@ -1,0 +1,145 @@
+"""LM engine bound to one packed BA problem -- the replacement for
+``bae.optim.LM(model, strategy=TrustRegion(...), solver=PCG(tol=1e-5), kernel=Huber(thres), reject=30)``
+(instantsfm/processors/bundle_adjustment.py:115-119) and its ``step(input)`` (:132).
+
+All arithmetic runs in the HIP library (libinsfm_ba.so) through the C ABI of include/insfm_ba.h; torch ROCm tensors
+only hold device memory and provide the stream / torch.distributed plumbing.  There is no CPU path.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _capi
+
+# TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.
+LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4, tr_factor=0.5,
+                   tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, max_rejects=30, pcg_tol=1e-5,
+                   pcg_max_iter=500)
+
+
+def _require_gpu(device):
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError(f"insfm_ba runs on an MI355X (ROCm 'cuda' device); got device={device!r}. There is no CPU path.")
+    if not torch.cuda.is_available():
+        raise RuntimeError("insfm_ba: no ROCm GPU visible (torch.cuda.is_available() is False); there is no CPU fallback")
+    return dev
+
+
+class BundleAdjuster:
+    """One LM problem on one GPU (or one track shard of it)."""
+
+    def __init__(self, model, uv, cam_idx, pt_idx, pp, n_cams, n_points, device="cuda:0", optimize_poses=True,
+                 huber_delta=1.0, deterministic=False, world_size=1, rank=0, shard=None, process_group=None, **lm):
+        self.device = _require_gpu(device)
+        L = _capi.load()
+        opts = dict(LM_DEFAULTS, **lm)
+        uv = np.ascontiguousarray(uv, dtype=np.float64).reshape(-1, 2)
+        cam_idx = np.ascontiguousarray(cam_idx, dtype=np.int32).reshape(-1)
+        pt_idx = np.ascontiguousarray(pt_idx, dtype=np.int32).reshape(-1)
+        pp = np.ascontiguousarray(pp, dtype=np.float64).reshape(-1, 2)
+        d = _capi.default_desc()
+        d.n_cams, d.n_points, d.n_obs = int(n_cams), int(n_points), int(uv.shape[0])
+        d.cam_model = int(model)
+        d.optimize_poses = int(bool(optimize_poses))
+        d.deterministic = int(bool(deterministic))
+        d.huber_delta = float(huber_delta)
+        for k, v in opts.items():
+            setattr(d, k, type(getattr(d, k))(v))
+        d.world_size, d.rank = int(world_size), int(rank)
+        d.shard_point_begin, d.shard_point_end = (0, -1) if shard is None else (int(shard[0]), int(shard[1]))
+        self._xbuf = None
+        self._cb = None
+        if world_size > 1:
+            import torch.distributed as dist
+            group = process_group
+
+            def _allreduce(ctx, ptr, count):
+                try:
+                    base = self._xbuf.data_ptr()
+                    off = (ctypes.cast(ptr, ctypes.c_void_p).value - base) // 8
+                    dist.all_reduce(self._xbuf[off:off + count], op=dist.ReduceOp.SUM, group=group)
+                    return 0
+                except Exception as e:  # pragma: no cover - surfaced as INSFM_BA_ECOMM
+                    self._cb_error = e
+                    return -1
+            self._cb = _capi.ALLREDUCE_FN(_allreduce)
+            d.allreduce = self._cb
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        h = ctypes.c_void_p()
+        rc = L.insfm_ba_create(ctypes.byref(d), uv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                               cam_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                               pt_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                               pp.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.c_void_p(stream), ctypes.byref(h))
+        if rc != 0:
+            msg = L.insfm_ba_last_error(h).decode() if h.value else ""
+            if h.value:
+                L.insfm_ba_destroy(h)
+            raise _capi.BAError(rc, msg)
+        self._h = h
+        self.desc = d
+        self.n_cams, self.n_points, self.n_obs = d.n_cams, d.n_points, d.n_obs
+        self.D = 6 + {0: 1, 1: 2, 2: 2, 3: 3, 4: 6, 5: 6, 6: 10, 8: 2, 9: 3}[int(model)]
+        if world_size > 1:
+            n = L.insfm_ba_exchange_count(h)
+            self._xbuf = torch.zeros(int(n), dtype=torch.float64, device=self.device)
+            _capi.check(h, L.insfm_ba_set_exchange(h, ctypes.c_void_p(self._xbuf.data_ptr()), n))
+
+    # ------------------------------------------------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _capi.load().insfm_ba_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _ptr(self, t, shape):
+        if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()):
+            raise ValueError("parameters must be contiguous float64 tensors on the GPU")
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
+        return ctypes.c_void_p(t.data_ptr())
+
+    def step(self, cam_params, points):
+        """One LM step; updates ``cam_params`` [C, 7+ni] and ``points`` [P, 3] in place.  Returns (loss, stats)."""
+        st = _capi.Stats()
+        L = _capi.load()
+        rc = L.insfm_ba_step(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)), self._ptr(points, (self.n_points, 3)),
+                             ctypes.byref(st))
+        _capi.check(self._h, rc)
+        return st.loss, st.as_dict()
+
+    def cost(self, cam_params, points):
+        loss, rmse = ctypes.c_double(), ctypes.c_double()
+        L = _capi.load()
+        _capi.check(self._h, L.insfm_ba_cost(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)),
+                                             self._ptr(points, (self.n_points, 3)), ctypes.byref(loss), ctypes.byref(rmse)))
+        return loss.value, rmse.value
+
+    def reset(self):
+        _capi.check(self._h, _capi.load().insfm_ba_reset(self._h))
+
+    # ---- parity introspection -----------------------------------------------------------------------------------
+    def debug_linearize(self, cam_params, points):
+        L = _capi.load()
+        _capi.check(self._h, L.insfm_ba_debug_linearize(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)),
+                                                        self._ptr(points, (self.n_points, 3))))
+
+    def debug_solve(self, f):
+        return _capi.check(self._h, _capi.load().insfm_ba_debug_solve(self._h, float(f)))
+
+    def nnzb(self):
+        return int(_capi.load().insfm_ba_nnzb(self._h))
+
+    def debug_get(self, which, shape):
+        out = np.zeros(shape, dtype=np.float64)
+        n = _capi.load().insfm_ba_debug_get(self._h, int(which), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        _capi.check(self._h, n)
+        assert n == out.size, (n, out.shape)
+        return out

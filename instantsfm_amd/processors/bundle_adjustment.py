@@ -1,0 +1,205 @@
+"""TorchBA -- drop-in for ``instantsfm/processors/bundle_adjustment.py`` (reference :1-154).
+
+Same constructor and ``Solve(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)`` signature, same filters, ordering,
+stop rule and in-place write-back; the LM engine underneath is the MI355X HIP library (``engine.BundleAdjuster``)
+instead of bae/pypose.  Packing (reference :66-113, a Python double loop over tracks x observations) is vectorized.
+"""
+import numpy as np
+import torch
+
+from ..engine import BundleAdjuster
+from ..scene.defs import CameraModelId, IMPLEMENTED_MODELS, get_camera_model_info
+
+
+def _quat_xyzw_from_matrix(R):
+    """pp.mat2SE3 rotation part: rotation matrix -> quaternion [x, y, z, w] (sign: w >= 0)."""
+    from scipy.spatial.transform import Rotation
+    q = Rotation.from_matrix(np.asarray(R, dtype=np.float64)).as_quat()
+    return -q if q[3] < 0 else q
+
+
+def _pose_matrices(cam_rows):
+    """pp.SE3(rows[:, :7]).matrix(): the 4x4 of the action p -> p + 2w(q x p) + 2 q x (q x p) + t."""
+    t = cam_rows[:, 0:3]
+    qx, qy, qz, w = (cam_rows[:, 3 + k] for k in range(4))
+    n = cam_rows.shape[0]
+    K = np.zeros((n, 3, 3))
+    K[:, 0, 1], K[:, 0, 2] = -qz, qy
+    K[:, 1, 0], K[:, 1, 2] = qz, -qx
+    K[:, 2, 0], K[:, 2, 1] = -qy, qx
+    M = np.eye(4)[None].repeat(n, axis=0)
+    M[:, :3, :3] = np.eye(3)[None] + 2.0 * w[:, None, None] * K + 2.0 * K @ K
+    M[:, :3, 3] = t
+    return M
+
+
+def _as_torch_like_params(params):
+    """``torch.tensor(cameras[id].params)`` (reference :71-72): a Python list of floats becomes float32 in torch
+    (default dtype) before it is concatenated with the float64 pose; a numpy array keeps its dtype."""
+    if isinstance(params, np.ndarray):
+        return params.astype(np.float64)
+    if torch.is_tensor(params):
+        return params.detach().cpu().numpy().astype(np.float64)
+    vals = list(params)
+    # torch infers the default dtype (float32) for plain Python scalars when at least one is a float; numpy
+    # scalars keep their own dtype (np.float64 -> float64) and promote the result.
+    plain = all(type(x) in (float, int, bool) for x in vals)
+    arr = np.asarray(vals, dtype=np.float64)
+    if plain and any(type(x) is float for x in vals):
+        return arr.astype(np.float32).astype(np.float64)
+    return arr
+
+
+def _rotate_quat(points, pose):
+    t, qv, w = pose[:, 0:3], pose[:, 3:6], pose[:, 6:7]
+    uv = np.cross(qv, points)
+    return points + 2.0 * (w * uv + np.cross(qv, uv)) + t
+
+
+class PackedProblem:
+    """What TorchBA.Solve hands the LM (reference :98-126): compacted, track-major arrays + bookkeeping."""
+
+    def __init__(self, model, points_2d, camera_indices, point_indices, camera_pps, camera_params, points_3d,
+                 unique_cameras, unique_points, track_keys, remaining_indices, pp_indices):
+        self.model = model
+        self.points_2d = points_2d
+        self.camera_indices = camera_indices
+        self.point_indices = point_indices
+        self.camera_pps = camera_pps
+        self.camera_params = camera_params
+        self.points_3d = points_3d
+        self.unique_cameras = unique_cameras
+        self.unique_points = unique_points
+        self.track_keys = track_keys
+        self.remaining_indices = remaining_indices
+        self.pp_indices = pp_indices
+
+
+def pack(cameras, images, tracks, options):
+    """Vectorized restatement of bundle_adjustment.py:66-113."""
+    model = cameras[0].model_id  # :45 "assume all cameras are under the same model"
+    info = get_camera_model_info(model)
+    if model.value not in IMPLEMENTED_MODELS:
+        raise NotImplementedError("Unsupported camera model")
+    track_keys = list(tracks.keys())
+    lengths = np.array([len(tracks[k].observations) for k in track_keys], dtype=np.int64)
+    is_valid = lengths >= options['min_num_view_per_track']                                   # :66-68
+    registered = np.array([img.is_registered for img in images], dtype=bool)                  # :70
+    rows = []
+    for img in images:                                                                        # :71-73
+        if img.is_registered:
+            w2c = np.asarray(img.world2cam, dtype=np.float64)
+            se3 = np.concatenate([w2c[:3, 3], _quat_xyzw_from_matrix(w2c[:3, :3])])
+        else:
+            se3 = np.array([0, 0, 0, 0, 0, 0, 1.0])
+        rows.append(np.concatenate([se3, _as_torch_like_params(cameras[img.cam_id].params)]))
+    camera_params = np.stack(rows).astype(np.float64)
+    pp_indices = np.asarray(info['pp']) + 7                                                   # :75-80
+    remaining = np.array([i for i in range(camera_params.shape[1]) if i not in pp_indices])
+    camera_pps = camera_params[:, pp_indices]
+    camera_params = camera_params[:, remaining]
+    points_3d = np.stack([np.asarray(tracks[k].xyz, dtype=np.float64) for k in track_keys])   # :82-83
+
+    valid_ids = np.nonzero(is_valid)[0]                                                       # :85-96
+    if valid_ids.size:
+        obs = [np.asarray(tracks[track_keys[t]].observations).reshape(-1, 2) for t in valid_ids]
+        counts = np.array([o.shape[0] for o in obs])
+        obs = np.concatenate(obs).astype(np.int64)
+        tid = np.repeat(valid_ids, counts)
+    else:
+        obs = np.zeros((0, 2), np.int64)
+        tid = np.zeros(0, np.int64)
+    img_id, feat_id = obs[:, 0], obs[:, 1]
+    keep = registered[img_id]
+    img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
+    feats = [np.asarray(im.features, dtype=np.float64).reshape(-1, 2) for im in images]
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])])
+    feat_all = np.concatenate(feats) if feats else np.zeros((0, 2))
+    points_2d = feat_all[foff[img_id] + feat_id]
+
+    z = _rotate_quat(points_3d[tid], camera_params[img_id][:, :7])[:, 2]                      # :102-107
+    ok = z > 0.1
+    points_2d, img_id, tid = points_2d[ok], img_id[ok], tid[ok]
+    unique_cameras, cam_inv = np.unique(img_id, return_inverse=True)                          # :108-113
+    unique_points, pt_inv = np.unique(tid, return_inverse=True)
+    return PackedProblem(model, np.ascontiguousarray(points_2d), cam_inv.astype(np.int64), pt_inv.astype(np.int64),
+                         np.ascontiguousarray(camera_pps[unique_cameras]),
+                         np.ascontiguousarray(camera_params[unique_cameras]),
+                         np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points, track_keys,
+                         remaining, pp_indices)
+
+
+def update(cameras, images, tracks, packed, camera_params, points_3d):
+    """bundle_adjustment.py:18-36: write the optimized parameters back into the scene objects."""
+    cp = camera_params.detach().cpu().numpy() if torch.is_tensor(camera_params) else np.asarray(camera_params)
+    pts = points_3d.detach().cpu().numpy() if torch.is_tensor(points_3d) else np.asarray(points_3d)
+    full = np.zeros((cp.shape[0], cp.shape[1] + 2))
+    full[:, packed.remaining_indices] = cp
+    full[:, packed.pp_indices] = packed.camera_pps
+    mats = _pose_matrices(full[:, :7])
+    for i, orig in enumerate(packed.unique_points.tolist()):
+        tracks[packed.track_keys[orig]].xyz = pts[i]
+    for i, image_id in enumerate(packed.unique_cameras.tolist()):
+        image = images[image_id]
+        image.world2cam = mats[i]
+        cameras[image.cam_id].set_params(full[i, 7:])
+
+
+class TorchBA:
+    """bundle_adjustment.py:38-154 with the HIP engine underneath."""
+
+    def __init__(self, visualizer=None, device="cuda:0"):
+        self.device = device
+        self.visualizer = visualizer
+        self.loss_history = []
+        self.last_stats = None
+
+    def Solve(self, cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=True):
+        opts = BUNDLE_ADJUSTER_OPTIONS
+        packed = pack(cameras, images, tracks, opts)
+        if packed.points_2d.shape[0] == 0:
+            return
+        # the engine wants track-major observations: point_indices from np.unique are already nondecreasing because
+        # observations were gathered track by track (reference :88-96), so no reordering is needed.
+        eng = BundleAdjuster(packed.model.value, packed.points_2d, packed.camera_indices, packed.point_indices,
+                             packed.camera_pps, packed.camera_params.shape[0], packed.points_3d.shape[0],
+                             device=self.device, optimize_poses=opts['optimize_poses'],
+                             huber_delta=opts['thres_loss_function'], deterministic=opts.get('deterministic', False),
+                             **{k: opts[k] for k in ('pcg_max_iter', 'pcg_tol') if k in opts})
+        dev = torch.device(self.device)
+        cams_t = torch.from_numpy(packed.camera_params).to(dev).contiguous()
+        pts_t = torch.from_numpy(packed.points_3d).to(dev).contiguous()
+        window_size = 4                                                                       # :128-150
+        loss_history = []
+        it = range(opts['max_num_iterations'])
+        bar = None
+        if progress:
+            try:
+                import tqdm
+                bar = tqdm.trange(opts['max_num_iterations'])
+                it = bar
+            except ImportError:
+                pass
+        for _ in it:
+            loss, stats = eng.step(cams_t, pts_t)
+            self.last_stats = stats
+            loss_history.append(loss)
+            if len(loss_history) >= 2 * window_size:
+                avg_recent = np.mean(loss_history[-window_size:])
+                avg_previous = np.mean(loss_history[-2 * window_size:-window_size])
+                improvement = (avg_previous - avg_recent) / avg_previous
+                if abs(improvement) < opts['function_tolerance']:
+                    break
+                if loss_history[-1] == loss_history[-2]:
+                    break
+            if bar is not None:
+                bar.set_postfix({"loss": loss})
+            if self.visualizer:
+                update(cameras, images, tracks, packed, cams_t, pts_t)
+                self.visualizer.add_step(cameras, images, tracks, "bundle_adjustment")
+        if bar is not None:
+            bar.close()
+        self.loss_history = loss_history
+        self.final_loss, self.final_rmse = eng.cost(cams_t, pts_t)
+        update(cameras, images, tracks, packed, cams_t, pts_t)
+        eng.close()

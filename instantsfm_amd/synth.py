@@ -1,0 +1,244 @@
+"""Seeded synthetic BA scenes.
+
+* C cameras on a ring of radius 30 around the origin (height jitter +-2), looking at the origin.
+* SIMPLE_RADIAL by default: f=1000, image 2000x1500, pp=(1000,750), GT k=-0.02.
+* P points uniform in a ball of radius 8; every track has L=10 observations whose cameras are L
+  distinct indices from the window {h-30..h+30} mod C around a uniform home camera h
+  (the whole ring when C <= 61).
+* observations = GT projection + N(0, 0.5^2) px; 1% outliers get +-U(5,20) px per coordinate.
+* initial values: rotation (+) N(0, 0.002^2) rad, translation + N(0, 0.05^2), points + N(0, 0.05^2),
+  focal * (1 + N(0, 0.005^2)), distortion = 0.
+* observations are stored track-major (the order ``TorchBA.Solve`` packs them in,
+  bundle_adjustment.py:85-100); camera rows are pypose ``[t, q_xyzw, intrinsics-without-pp]``.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+from .scene.defs import Camera, CameraModelId, Image, Track, num_intrinsics
+
+# Ground-truth intrinsics (without the principal point) per model id.
+_GT_INTR = {
+    0: [1000.0],
+    1: [1000.0, 1010.0],
+    2: [1000.0, -0.02],
+    3: [1000.0, -0.02, 0.004],
+    4: [1000.0, 1010.0, -0.02, 0.004, 1e-4, -2e-4],
+    5: [1000.0, 1010.0, -0.01, 0.002, -3e-4, 0.0],
+    6: [1000.0, 1010.0, -0.02, 0.004, 1e-4, -2e-4, 1e-3, 0.01, -0.002, 3e-4],
+    8: [1000.0, -0.01],
+    9: [1000.0, -0.01, 0.002],
+}
+_FOCAL_COUNT = {0: 1, 1: 2, 2: 1, 3: 1, 4: 2, 5: 2, 6: 2, 8: 1, 9: 1}
+
+
+@dataclass
+class BAProblem:
+    model: int
+    cams_gt: np.ndarray      # [C, 7+ni] f64
+    cams_init: np.ndarray    # [C, 7+ni] f64
+    pp: np.ndarray           # [C, 2] f64
+    points_gt: np.ndarray    # [P, 3] f64
+    points_init: np.ndarray  # [P, 3] f64
+    uv: np.ndarray           # [N, 2] f64, track-major
+    cam_idx: np.ndarray      # [N] int32
+    pt_idx: np.ndarray       # [N] int32, nondecreasing
+
+    @property
+    def n_cams(self):
+        return self.cams_init.shape[0]
+
+    @property
+    def n_points(self):
+        return self.points_init.shape[0]
+
+    @property
+    def n_obs(self):
+        return self.uv.shape[0]
+
+
+def _quat_mul(a, b):
+    """Hamilton product of xyzw quaternions (broadcasting)."""
+    ax, ay, az, aw = np.moveaxis(a, -1, 0)
+    bx, by, bz, bw = np.moveaxis(b, -1, 0)
+    return np.stack([aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw,
+                     aw * bw - ax * bx - ay * by - az * bz], axis=-1)
+
+
+def _quat_from_rotvec(v):
+    th = np.linalg.norm(v, axis=-1, keepdims=True)
+    half = 0.5 * th
+    s = np.where(th > 1e-12, np.sin(half) / np.maximum(th, 1e-300), 0.5 - th * th / 48.0)
+    return np.concatenate([v * s, np.cos(half)], axis=-1)
+
+
+def _quat_from_matrix(R):
+    """Rotation matrix -> xyzw quaternion with w >= 0 (batched)."""
+    from scipy.spatial.transform import Rotation
+    q = Rotation.from_matrix(R).as_quat()
+    return np.where(q[..., 3:4] < 0, -q, q)
+
+
+def quat_to_matrix(q):
+    x, y, z, w = np.moveaxis(q, -1, 0)
+    return np.stack([
+        np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)], -1),
+        np.stack([2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)], -1),
+        np.stack([2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)], -1)], -2)
+
+
+def _project(model, X, cams, pp):
+    R = quat_to_matrix(cams[:, 3:7])
+    pc = np.einsum('nij,nj->ni', R, X) + cams[:, :3]
+    uv = pc[:, :2] / pc[:, 2:3]
+    intr = cams[:, 7:]
+    nf = _FOCAL_COUNT[model]
+    ff = intr[:, :nf] if nf == 2 else np.repeat(intr[:, :1], 2, axis=1)
+    k = intr[:, nf:]
+    r2 = np.sum(uv * uv, axis=1, keepdims=True)
+    if model in (0, 1):
+        d = uv
+    elif model == 2:
+        d = uv * (1 + k[:, 0:1] * r2)
+    elif model == 3:
+        d = uv * (1 + k[:, 0:1] * r2 + k[:, 1:2] * r2 ** 2)
+    elif model in (4, 6):
+        k1, k2, p = k[:, 0:1], k[:, 1:2], k[:, 2:4]
+        if model == 4:
+            radial = k1 * r2 + k2 * r2 ** 2
+        else:
+            k3, k4, k5, k6 = k[:, 4:5], k[:, 5:6], k[:, 6:7], k[:, 7:8]
+            radial = (1 + k1 * r2 + k2 * r2 ** 2 + k3 * r2 ** 3) / (1 + k4 * r2 + k5 * r2 ** 2 + k6 * r2 ** 3) - 1
+        uvp = uv[:, 0:1] * uv[:, 1:2]
+        d = uv + uv * radial + 2 * p * uvp + p[:, ::-1] * (r2 + 2 * uv ** 2)
+    elif model in (5, 8, 9):
+        r = np.sqrt(r2)
+        g = np.arctan(r) / r
+        if model == 5:
+            d = uv * g * (1 + k[:, 0:1] * r2 + k[:, 1:2] * r2 ** 2 + k[:, 2:3] * r2 ** 3)
+        elif model == 8:
+            d = uv * g * (1 + k[:, 0:1] * r2)
+        else:
+            d = uv * g * (1 + k[:, 0:1] * r2 + k[:, 1:2] * r2 ** 2)
+    else:
+        raise NotImplementedError
+    return d * ff + pp, pc
+
+
+def make_problem(n_cams, n_points, track_len=10, seed=0, model=2, noise_px=0.5, outlier_frac=0.01,
+                 window=30, rot_sigma=0.002, trans_sigma=0.05, point_sigma=0.05, focal_sigma=0.005):
+    """Build a seeded BAProblem; see module docstring for the recipe."""
+    if model not in _GT_INTR:
+        raise NotImplementedError(f"camera model {model}")
+    rng = np.random.default_rng(seed)
+    C, P, L = int(n_cams), int(n_points), int(track_len)
+    if L > C:
+        raise ValueError("track_len exceeds number of cameras")
+    ni = num_intrinsics(model)
+
+    ang = 2 * np.pi * np.arange(C) / C
+    centers = np.stack([30 * np.cos(ang), 30 * np.sin(ang), rng.uniform(-2, 2, C)], axis=1)
+    zax = -centers / np.linalg.norm(centers, axis=1, keepdims=True)
+    up = np.array([0.0, 0.0, 1.0])
+    xax = np.cross(zax, up)
+    xax /= np.linalg.norm(xax, axis=1, keepdims=True)
+    yax = np.cross(zax, xax)
+    Rw2c = np.stack([xax, yax, zax], axis=1)
+    t = -np.einsum('cij,cj->ci', Rw2c, centers)
+    q = _quat_from_matrix(Rw2c)
+    intr = np.tile(np.asarray(_GT_INTR[model], dtype=np.float64), (C, 1))
+    cams_gt = np.concatenate([t, q, intr], axis=1)
+    pp = np.tile(np.array([1000.0, 750.0]), (C, 1))
+
+    d = rng.normal(size=(P, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    points_gt = d * (8.0 * rng.uniform(0, 1, (P, 1)) ** (1.0 / 3.0))
+
+    if C <= 2 * window + 1:
+        keys = rng.uniform(size=(P, C))
+        cams_of = np.argsort(keys, axis=1)[:, :L]
+    else:
+        home = rng.integers(0, C, P)
+        keys = rng.uniform(size=(P, 2 * window + 1))
+        offs = np.argsort(keys, axis=1)[:, :L] - window
+        cams_of = (home[:, None] + offs) % C
+    cams_of = np.sort(cams_of, axis=1)
+    cam_idx = cams_of.reshape(-1).astype(np.int32)
+    pt_idx = np.repeat(np.arange(P, dtype=np.int32), L)
+
+    uv, _ = _project(model, points_gt[pt_idx], cams_gt[cam_idx], pp[cam_idx])
+    uv = uv + rng.normal(0, noise_px, uv.shape)
+    n_out = int(round(outlier_frac * uv.shape[0]))
+    if n_out:
+        which = rng.choice(uv.shape[0], n_out, replace=False)
+        uv[which] += rng.choice([-1.0, 1.0], (n_out, 2)) * rng.uniform(5, 20, (n_out, 2))
+
+    dq = _quat_from_rotvec(rng.normal(0, rot_sigma, (C, 3)))
+    q0 = _quat_mul(dq, q)
+    t0 = t + rng.normal(0, trans_sigma, (C, 3))
+    intr0 = np.zeros_like(intr)
+    nf = _FOCAL_COUNT[model]
+    intr0[:, :nf] = intr[:, :nf] * (1 + rng.normal(0, focal_sigma, (C, 1)))
+    cams_init = np.concatenate([t0, q0, intr0], axis=1)
+    points_init = points_gt + rng.normal(0, point_sigma, (P, 3))
+    assert cams_init.shape[1] == 7 + ni
+    return BAProblem(model, cams_gt, cams_init, pp, points_gt, points_init,
+                     np.ascontiguousarray(uv), cam_idx, pt_idx)
+
+
+# reference configs (BASELINE.json "configs")
+CONFIGS = {
+    1: dict(n_cams=20, n_points=2000),
+    2: dict(n_cams=200, n_points=50000),
+    3: dict(n_cams=1000, n_points=200000),
+}
+
+
+def make_config(cfg, seed=0, **kw):
+    return make_problem(seed=seed, **CONFIGS[cfg], **kw)
+
+
+def full_params(model, cam_row, pp):
+    """Re-insert the pp columns into an intrinsics vector (inverse of bundle_adjustment.py:75-80)."""
+    from .scene.defs import get_camera_model_info
+    info = get_camera_model_info(CameraModelId(model))
+    out = np.zeros(info['num_params'])
+    rest = [i for i in range(info['num_params']) if i not in info['pp']]
+    out[rest] = cam_row
+    out[info['pp']] = pp
+    return out
+
+
+def to_scene(problem: BAProblem, use_init=True, image_features_dtype=np.float64):
+    """Scene objects (cameras list, images list, tracks dict) for ``TorchBA.Solve``.
+
+    One camera per image; image i observes its features in track order.
+    """
+    cams = problem.cams_init if use_init else problem.cams_gt
+    pts = problem.points_init if use_init else problem.points_gt
+    C = problem.n_cams
+    model = CameraModelId(problem.model)
+    cameras, images = [], []
+    order = np.argsort(problem.cam_idx, kind='stable')
+    counts = np.bincount(problem.cam_idx, minlength=C)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    feat_id = np.empty(problem.n_obs, dtype=np.int64)
+    feat_id[order] = np.arange(problem.n_obs) - np.repeat(starts[:-1], counts)
+    for c in range(C):
+        cameras.append(Camera(id=c, model_id=model, width=2000, height=1500,
+                              params=full_params(problem.model, cams[c, 7:], problem.pp[c])))
+        R = quat_to_matrix(cams[c, 3:7])
+        w2c = np.eye(4)
+        w2c[:3, :3] = R
+        w2c[:3, 3] = cams[c, :3]
+        feats = problem.uv[order[starts[c]:starts[c + 1]]].astype(image_features_dtype)
+        images.append(Image(id=c, cam_id=c, is_registered=True, world2cam=w2c, features=feats))
+    tracks = {}
+    L_ptr = np.concatenate([[0], np.cumsum(np.bincount(problem.pt_idx, minlength=problem.n_points))])
+    obs_pairs = np.stack([problem.cam_idx.astype(np.int64), feat_id], axis=1)
+    for p in range(problem.n_points):
+        tracks[p] = Track(id=p, xyz=pts[p].copy(), observations=obs_pairs[L_ptr[p]:L_ptr[p + 1]].copy(),
+                          is_initialized=True)
+    return cameras, images, tracks

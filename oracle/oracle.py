@@ -1,0 +1,177 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY -- ctypes wrapper of oracle/ba_oracle.c.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libba_oracle.so")
+_lib = None
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+# buffer ids for ora_get
+W, V, GP, U, GC, S, B, DC, DP = range(9)
+
+
+def build(quiet=True):
+    subprocess.run(["make", "-C", _HERE], check=True, capture_output=quiet)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.ora_create.restype = ctypes.c_void_p
+        L.ora_create.argtypes = [ctypes.c_int] * 4 + [_dp, _ip, _ip, _dp, _dp, _ip]
+        L.ora_destroy.argtypes = [ctypes.c_void_p]
+        L.ora_step.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
+        L.ora_cost.restype = ctypes.c_double
+        L.ora_cost.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
+        L.ora_linearize.argtypes = [ctypes.c_void_p, _dp, _dp]
+        L.ora_solve.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.ora_get.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp]
+        L.ora_nnzb.argtypes = [ctypes.c_void_p]
+        L.ora_pattern.argtypes = [ctypes.c_void_p, _ip, _ip]
+        L.ora_stats.argtypes = [ctypes.c_void_p, _dp]
+        L.ora_eval.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.ora_retract_pose.argtypes = [_dp, _dp, _dp]
+        L.ora_n_intr.argtypes = [ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _i(a):
+    return a.ctypes.data_as(_ip)
+
+
+def n_intr(model):
+    return lib().ora_n_intr(model)
+
+
+def evaluate(model, X, cam, pp, uv=None, want_jac=True):
+    """Residual (or projection when uv is None) and analytic Jacobians for n observations."""
+    X = np.ascontiguousarray(X, np.float64)
+    cam = np.ascontiguousarray(cam, np.float64)
+    pp = np.ascontiguousarray(pp, np.float64)
+    n = X.shape[0]
+    D = 6 + n_intr(model)
+    r = np.zeros((n, 2))
+    Jc = np.zeros((n, 2, D)) if want_jac else None
+    Jp = np.zeros((n, 2, 3)) if want_jac else None
+    u = np.ascontiguousarray(uv, np.float64) if uv is not None else None
+    lib().ora_eval(model, n, _d(X), _d(cam), _d(pp), _d(u) if u is not None else None, _d(r),
+                   _d(Jc) if want_jac else None, _d(Jp) if want_jac else None)
+    return r, Jc, Jp
+
+
+def retract_pose(x7, d6):
+    x7 = np.ascontiguousarray(x7, np.float64)
+    d6 = np.ascontiguousarray(d6, np.float64)
+    out = np.zeros(7)
+    lib().ora_retract_pose(_d(x7), _d(d6), _d(out))
+    return out
+
+
+DEFAULTS = dict(huber_delta=1.0, tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4,
+                tr_factor=0.5, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
+                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0)
+
+
+class OracleBA:
+    """CPU LM-BA restatement on a packed problem (track-major obs, pypose camera rows)."""
+
+    def __init__(self, model, uv, cam_idx, pt_idx, pp, n_cams, n_points, **opts):
+        o = dict(DEFAULTS, **opts)
+        self.model = int(model)
+        self.C, self.P = int(n_cams), int(n_points)
+        self.uv = np.ascontiguousarray(uv, np.float64)
+        self.cam = np.ascontiguousarray(cam_idx, np.int32)
+        self.pt = np.ascontiguousarray(pt_idx, np.int32)
+        self.pp = np.ascontiguousarray(pp, np.float64)
+        self.N = self.uv.shape[0]
+        self.D = 6 + n_intr(self.model)
+        dopt = np.array([o['huber_delta'], o['tr_radius'], o['tr_max'], o['tr_min'], o['tr_up'], o['tr_down'],
+                         o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
+        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], o['optimize_poses'], o['threads']], np.int32)
+        self.h = lib().ora_create(self.model, self.C, self.P, self.N, _d(self.uv), _i(self.cam), _i(self.pt),
+                                  _d(self.pp), _d(dopt), _i(iopt))
+        if not self.h:
+            raise ValueError("ora_create failed (bad sizes/model or obs not track-major)")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_destroy(self.h)
+            self.h = None
+
+    def step(self, cams, pts):
+        """One LM step; cams [C,stride] / pts [P,3] float64 arrays are updated in place."""
+        assert cams.flags.c_contiguous and pts.flags.c_contiguous
+        loss = ctypes.c_double()
+        lib().ora_step(self.h, _d(cams), _d(pts), ctypes.byref(loss))
+        return loss.value
+
+    def stats(self):
+        s = np.zeros(8)
+        lib().ora_stats(self.h, _d(s))
+        return dict(trials=int(s[0]), pcg_iters=int(s[1]), pcg_total=int(s[2]), damp_factor=s[3],
+                    damping=s[4], failed=int(s[5]), rejects=int(s[6]))
+
+    def cost(self, cams, pts):
+        sq = ctypes.c_double()
+        loss = lib().ora_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)), ctypes.byref(sq))
+        return loss, float(np.sqrt(sq.value / self.N))
+
+    def linearize(self, cams, pts):
+        lib().ora_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)))
+
+    def solve(self, f):
+        return lib().ora_solve(self.h, float(f))
+
+    def nnzb(self):
+        return lib().ora_nnzb(self.h)
+
+    def pattern(self):
+        rp = np.zeros(self.C + 1, np.int32)
+        col = np.zeros(self.nnzb(), np.int32)
+        lib().ora_pattern(self.h, _i(rp), _i(col))
+        return rp, col
+
+    def get(self, which):
+        shapes = {W: (self.N, self.D, 3), V: (self.P, 6), GP: (self.P, 3), U: (self.C, self.D, self.D),
+                  GC: (self.C, self.D), S: (self.nnzb(), self.D, self.D), B: (self.C, self.D),
+                  DC: (self.C, self.D), DP: (self.P, 3)}
+        out = np.zeros(shapes[which])
+        lib().ora_get(self.h, which, _d(out))
+        return out
+
+
+def solve_to_convergence(problem, max_iters=200, ftol=5e-4, window=4, **opts):
+    """TorchBA.Solve's loop (bundle_adjustment.py:128-150) driven by the oracle step."""
+    ba = OracleBA(problem.model, problem.uv, problem.cam_idx, problem.pt_idx, problem.pp,
+                  problem.n_cams, problem.n_points, **opts)
+    cams = problem.cams_init.copy()
+    pts = problem.points_init.copy()
+    hist = []
+    for _ in range(max_iters):
+        hist.append(ba.step(cams, pts))
+        if len(hist) >= 2 * window:
+            recent = np.mean(hist[-window:])
+            prev = np.mean(hist[-2 * window:-window])
+            if abs((prev - recent) / prev) < ftol:
+                break
+            if hist[-1] == hist[-2]:
+                break
+    loss, rmse = ba.cost(cams, pts)
+    return cams, pts, hist, rmse

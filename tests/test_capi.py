@@ -1,0 +1,89 @@
+"""C-ABI library: loads without a GPU, exports every symbol include/insfm_ba.h declares, rejects bad inputs before
+touching the device, and the product path refuses to run without a GPU (no CPU fallback)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from instantsfm_amd import _capi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(REPO, "include", "insfm_ba.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(insfm_ba_[a-z_]+)\s*\(", txt)) - {"insfm_ba_allreduce_fn"})
+
+
+def test_header_declares_expected_api():
+    fns = header_functions()
+    for name in ("insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_destroy", "insfm_ba_last_error"):
+        assert name in fns
+
+
+def test_library_exports_every_header_symbol():
+    L = _capi.load()
+    for name in header_functions():
+        assert hasattr(L, name), name
+    assert set(header_functions()) == set(_capi.SYMBOLS)
+
+
+def test_struct_layout_matches_header():
+    # field order/size of insfm_ba_desc as the C compiler sees it
+    d = _capi.default_desc()
+    assert d.huber_delta == 1.0 and d.tr_radius == 1e4 and d.tr_max == 1e10 and d.tr_down == 1 / 16
+    assert d.max_rejects == 30 and abs(d.pcg_tol - 1e-5) < 1e-20 and d.world_size == 1 and d.cam_model == 2
+
+
+def _create(desc, uv, cam, pt, pp):
+    L = _capi.load()
+    h = ctypes.c_void_p()
+    rc = L.insfm_ba_create(ctypes.byref(desc), uv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                           cam.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), pt.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                           pp.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), None, ctypes.byref(h))
+    msg = L.insfm_ba_last_error(h).decode() if h.value else ""
+    if h.value:
+        L.insfm_ba_destroy(h)
+    return rc, msg
+
+
+@pytest.mark.parametrize("case", ["model7", "model10", "not_track_major", "cam_oob", "pt_oob", "bad_rank"])
+def test_create_rejects_bad_inputs_without_gpu(case):
+    d = _capi.default_desc()
+    uv = np.zeros((4, 2))
+    cam = np.array([0, 1, 0, 1], np.int32)
+    pt = np.array([0, 0, 1, 1], np.int32)
+    pp = np.zeros((2, 2))
+    d.n_cams, d.n_points, d.n_obs = 2, 2, 4
+    if case == "model7":
+        d.cam_model = 7
+    elif case == "model10":
+        d.cam_model = 10
+    elif case == "not_track_major":
+        pt = np.array([1, 0, 1, 0], np.int32)
+    elif case == "cam_oob":
+        cam = np.array([0, 2, 0, 1], np.int32)
+    elif case == "pt_oob":
+        pt = np.array([0, 0, 1, 5], np.int32)
+    elif case == "bad_rank":
+        d.world_size, d.rank = 2, 3
+    rc, msg = _create(d, uv, cam, pt, pp)
+    assert rc == _capi.INSFM_BA_EINVAL, (rc, msg)
+    assert msg
+
+
+def test_no_cpu_fallback():
+    from instantsfm_amd.engine import BundleAdjuster
+    with pytest.raises(RuntimeError):
+        BundleAdjuster(2, np.zeros((4, 2)), [0, 1, 0, 1], [0, 0, 1, 1], np.zeros((2, 2)), 2, 2, device="cpu")
+
+
+def test_product_path_does_not_import_oracle():
+    for root, _, files in os.walk(os.path.join(REPO, "instantsfm_amd")):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                src = open(os.path.join(root, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace("oracle's", ""), f

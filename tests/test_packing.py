@@ -1,0 +1,96 @@
+"""TorchBA.Solve packing (bundle_adjustment.py:66-126) vs golden vectors captured from the reference itself
+(tools/gen_golden.py).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from instantsfm_amd.processors.bundle_adjustment import _pose_matrices, pack, update
+from instantsfm_amd.scene.defs import Camera, CameraModelId, Image, Track
+
+OPTS = dict(optimize_poses=True, optimize_points=True, min_num_view_per_track=2, thres_loss_function=1.0,
+            max_num_iterations=200, function_tolerance=5e-4)
+
+
+def scene_from_fixture(g, params_kind):
+    """params_kind: 'pyfloat' (list of Python floats), 'np64list' (list of np.float64), 'array' (float64 ndarray)."""
+    model = CameraModelId(int(g["model"]))
+    cams = []
+    for i, p in enumerate(g["cam_params"]):
+        params = {"pyfloat": [float(x) for x in p], "np64list": list(p), "array": np.array(p)}[params_kind]
+        cams.append(Camera(id=i, model_id=model, params=params))
+    imgs = []
+    fp = g["img_feat_ptr"]
+    for i in range(len(g["img_cam_id"])):
+        imgs.append(Image(id=i, cam_id=int(g["img_cam_id"][i]), is_registered=bool(g["img_registered"][i]),
+                          world2cam=g["img_world2cam"][i], features=g["img_feats"][fp[i]:fp[i + 1]]))
+    tracks = {}
+    tp = g["track_obs_ptr"]
+    for k, key in enumerate(g["track_keys"]):
+        tracks[int(key)] = Track(id=int(key), xyz=g["track_xyz"][k], observations=g["track_obs"][tp[k]:tp[k + 1]])
+    return cams, imgs, tracks
+
+
+def quat_equal_up_to_sign(a, b, tol):
+    return np.all(np.minimum(np.abs(a - b).max(-1), np.abs(a + b).max(-1)) < tol)
+
+
+@pytest.mark.parametrize("name", ["packing_config1", "packing_edge", "packing_edge_points_only"])
+def test_pack_matches_reference(golden_dir, name):
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    # rebuild the scene with the parameter types tools/gen_golden.py used for that fixture
+    kind = "np64list" if name == "packing_config1" else "pyfloat"
+    cams, imgs, tracks = scene_from_fixture(g, kind)
+    opts = dict(OPTS, optimize_poses=bool(g["out_optimize_poses"]))
+    pk = pack(cams, imgs, tracks, opts)
+    np.testing.assert_array_equal(pk.points_2d, g["out_points_2d"])
+    np.testing.assert_array_equal(pk.camera_indices, g["out_camera_indices"])
+    np.testing.assert_array_equal(pk.point_indices, g["out_point_indices"])
+    np.testing.assert_array_equal(pk.camera_pps, g["out_camera_pps"])
+    np.testing.assert_array_equal(pk.points_3d, g["out_points_3d"])
+    pose = g["out_pose"]
+    np.testing.assert_allclose(pk.camera_params[:, :3], pose[:, :3], rtol=0, atol=1e-12)
+    assert quat_equal_up_to_sign(pk.camera_params[:, 3:7], pose[:, 3:7], 1e-12)
+    # intrinsics: bit-exact, including the reference's float32 rounding of list-typed params
+    np.testing.assert_array_equal(pk.camera_params[:, 7:], pose[:, 7:])
+    assert np.all(np.diff(pk.point_indices) >= 0), "track-major order"
+
+
+def test_pack_float64_params_not_rounded(golden_dir):
+    g = np.load(os.path.join(golden_dir, "packing_edge.npz"))
+    cams, imgs, tracks = scene_from_fixture(g, "array")
+    pk = pack(cams, imgs, tracks, OPTS)
+    # numpy float64 params (what the COLMAP database reader produces, data_reader.py:44) stay float64
+    expect = np.asarray(g["cam_params"])[:, [0, 1, 4, 5, 6, 7]]
+    assert np.array_equal(pk.camera_params[0, 7:], expect[int(g["img_cam_id"][0])])
+
+
+def test_unsupported_models_raise():
+    for m in (CameraModelId.FOV, CameraModelId.THIN_PRISM_FISHEYE):
+        n = 5 if m == CameraModelId.FOV else 12
+        cams = [Camera(id=0, model_id=m, params=[100.0] * n)]
+        imgs = [Image(id=0, cam_id=0, is_registered=True, features=np.zeros((1, 2)))]
+        tracks = {0: Track(xyz=np.zeros(3), observations=np.array([[0, 0], [0, 0]]))}
+        with pytest.raises(NotImplementedError):
+            pack(cams, imgs, tracks, OPTS)
+
+
+def test_update_writes_back(golden_dir):
+    """update() (reference :18-36): pp re-inserted, SE3 -> 4x4, last image of a shared camera wins."""
+    g = np.load(os.path.join(golden_dir, "packing_edge.npz"))
+    cams, imgs, tracks = scene_from_fixture(g, "array")
+    pk = pack(cams, imgs, tracks, OPTS)
+    cp = pk.camera_params.copy()
+    cp[:, 7] += np.arange(cp.shape[0])  # distinct fx per packed image
+    pts = pk.points_3d + 1.0
+    update(cams, imgs, tracks, pk, cp, pts)
+    for i, orig in enumerate(pk.unique_points):
+        np.testing.assert_array_equal(tracks[pk.track_keys[orig]].xyz, pts[i])
+    M = _pose_matrices(cp[:, :7])
+    for i, image_id in enumerate(pk.unique_cameras):
+        np.testing.assert_allclose(imgs[image_id].world2cam, M[i], atol=1e-15)
+        np.testing.assert_allclose(imgs[image_id].world2cam[:3, :3] @ imgs[image_id].world2cam[:3, :3].T, np.eye(3), atol=1e-12)
+    # images 0, 2, 4 share camera 0: the last packed one of them wins
+    last = max(i for i, image_id in enumerate(pk.unique_cameras) if imgs[image_id].cam_id == 0)
+    assert cams[0].params[0] == cp[last, 7]
+    assert cams[0].params[2] == pk.camera_pps[last, 0]  # principal point re-inserted

@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Generate golden vectors from the reference itself (run in the build container only).
+
+The reference (``/root/reference``) imports five modules that are absent from this image
+(pyceres, cv2, pypose@bae, bae.*).  Following SURVEY.md Appendix B, this script writes tiny shim
+modules into a temporary directory OUTSIDE the repository, imports the reference's own
+``instantsfm.utils.cost_function`` / ``instantsfm.processors.bundle_adjustment`` through them and
+records:
+
+* ``projection_golden.npz`` -- ``reproject_funcs[m]`` (cost_function.py:32-208) for the 9 implemented
+  models, 256 random observations each (seed 0).  The only restated piece inside is
+  ``bae.utils.ba.rotate_quat`` (R(q) p + t, pypose [t, q_xyzw] layout).
+* ``packing_<name>.npz`` -- what ``TorchBA.Solve`` (bundle_adjustment.py:66-126) hands to the LM:
+  ``points_2d``, ``camera_indices``, ``point_indices``, ``camera_pps`` and the model's ``pose`` /
+  ``points_3d`` parameters, together with the scene that produced them.  The LM shim raises after
+  capturing its input, so nothing past bundle_adjustment.py:132 runs.
+
+Only data leaves this script: no reference source is copied into the repository.
+Usage:  python tools/gen_golden.py [--out tests/golden]
+"""
+import argparse
+import os
+import sys
+import tempfile
+import types
+
+sys.dont_write_bytecode = True  # never write __pycache__ into /root/reference
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+
+class _Captured(Exception):
+    pass
+
+
+def install_shims():
+    """Register in-memory shim modules for the absent dependencies (Appendix B)."""
+    from scipy.spatial.transform import Rotation
+
+    def mod(name):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+        return m
+
+    pyceres = mod("pyceres")
+
+    class CostFunction:  # pragma: no cover - only subclassed at import time
+        def __init__(self, *a, **k):
+            pass
+    pyceres.CostFunction = CostFunction
+    mod("cv2")
+
+    # --- bae ---------------------------------------------------------------------------------
+    bae = mod("bae")
+    bae_utils = mod("bae.utils")
+    bae_ba = mod("bae.utils.ba")
+    bae_solvers = mod("bae.utils.pysolvers")
+    bae_optim = mod("bae.optim")
+    bae_autograd = mod("bae.autograd")
+    bae_fn = mod("bae.autograd.function")
+    bae.utils, bae.optim, bae.autograd = bae_utils, bae_optim, bae_autograd
+    bae_utils.ba, bae_utils.pysolvers, bae_autograd.function = bae_ba, bae_solvers, bae_fn
+
+    def rotate_quat(points, pose):
+        t, qv, w = pose[..., 0:3], pose[..., 3:6], pose[..., 6:7]
+        uv = torch.cross(qv, points, dim=-1)
+        uuv = torch.cross(qv, uv, dim=-1)
+        return points + 2.0 * (w * uv + uuv) + t
+    bae_ba.rotate_quat = rotate_quat
+    bae_fn.TrackingTensor = lambda x: x
+    bae_fn.map_transform = lambda f: f
+
+    class PCG:
+        def __init__(self, tol=None, **kw):
+            self.tol = tol
+    bae_solvers.PCG = PCG
+
+    class LM:
+        last = None
+
+        def __init__(self, model, **kwargs):
+            self.model, self.kwargs = model, kwargs
+
+        def step(self, inp):
+            LM.last = (self.model, self.kwargs, inp)
+            raise _Captured()
+    bae_optim.LM = LM
+
+    # --- pypose ------------------------------------------------------------------------------
+    pp = mod("pypose")
+    pp_optim = mod("pypose.optim")
+    pp_kernel = mod("pypose.optim.kernel")
+    pp_strategy = mod("pypose.optim.strategy")
+    pp.optim, pp_optim.kernel, pp_optim.strategy = pp_optim, pp_kernel, pp_strategy
+
+    class _SE3:
+        def __init__(self, data):
+            self.data = torch.as_tensor(data, dtype=torch.float64)
+
+        def tensor(self):
+            return self.data
+
+        def matrix(self):
+            d = self.data.detach().cpu().numpy().reshape(-1, 7)
+            out = np.tile(np.eye(4), (d.shape[0], 1, 1))
+            out[:, :3, :3] = Rotation.from_quat(d[:, 3:7]).as_matrix()
+            out[:, :3, 3] = d[:, :3]
+            return torch.from_numpy(out.reshape(self.data.shape[:-1] + (4, 4)))
+
+    def mat2SE3(m):
+        m = np.asarray(m, dtype=np.float64)
+        q = Rotation.from_matrix(m[:3, :3]).as_quat()
+        return _SE3(np.concatenate([m[:3, 3], q]))
+    pp.mat2SE3 = mat2SE3
+    pp.identity_SE3 = lambda: _SE3([0, 0, 0, 0, 0, 0, 1.0])
+    pp.SE3 = _SE3
+
+    class _Rec:
+        def __init__(self, *a, **k):
+            self.args, self.kwargs = a, k
+    pp_strategy.TrustRegion = _Rec
+    pp_kernel.Huber = _Rec
+    pp_kernel.Cauchy = _Rec
+    return LM
+
+
+def gen_projection(out_dir):
+    from instantsfm.utils.cost_function import reproject_funcs
+    sys.path.insert(0, REPO)
+    from oracle.projection_ref import N_INTR
+    rng = np.random.default_rng(0)
+    res = {}
+    n = 256
+    base = {0: [900.0], 1: [900.0, 950.0], 2: [900.0, -0.05], 3: [900.0, -0.05, 0.01],
+            4: [900.0, 950.0, -0.05, 0.01, 1e-3, -2e-3], 5: [900.0, 950.0, -0.02, 0.004, -1e-3, 5e-4],
+            6: [900.0, 950.0, -0.05, 0.01, 1e-3, -2e-3, 3e-3, 0.02, -0.004, 6e-4],
+            8: [900.0, -0.03], 9: [900.0, -0.03, 0.006]}
+    for m, ni in N_INTR.items():
+        q = rng.normal(size=(n, 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        t = rng.normal(0, 0.5, (n, 3))
+        intr = np.asarray(base[m])[None, :] * (1 + rng.normal(0, 0.1, (n, ni)))
+        cam = np.concatenate([t, q, intr], axis=1)
+        # points in front of the camera: p = R^T (pc - t) with pc at depth 2..10
+        from scipy.spatial.transform import Rotation
+        R = Rotation.from_quat(q).as_matrix()
+        pc = np.stack([rng.uniform(-1.5, 1.5, n), rng.uniform(-1.2, 1.2, n), np.ones(n)], 1) * rng.uniform(2, 10, (n, 1))
+        X = np.einsum('nji,nj->ni', R, pc - t)
+        ppt = rng.uniform(200, 1200, (n, 2))
+        out = reproject_funcs[m](torch.from_numpy(X), torch.from_numpy(cam), torch.from_numpy(ppt))
+        res[f"m{m}_points"] = X
+        res[f"m{m}_cam"] = cam
+        res[f"m{m}_pp"] = ppt
+        res[f"m{m}_out"] = out.numpy()
+    for m in (7, 10):  # FOV / THIN_PRISM_FISHEYE raise in the reference
+        try:
+            reproject_funcs[m](torch.zeros(1, 3), torch.zeros(1, 19), torch.zeros(1, 2))
+            res[f"m{m}_raises"] = np.array(0)
+        except NotImplementedError:
+            res[f"m{m}_raises"] = np.array(1)
+    np.savez_compressed(os.path.join(out_dir, "projection_golden.npz"), **res)
+    print("projection_golden.npz", len(res), "arrays")
+
+
+def _scene_arrays(cameras, images, tracks, model):
+    """Serialise a reference-class scene into plain arrays (inputs of the fixture)."""
+    keys = list(tracks.keys())
+    obs = [np.asarray(tracks[k].observations, dtype=np.int64).reshape(-1, 2) for k in keys]
+    feats = [np.asarray(im.features, dtype=np.float64).reshape(-1, 2) for im in images]
+    return dict(
+        model=np.array(model),
+        cam_params=np.stack([np.asarray(c.params, dtype=np.float64) for c in cameras]),
+        img_cam_id=np.array([im.cam_id for im in images]),
+        img_registered=np.array([im.is_registered for im in images]),
+        img_world2cam=np.stack([np.asarray(im.world2cam, dtype=np.float64) for im in images]),
+        img_feat_ptr=np.concatenate([[0], np.cumsum([len(f) for f in feats])]),
+        img_feats=np.concatenate(feats) if feats else np.zeros((0, 2)),
+        track_keys=np.array(keys, dtype=np.int64),
+        track_xyz=np.stack([np.asarray(tracks[k].xyz, dtype=np.float64) for k in keys]),
+        track_obs_ptr=np.concatenate([[0], np.cumsum([len(o) for o in obs])]),
+        track_obs=np.concatenate(obs) if obs else np.zeros((0, 2), np.int64),
+    )
+
+
+def _run_solve(LM, cameras, images, tracks, opts):
+    from instantsfm.processors.bundle_adjustment import TorchBA
+    try:
+        TorchBA(device="cpu").Solve(cameras, images, tracks, opts)
+    except _Captured:
+        pass
+    model, kwargs, inp = LM.last
+    return dict(
+        out_points_2d=inp["points_2d"].numpy(),
+        out_camera_indices=inp["camera_indices"].numpy(),
+        out_point_indices=inp["point_indices"].numpy(),
+        out_camera_pps=inp["camera_pps"].numpy(),
+        out_pose=model.pose.detach().numpy(),
+        out_points_3d=model.points_3d.detach().numpy(),
+        out_optimize_poses=np.array(bool(model.pose.requires_grad)),
+        out_reject=np.array(kwargs.get("reject", -1)),
+    )
+
+
+def gen_packing(out_dir, LM):
+    from instantsfm.scene.defs import Camera, CameraModelId, Image, Track
+    sys.path.insert(0, REPO)
+    from instantsfm_amd.synth import make_config, full_params, quat_to_matrix
+    opts = dict(optimize_poses=True, optimize_points=True, min_num_view_per_track=2, thres_loss_function=1.0,
+                max_num_iterations=200, function_tolerance=5e-4)
+
+    # (1) config-1 synthetic scene (20 cams / 2k points / 20k obs), SIMPLE_RADIAL
+    prob = make_config(1, seed=0)
+    cams, imgs, trks = [], [], {}
+    C = prob.n_cams
+    order = np.argsort(prob.cam_idx, kind="stable")
+    counts = np.bincount(prob.cam_idx, minlength=C)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    feat_id = np.empty(prob.n_obs, np.int64)
+    feat_id[order] = np.arange(prob.n_obs) - np.repeat(starts[:-1], counts)
+    for c in range(C):
+        cams.append(Camera(id=c, model_id=CameraModelId(prob.model), width=2000, height=1500,
+                           params=list(full_params(prob.model, prob.cams_init[c, 7:], prob.pp[c]))))
+        w2c = np.eye(4)
+        w2c[:3, :3] = quat_to_matrix(prob.cams_init[c, 3:7])
+        w2c[:3, 3] = prob.cams_init[c, :3]
+        imgs.append(Image(id=c, cam_id=c, is_registered=True, world2cam=w2c,
+                          features=prob.uv[order[starts[c]:starts[c + 1]]].copy()))
+    ptr = np.concatenate([[0], np.cumsum(np.bincount(prob.pt_idx, minlength=prob.n_points))])
+    pairs = np.stack([prob.cam_idx.astype(np.int64), feat_id], 1)
+    for p in range(prob.n_points):
+        trks[p] = Track(id=p, xyz=prob.points_init[p].copy(), observations=pairs[ptr[p]:ptr[p + 1]].copy())
+    res = _scene_arrays(cams, imgs, trks, prob.model)
+    res.update(_run_solve(LM, cams, imgs, trks, opts))
+    np.savez_compressed(os.path.join(out_dir, "packing_config1.npz"), **res)
+    print("packing_config1.npz", res["out_points_2d"].shape)
+
+    # (2) hand-built edge cases, OPENCV (pp at columns 2,3): unregistered image, length-1 track,
+    #     point behind a camera (z <= 0.1), two images sharing one camera, non-contiguous track keys
+    rng = np.random.default_rng(1)
+    model = CameraModelId.OPENCV
+    cams = [Camera(id=0, model_id=model, params=[800.0, 810.0, 500.0, 400.0, -0.01, 0.001, 1e-4, -1e-4]),
+            Camera(id=1, model_id=model, params=[900.0, 905.0, 520.0, 390.0, 0.02, -0.002, -2e-4, 3e-4])]
+    imgs = []
+    for i in range(5):
+        w2c = np.eye(4)
+        ang = 0.1 * i
+        w2c[:3, :3] = np.array([[np.cos(ang), 0, np.sin(ang)], [0, 1, 0], [-np.sin(ang), 0, np.cos(ang)]])
+        w2c[:3, 3] = [0.3 * i, -0.1 * i, 4.0]
+        imgs.append(Image(id=i, cam_id=0 if i in (0, 2, 4) else 1, is_registered=(i != 3), world2cam=w2c,
+                          features=rng.uniform(0, 1000, (6, 2))))
+    pts = {17: ([0.1, 0.2, 0.5], [[0, 0], [1, 1], [2, 2]]),
+           3: ([0.0, 0.0, 0.0], [[1, 0]]),                      # length 1 -> dropped
+           9: ([-0.3, 0.1, 1.0], [[0, 1], [3, 2], [4, 3]]),      # obs in unregistered image 3 skipped
+           42: ([0.0, 0.0, -5.0], [[0, 2], [2, 3], [4, 4]]),     # z_cam ~ -1 < 0.1 -> all filtered
+           5: ([0.2, -0.2, 0.3], [[3, 4], [2, 5]]),              # one registered obs survives
+           11: ([0.05, 0.0, 0.2], [[4, 0], [1, 3], [0, 5], [2, 1]])}
+    trks = {k: Track(id=k, xyz=np.array(v[0]), observations=np.array(v[1])) for k, v in pts.items()}
+    res = _scene_arrays(cams, imgs, trks, model.value)
+    res.update(_run_solve(LM, cams, imgs, trks, opts))
+    np.savez_compressed(os.path.join(out_dir, "packing_edge.npz"), **res)
+    print("packing_edge.npz", res["out_points_2d"].shape)
+
+    # (3) points-only variant (track_retriangulation.py:247-249 passes optimize_poses=False)
+    opts2 = dict(opts, optimize_poses=False)
+    trks = {k: Track(id=k, xyz=np.array(v[0]), observations=np.array(v[1])) for k, v in pts.items()}
+    res = _scene_arrays(cams, imgs, trks, model.value)
+    res.update(_run_solve(LM, cams, imgs, trks, opts2))
+    np.savez_compressed(os.path.join(out_dir, "packing_edge_points_only.npz"), **res)
+    print("packing_edge_points_only.npz", res["out_points_2d"].shape)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    with tempfile.TemporaryDirectory():
+        LM = install_shims()
+        sys.path.insert(0, REF)
+        gen_projection(args.out)
+        gen_packing(args.out, LM)
+
+
+if __name__ == "__main__":
+    main()
