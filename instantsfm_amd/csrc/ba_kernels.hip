@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -235,29 +236,33 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Schur complement: one workgroup per (camera row i, chunk of its upper blocks).  The chunk of S's row lives in LDS;
-// each wave walks camera i's observations o (camera-major list), forms W^_o = W_o V_p^-1 per lane-entry, and for every
-// partner q of track p with camera j >= i in the chunk adds -W^_o W_q^T into slot(j).  Lane <-> block entry (a, b):
-// 64 lanes cover an 8x8 block.  WAVES = 1 gives a fixed accumulation order (deterministic mode).
+// Schur complement: one workgroup per (camera row i, chunk of its upper blocks); the chunk of S's row lives in LDS.
+// A group of D lanes owns one of camera i's observations o (64/D observations in flight per wave); lane b of the
+// group owns column b.  The group forms W^_o = W_o V_p^-1 (row b per lane, shared through LDS), then walks the
+// upper partners q of track p -- tracks are sorted by camera at create, so they are exactly [ustart[o], end) --
+// and adds column b of -W^_o W_q^T into slot(cam[q]) with LDS f64 atomics (ds_add_f64).  Each camera's
+// observation list is sorted by partner count so the groups of a wave stay balanced.
 // ------------------------------------------------------------------------------------------------------------
 template <int D, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
-                                                      const int* __restrict__ pt_ptr, const int* __restrict__ cam,
-                                                      const double* __restrict__ W, const double* __restrict__ Vinv,
-                                                      const double* __restrict__ y, const double* __restrict__ U,
-                                                      const double* __restrict__ gc, double f, double cmin, double cmax,
-                                                      int add_diag, double* __restrict__ S, double* __restrict__ b) {
+                                                      const int* __restrict__ pt_ptr, const int* __restrict__ ustart,
+                                                      const int* __restrict__ cam, const double* __restrict__ W,
+                                                      const double* __restrict__ Vinv, const double* __restrict__ y,
+                                                      const double* __restrict__ U, const double* __restrict__ gc, double f,
+                                                      double cmin, double cmax, int add_diag, double* __restrict__ S,
+                                                      double* __restrict__ b) {
     constexpr int DD = D * D;
-    constexpr int ENT = (DD + 63) / 64;
+    constexpr int NG = 64 / D;  // observation groups per wave
     constexpr int NT = WAVES * 64;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int4 wk = work[blockIdx.x];
     const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
     double* acc = sh;
-    double* bacc = acc + (size_t)nb * DD;
-    int* slot = reinterpret_cast<int*>(bacc + D);
+    double* wsh = acc + (size_t)nb * DD;           // [WAVES][NG][D][4]  W^ rows (padded)
+    double* bacc = wsh + (size_t)WAVES * NG * D * 4;  // [D]
+    int* slot = reinterpret_cast<int*>(bacc + D);  // [C]
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     for (int k = t; k < nb * DD; k += NT) acc[k] = 0.0;
     for (int k = t; k < C; k += NT) slot[k] = -1;
@@ -266,66 +271,87 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
     for (int e = kb + t; e < ke; e += NT) slot[col[e]] = e - kb;
     __syncthreads();
     const bool diag_chunk = (kb == row_ptr[i]);
-    int ea[ENT], ebv[ENT];
-#pragma unroll
-    for (int m = 0; m < ENT; ++m) {
-        const int ent = lane + 64 * m;
-        ea[m] = ent < DD ? ent / D : 0;
-        ebv[m] = ent < DD ? ent % D : 0;
-    }
+    const int g = lane / D, cb = lane - g * D;
+    const bool active = g < NG;
+    double* my_wh = wsh + ((size_t)(wv * NG + (active ? g : 0)) * D) * 4;
     double breg = 0.0;
     const int ob = cam_ptr[i], oe = cam_ptr[i + 1];
-    for (int e = ob + wv; e < oe; e += WAVES) {
-        const int o = cam_obs[e];
-        const int p = ptl[o];
-        const double* vi = Vinv + 6 * (size_t)p;
-        const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
-        const double* Wo = W + (size_t)o * D * 3;
-        double wh[ENT][3];
-#pragma unroll
-        for (int m = 0; m < ENT; ++m) {
-            const double w0 = Wo[ea[m] * 3 + 0], w1 = Wo[ea[m] * 3 + 1], w2 = Wo[ea[m] * 3 + 2];
-            wh[m][0] = w0 * v00 + w1 * v01 + w2 * v02;
-            wh[m][1] = w0 * v01 + w1 * v11 + w2 * v12;
-            wh[m][2] = w0 * v02 + w1 * v12 + w2 * v22;
+    for (int base = ob + wv * NG; base < oe; base += WAVES * NG) {
+        const int e = base + g;
+        const bool has = active && e < oe;
+        int qs = 0, qe = 0;
+        if (has) {
+            const int o = cam_obs[e];
+            const int p = ptl[o];
+            const double* vi = Vinv + 6 * (size_t)p;
+            const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
+            const double* wo = W + (size_t)o * D * 3 + cb * 3;
+            const double w0 = wo[0], w1 = wo[1], w2 = wo[2];
+            my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
+            my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
+            my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
+            if (diag_chunk) {
+                const double* yp = y + 3 * (size_t)p;
+                breg -= w0 * yp[0] + w1 * yp[1] + w2 * yp[2];
+            }
+            qs = ustart[o];
+            qe = pt_ptr[p + 1];
         }
-        if (diag_chunk && lane < D) {
-            const double* yp = y + 3 * (size_t)p;
-            breg -= Wo[lane * 3 + 0] * yp[0] + Wo[lane * 3 + 1] * yp[1] + Wo[lane * 3 + 2] * yp[2];
-        }
-        const int qb = pt_ptr[p], qe = pt_ptr[p + 1];
-        for (int q = qb; q < qe; ++q) {
-            const int j = cam[q];
-            if (j < i) continue;
-            const int s = slot[j];
-            if (s < 0) continue;
-            const double* Wq = W + (size_t)q * D * 3;
-            double* blk = acc + (size_t)s * DD;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        double wh[D][3];
+        if (has) {
 #pragma unroll
-            for (int m = 0; m < ENT; ++m) {
-                const int ent = lane + 64 * m;
-                if (ent < DD) {
-                    const double* wq = Wq + ebv[m] * 3;
-                    const double v = wh[m][0] * wq[0] + wh[m][1] * wq[1] + wh[m][2] * wq[2];
-                    if constexpr (WAVES == 1) blk[ent] -= v;
-                    else atomicAdd(blk + ent, -v);
+            for (int a2 = 0; a2 < D; ++a2) {
+                wh[a2][0] = my_wh[a2 * 4 + 0];
+                wh[a2][1] = my_wh[a2 * 4 + 1];
+                wh[a2][2] = my_wh[a2 * 4 + 2];
+            }
+        }
+        const int n = qe - qs;
+        int nmax = n;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
+        constexpr int UP = 4;  // partners in flight per group
+        for (int k0 = 0; k0 < nmax; k0 += UP) {
+            double x[UP][3];
+            int cj[UP];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                cj[u] = -1;
+                if (k0 + u < n) {
+                    const int q = qs + k0 + u;
+                    const double* wq = W + (size_t)q * D * 3 + cb * 3;
+                    x[u][0] = wq[0]; x[u][1] = wq[1]; x[u][2] = wq[2];
+                    cj[u] = cam[q];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UP; ++u) {
+                if (cj[u] >= 0) {
+                    const int sl = slot[cj[u]];
+                    if (sl >= 0) {
+                        double* dst = acc + (size_t)sl * DD + cb;
+#pragma unroll
+                        for (int a2 = 0; a2 < D; ++a2)
+                            atomicAdd(dst + a2 * D, -(wh[a2][0] * x[u][0] + wh[a2][1] * x[u][1] + wh[a2][2] * x[u][2]));
+                    }
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
-    if (diag_chunk && lane < D) {
-        if constexpr (WAVES == 1) bacc[lane] += breg;
-        else atomicAdd(bacc + lane, breg);
-    }
+    if (diag_chunk && active) atomicAdd(bacc + cb, breg);
     __syncthreads();
     double* Sout = S + (size_t)kb * DD;
     const double* Ui = U + (size_t)i * DD;
     for (int k = t; k < nb * DD; k += NT) {
         double v = acc[k];
         if (diag_chunk && add_diag && k < DD) {
-            const int a = k / D, bb = k % D;
+            const int a2 = k / D, bb = k % D;
             double u = Ui[k];
-            if (a == bb) u = clampd(u, cmin, cmax) * f;
+            if (a2 == bb) u = clampd(u, cmin, cmax) * f;
             v += u;
         }
         Sout[k] = v;
@@ -344,6 +370,7 @@ struct CgBufs {
     double* x;
     double* part[2];  // [nwg][3]: gamma, delta, rho
     double* hist;     // [maxit + 2][2]: alpha_i, gamma_i ; hist_bb at the end
+    double* scal;     // [4]: alpha, beta, flag of the current recurrence step (written by k_cg_dots)
     int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
 };
 
@@ -407,12 +434,17 @@ __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __rest
     }
 }
 
-// One wave per upper block: S~_ij = L_i^-1 S_ij L_j^-T (diagonal blocks -> I).
+// One wave per upper block: S~_ij = L_i^-1 S_ij L_j^-T (diagonal blocks -> I).  Off-diagonal blocks are also
+// written, padded to DP = D + (D & 1) columns, into the row-contiguous neighbour copy Sn: S~_ij at slot pos_up[e]
+// of row i and S~_ij^T at slot pos_lo[e] of row j, so the CG iteration reads every row's blocks as one
+// contiguous, 16-byte-coalesced stream.
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __restrict__ blk_row, const int* __restrict__ col,
-                                                       const int* __restrict__ row_ptr, const double* __restrict__ Li,
-                                                       double* __restrict__ S) {
+                                                       const int* __restrict__ row_ptr, const int* __restrict__ pos_up,
+                                                       const int* __restrict__ pos_lo, const double* __restrict__ Li,
+                                                       double* __restrict__ S, double* __restrict__ Sn) {
     constexpr int DD = D * D;
+    constexpr int DP = D + (D & 1);
     __shared__ double T[kWaves][DD];
     __shared__ double Sb[kWaves][DD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -437,143 +469,241 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k = lane; k < DD; k += 64) {
-        const int a = k / D, bb = k % D;
-        double s = 0.0;
-        for (int m = 0; m <= bb; ++m) s += T[wv][a * D + m] * Ljj[bb * D + m];
-        blk[k] = s;
+    double* up = Sn + (size_t)pos_up[e] * D * DP;
+    double* lo = Sn + (size_t)pos_lo[e] * D * DP;
+    for (int k = lane; k < D * DP; k += 64) {
+        const int a = k / DP, bb = k % DP;
+        double v = 0.0, vt = 0.0;
+        if (bb < D) {
+            for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Ljj[bb * D + m];
+            blk[a * D + bb] = v;
+        }
+        up[k] = v;
+        (void)vt;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // transpose: lo[a][bb] = S~_ij[bb][a]  (read back the finished block)
+    for (int k = lane; k < D * DP; k += 64) {
+        const int a = k / DP, bb = k % DP;
+        lo[k] = (bb < D) ? blk[bb * D + a] : 0.0;
     }
 }
 
 // CG iteration kernel `it` (Chronopoulos-Gear on S~; diagonal blocks of S~ are I).  it = 0 computes w0 = S~ r0 and
-// the first dots.  it >= 1 performs recurrence step i = it-1: reads dots_i (partials of kernel it-1), decides
-// convergence on the true residual rho_i = ||L r~_i||^2 <= tol^2 ||b||^2, then per row
+// the first dots.  it >= 1 performs recurrence step i = it-1: reads dots_i (per-row partials of kernel it-1), decides
+// convergence on the true residual rho_i = ||L r~_i||^2 <= tol^2 ||b||^2, then for its camera row
 //   p = r + beta p; s = w + beta s; x += alpha p; r' = r - alpha s; w' = S~ r'
-// where every neighbour's r'_j is recomputed from its previous-iteration (r, w, s) so that the whole iteration is
-// ONE launch.  Lane (g, col) of a wave handles column `col` of neighbour block g (D lanes per block, 64/D blocks
-// in flight per wave); the D row sums are butterfly-reduced across the wave.
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_cg_iter(int it, int C, int nwg, int maxit, double tol2_rel,
-                                                      const int* __restrict__ row_ptr, const int* __restrict__ col,
-                                                      const int* __restrict__ lo_ptr, const int* __restrict__ lo_col,
-                                                      const int* __restrict__ lo_blk, const double* __restrict__ S,
-                                                      const double* __restrict__ Lf, CgBufs cg) {
-    constexpr int DD = D * D;
-    constexpr int NG = 64 / D;
-    __shared__ double red[3 * kThreads];
-    __shared__ double rsh[kWaves][D];
-    __shared__ double wpart[kWaves][3];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+// where every neighbour's r'_j is recomputed from its previous-iteration (r, w, s), so one iteration = ONE launch.
+// One 512-thread workgroup per camera row.  The row's neighbour blocks are contiguous in Sn (padded D x DP); lane l of
+// a wave owns 16-byte piece (l mod PPB) of block (l / PPB): every load instruction is a contiguous 1 KiB stream.
+// Loads that do not depend on alpha / beta (blocks, neighbour vectors, partials, history, own row) are issued first.
+// Recurrence scalars for step i = it-1: one 1024-thread workgroup sums the per-row partial dots of launch it-1 in a
+// fixed order, tests convergence on the true residual and publishes {alpha, beta, flag} (+ history) for k_cg_iter.
+__global__ __launch_bounds__(1024) void k_cg_dots(int it, int C, int maxit, double tol2_rel, CgBufs cg) {
+    __shared__ double red[3][1024];
+    const int t = threadIdx.x;
     if (cg.status[0] != 0) return;
-    double alpha = 0.0, beta = 0.0;
-    const int pin = (it + 1) & 1;  // parity of index it-1 (r_{it-1}, w_{it-1}, s_{it-1})
-    const int pout = it & 1;       // parity of index it   (r_it, w_it, s_{it-2} read, part_it)
-    if (it > 0) {
-        const int i = it - 1;
-        double d3[3];
-        sum_partials<3>(cg.part[pin], nwg, d3, red);
-        const double gam = d3[0], del = d3[1], rho = d3[2];
-        const double bb = (i == 0) ? rho : cg.hist[2 * (maxit + 1)];
-        if (rho <= tol2_rel * bb || i >= maxit) {
-            if (blockIdx.x == 0 && t == 0) { cg.status[0] = 1; cg.status[1] = i; }
-            return;
-        }
-        double den;
-        if (i == 0) { beta = 0.0; den = del; }
-        else {
-            const double alpha_prev = cg.hist[2 * (i - 1)], gam_prev = cg.hist[2 * (i - 1) + 1];
-            beta = gam / gam_prev;
-            den = del - beta * gam / alpha_prev;
-        }
-        if (!(den > 0.0)) {
-            if (blockIdx.x == 0 && t == 0) { cg.status[0] = 2; cg.status[1] = i; }
-            return;
-        }
-        alpha = gam / den;
-        if (blockIdx.x == 0 && t == 0) {
-            cg.hist[2 * i] = alpha;
-            cg.hist[2 * i + 1] = gam;
-            if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
-        }
+    const int i = it - 1;
+    const double* P0 = cg.part[it & 1 ? 0 : 1];
+    const double* P1 = P0 + C;
+    const double* P2 = P1 + C;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    for (int k = t; k < C; k += 1024) { g0 += P0[k]; g1 += P1[k]; g2 += P2[k]; }
+    red[0][t] = g0; red[1][t] = g1; red[2][t] = g2;
+    __syncthreads();
+    for (int st = 512; st >= 1; st >>= 1) {
+        if (t < st) { red[0][t] += red[0][t + st]; red[1][t] += red[1][t + st]; red[2][t] += red[2][t + st]; }
+        __syncthreads();
     }
-    const int row = blockIdx.x * kWaves + wv;
+    if (t == 0) {
+        const double gam = red[0][0], del = red[1][0], rho = red[2][0];
+        const double bb = (i == 0) ? rho : cg.hist[2 * (maxit + 1)];
+        double flag = 0.0, al = 0.0, be = 0.0;
+        if (rho <= tol2_rel * bb || i >= maxit) {
+            flag = 1.0;
+            cg.status[0] = 1; cg.status[1] = i;
+        } else {
+            double den;
+            if (i == 0) { be = 0.0; den = del; }
+            else {
+                be = gam / cg.hist[2 * (i - 1) + 1];
+                den = del - be * gam / cg.hist[2 * (i - 1)];
+            }
+            if (!(den > 0.0)) {
+                flag = 2.0;
+                cg.status[0] = 2; cg.status[1] = i;
+            } else {
+                al = gam / den;
+                cg.hist[2 * i] = al;
+                cg.hist[2 * i + 1] = gam;
+                if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
+            }
+        }
+        cg.scal[0] = al; cg.scal[1] = be; cg.scal[2] = flag;
+    }
+}
+
+constexpr int kCgThreads = 512;
+constexpr int kCgWaves = kCgThreads / 64;
+
+template <int D>
+struct CgGeom {
+    static constexpr int DP = D + (D & 1);     // padded row length
+    static constexpr int HP = DP / 2;          // 16-byte pieces per block row
+    static constexpr int PPB = D * HP;         // pieces per block
+    static constexpr int BPW = PPB <= 64 ? 64 / PPB : 1;          // blocks per wave per round
+    static constexpr int PPL = PPB <= 64 ? 1 : (PPB + 63) / 64;   // pieces per lane
+    static constexpr int BPR = BPW * kCgWaves;                    // blocks per round per workgroup
+};
+
+template <int D>
+__global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit, double tol2_rel,
+                                                        const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_j,
+                                                        const double* __restrict__ Sn, const double* __restrict__ Lf,
+                                                        CgBufs cg, int probe) {
+    using G = CgGeom<D>;
+    constexpr int DD = D * D;
+    constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = G::BPR;
+    __shared__ double red[kCgWaves][BPW][PPB];
+    __shared__ double rsh[D];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int row = blockIdx.x;
+    const int pin = (it + 1) & 1;
+    const int pout = it & 1;
     const double* r_old = cg.r[it == 0 ? 0 : pin];
     const double* w_old = cg.w[pin];
-    const double* s_old = cg.s[pout];  // s_{it-2}
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    if (row < C) {
-        // own row update (lanes < D)
-        if (lane < D) {
-            const size_t idx = (size_t)row * D + lane;
-            double rn;
-            if (it == 0) {
-                rn = r_old[idx];
-            } else {
-                const double sn = w_old[idx] + beta * s_old[idx];
-                const double pn = r_old[idx] + beta * cg.p[idx];
-                cg.x[idx] += alpha * pn;
-                cg.p[idx] = pn;
-                cg.s[pin][idx] = sn;
-                rn = r_old[idx] - alpha * sn;
-                cg.r[pout][idx] = rn;
+    const double* s_old = cg.s[pout];
+    const int bw = (PPB <= 64) ? lane / PPB : 0;     // block slot within the wave
+    const int pc0 = (PPB <= 64) ? lane - bw * PPB : lane;
+    const bool lane_on = (PPB <= 64) ? (bw < BPW) : true;
+    const int slot = wv * BPW + bw;                  // block slot within the round
+    // ======== phase 1: loads independent of alpha / beta ========
+    const int status = (probe & 8) ? 0 : cg.status[0];
+    const int n0 = nbr_ptr[row], n1 = (probe & 2) ? nbr_ptr[row] : nbr_ptr[row + 1];
+    double acc[PPL];
+#pragma unroll
+    for (int m = 0; m < PPL; ++m) acc[m] = 0.0;
+    // first round prefetch
+    double s0[PPL], s1[PPL], xr0[PPL], xr1[PPL], xw0[PPL], xw1[PPL], xs0[PPL], xs1[PPL];
+    const int nfirst = n0 + slot;
+    const bool have = lane_on && nfirst < n1;
+    auto load_piece = [&](int nn, int m, double& a0, double& a1, double& r0, double& r1, double& w0, double& w1, double& q0,
+                          double& q1) {
+        const int pc = pc0 + 64 * m;
+        a0 = a1 = r0 = r1 = w0 = w1 = q0 = q1 = 0.0;
+        if (pc >= PPB) return;
+        const int b = 2 * (pc % HP);
+        const double2 sv = *reinterpret_cast<const double2*>(Sn + ((size_t)nn * D * DP + 2 * (size_t)pc));
+        a0 = sv.x; a1 = sv.y;
+        const int j = nbr_j[nn];
+        const size_t jx = (size_t)j * D + b;
+        if constexpr ((D & 1) == 0) {
+            const double2 rv = *reinterpret_cast<const double2*>(r_old + jx);
+            r0 = rv.x; r1 = rv.y;
+            if (it > 0) {
+                const double2 wv2 = *reinterpret_cast<const double2*>(w_old + jx);
+                const double2 sv2 = *reinterpret_cast<const double2*>(s_old + jx);
+                w0 = wv2.x; w1 = wv2.y; q0 = sv2.x; q1 = sv2.y;
             }
-            rsh[wv][lane] = rn;
-        }
-        // neighbour blocks
-        const int ub = row_ptr[row] + 1, ue = row_ptr[row + 1];
-        const int lb = lo_ptr[row], le = lo_ptr[row + 1];
-        const int nup = ue - ub, nbr = nup + (le - lb);
-        const int g = lane / D, cidx = lane % D;
-        double acc[D];
-#pragma unroll
-        for (int a = 0; a < D; ++a) acc[a] = 0.0;
-        if (g < NG) {
-            for (int n = g; n < nbr; n += NG) {
-                int blk, j;
-                const bool up = n < nup;
-                if (up) { blk = ub + n; j = col[blk]; }
-                else { const int k = lb + (n - nup); blk = lo_blk[k]; j = lo_col[k]; }
-                const size_t jx = (size_t)j * D + cidx;
-                const double rj = (it == 0) ? r_old[jx] : r_old[jx] - alpha * (w_old[jx] + beta * s_old[jx]);
-                const double* Sb = S + (size_t)blk * DD;
-                if (up) {
-#pragma unroll
-                    for (int a = 0; a < D; ++a) acc[a] += Sb[a * D + cidx] * rj;
-                } else {
-#pragma unroll
-                    for (int a = 0; a < D; ++a) acc[a] += Sb[cidx * D + a] * rj;
-                }
+        } else {
+            r0 = r_old[jx];
+            if (b + 1 < D) r1 = r_old[jx + 1];
+            if (it > 0) {
+                w0 = w_old[jx]; q0 = s_old[jx];
+                if (b + 1 < D) { w1 = w_old[jx + 1]; q1 = s_old[jx + 1]; }
             }
         }
+    };
+    if (have) {
 #pragma unroll
-        for (int a = 0; a < D; ++a) acc[a] = wave_sum(acc[a]);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int m = 0; m < PPL; ++m) load_piece(nfirst, m, s0[m], s1[m], xr0[m], xr1[m], xw0[m], xw1[m], xs0[m], xs1[m]);
+    }
+    // wave 0: own row and the row of L (for the true-residual norm)
+    double own_r = 0.0, own_w = 0.0, own_s = 0.0, own_p = 0.0;
+    double lrow[D];
+    const size_t own = (size_t)row * D + (lane < D ? lane : 0);
+    if (wv == 0 && lane < D) {
+        own_r = r_old[own];
+        if (it > 0) { own_w = w_old[own]; own_s = s_old[own]; own_p = cg.p[own]; }
+        const double* L = Lf + (size_t)row * DD + lane * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) lrow[k] = (k <= lane) ? L[k] : 0.0;
+    }
+    // recurrence scalars published by k_cg_dots (uniform loads)
+    double alpha = 0.0, beta = 0.0;
+    if (it > 0) {
+        if ((probe & 8) == 0 && cg.scal[2] != 0.0) return;
+        alpha = cg.scal[0];
+        beta = cg.scal[1];
+    }
+    if (status != 0) return;
+    // ======== phase 3: own row update (wave 0, lanes < D) ========
+    double rn = 0.0;
+    if (wv == 0 && lane < D) {
+        if (it == 0) {
+            rn = own_r;
+        } else {
+            const double sn = own_w + beta * own_s;
+            const double pn = own_r + beta * own_p;
+            cg.x[own] += alpha * pn;
+            cg.p[own] = pn;
+            cg.s[pin][own] = sn;
+            rn = own_r - alpha * sn;
+            cg.r[pout][own] = rn;
+        }
+        rsh[lane] = rn;
+    }
+    // ======== phase 4: neighbour blocks, streamed one round (BPR blocks) at a time ========
+    auto consume = [&](int m, double a0, double a1, double r0, double r1, double w0, double w1, double q0, double q1) {
+        const double v0 = (it == 0) ? r0 : r0 - alpha * (w0 + beta * q0);
+        const double v1 = (it == 0) ? r1 : r1 - alpha * (w1 + beta * q1);
+        acc[m] += a0 * v0 + a1 * v1;
+    };
+    if (have) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) consume(m, s0[m], s1[m], xr0[m], xr1[m], xw0[m], xw1[m], xs0[m], xs1[m]);
+    }
+    for (int nn = nfirst + BPR; lane_on && nn < n1; nn += BPR) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            load_piece(nn, m, s0[m], s1[m], xr0[m], xr1[m], xw0[m], xw1[m], xs0[m], xs1[m]);
+            consume(m, s0[m], s1[m], xr0[m], xr1[m], xw0[m], xw1[m], xs0[m], xs1[m]);
+        }
+    }
+    if (lane_on) {
+#pragma unroll
+        for (int m = 0; m < PPL; ++m) {
+            const int pc = pc0 + 64 * m;
+            if (pc < PPB) red[wv][bw][pc] = acc[m];
+        }
+    }
+    __syncthreads();
+    // ======== phase 5: w' for the row and the partial dots (wave 0) ========
+    if (wv == 0) {
+        double g0 = 0.0, g1 = 0.0, g2 = 0.0;
         if (lane < D) {
             const int a = lane;
-            double tot = acc[0];
+            double tot = 0.0;
+            for (int w = 0; w < kCgWaves; ++w)
 #pragma unroll
-            for (int k = 1; k < D; ++k) tot = (a == k) ? acc[k] : tot;
-            const double rn = rsh[wv][a];
+                for (int bb = 0; bb < BPW; ++bb)
+#pragma unroll
+                    for (int k = 0; k < HP; ++k) tot += red[w][bb][a * HP + k];
             const double wn = rn + tot;
-            const size_t idx = (size_t)row * D + a;
-            cg.w[pout][idx] = wn;
-            const double* L = Lf + (size_t)row * DD;
+            cg.w[pout][own] = wn;
             double lr = 0.0;
-            for (int k = 0; k <= a; ++k) lr += L[a * D + k] * rsh[wv][k];
+#pragma unroll
+            for (int k = 0; k < D; ++k) lr += lrow[k] * rsh[k];
             g0 = rn * rn;
             g1 = wn * rn;
             g2 = lr * lr;
         }
-    }
-    g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
-    if (lane == 0) { wpart[wv][0] = g0; wpart[wv][1] = g1; wpart[wv][2] = g2; }
-    __syncthreads();
-    if (t == 0) {
-        double a0 = 0, a1 = 0, a2 = 0;
-        for (int k = 0; k < kWaves; ++k) { a0 += wpart[k][0]; a1 += wpart[k][1]; a2 += wpart[k][2]; }
-        double* pp = cg.part[pout] + 3 * (size_t)blockIdx.x;
-        pp[0] = a0; pp[1] = a1; pp[2] = a2;
+        g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+        if (lane == 0) {
+            double* pp = cg.part[pout];
+            pp[row] = g0; pp[C + row] = g1; pp[2 * (size_t)C + row] = g2;
+        }
     }
 }
 
@@ -733,7 +863,11 @@ struct insfm_ba {
     // structure (device)
     double *uv = nullptr, *pp = nullptr;
     int *cam = nullptr, *ptl = nullptr, *pt_ptr = nullptr, *cam_ptr = nullptr, *cam_obs = nullptr;
-    int *row_ptr = nullptr, *col = nullptr, *lo_ptr = nullptr, *lo_col = nullptr, *lo_blk = nullptr, *blk_row = nullptr;
+    int *row_ptr = nullptr, *col = nullptr, *blk_row = nullptr, *ustart = nullptr;
+    int *nbr_ptr = nullptr, *nbr_j = nullptr, *pos_up = nullptr, *pos_lo = nullptr;
+    double* Sn = nullptr;  // row-contiguous scaled neighbour blocks for the CG (both triangles, padded rows)
+    int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
+    int64_t n_nbr = 0;
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
@@ -891,11 +1025,13 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             constexpr int DV = decltype(dc_)::value;
             if (h->d.deterministic)
                 k_schur<DV, 1><<<h->nwork, 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->cam, h->W, h->Vinv, h->y,
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
             else
                 k_schur<DV, 4><<<h->nwork, 256, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->cam, h->W, h->Vinv, h->y,
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
             return launch_err(h, "k_schur");
         });
@@ -907,7 +1043,8 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg);
-            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr, h->Li, h->S);
+            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
+                                                                            h->pos_up, h->pos_lo, h->Li, h->S, h->Sn);
             return launch_err(h, "k_cg_factor/scale");
         });
         if (rc) return rc;
@@ -922,9 +1059,11 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             rec(h, 8);
             rc = with_D(D, [&](auto dc_) -> int {
                 constexpr int DV = decltype(dc_)::value;
-                for (int k = it; k < stop; ++k)
-                    k_cg_iter<DV><<<h->cg_nwg, kThreads, 0, h->stream>>>(k, h->C, h->cg_nwg, maxit, tol2, h->row_ptr, h->col,
-                                                                       h->lo_ptr, h->lo_col, h->lo_blk, h->S, h->Lf, h->cg);
+                for (int k = it; k < stop; ++k) {
+                    if (k > 0) k_cg_dots<<<1, 1024, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
+                    k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(k, h->C, maxit, tol2, h->nbr_ptr, h->nbr_j, h->Sn,
+                                                                    h->Lf, h->cg, h->probe);
+                }
                 return launch_err(h, "k_cg_iter");
             });
             if (rc) return rc;
@@ -1062,16 +1201,35 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     h->o0 = gptr[h->p0];
     h->Nl = gptr[h->p1] - h->o0;
     const int o0 = h->o0, Nl = h->Nl, Pl = h->Pl;
-    // local arrays
-    std::vector<int> lptr(Pl + 1), lptl(Nl), lcam(Nl);
+    // local arrays; each track's observations are reordered by camera (stable) so that the upper-triangle partners
+    // of an observation are the contiguous tail [ustart[o], track end) of its track
+    std::vector<int> lptr(Pl + 1), lptl(Nl), lcam(Nl), lsrc(Nl), lust(Nl);
     for (int p = 0; p <= Pl; ++p) lptr[p] = gptr[h->p0 + p] - o0;
-    for (int o = 0; o < Nl; ++o) { lptl[o] = pt_idx[o0 + o] - h->p0; lcam[o] = cam_idx[o0 + o]; }
+    for (int p = 0; p < Pl; ++p) {
+        const int b0 = lptr[p], b1 = lptr[p + 1];
+        for (int o = b0; o < b1; ++o) lsrc[o] = o0 + o;
+        std::stable_sort(lsrc.begin() + b0, lsrc.begin() + b1, [&](int x, int y) { return cam_idx[x] < cam_idx[y]; });
+        for (int o = b0; o < b1; ++o) {
+            lcam[o] = cam_idx[lsrc[o]];
+            lptl[o] = p;
+        }
+        for (int o = b0; o < b1; ++o) {
+            int u = o;
+            while (u > b0 && lcam[u - 1] == lcam[o]) --u;
+            lust[o] = u;
+        }
+    }
     std::vector<int> cptr(C + 1, 0), cobs(Nl);
     for (int o = 0; o < Nl; ++o) cptr[lcam[o] + 1]++;
     for (int c = 0; c < C; ++c) cptr[c + 1] += cptr[c];
     {
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
         for (int o = 0; o < Nl; ++o) cobs[fill[lcam[o]]++] = o;
+        // balance the Schur groups: within a camera, observations with more upper partners first
+        for (int c = 0; c < C; ++c)
+            std::stable_sort(cobs.begin() + cptr[c], cobs.begin() + cptr[c + 1], [&](int x, int y) {
+                return (lptr[lptl[x] + 1] - lust[x]) > (lptr[lptl[y] + 1] - lust[y]);
+            });
     }
     // global upper pattern (identical on every rank)
     std::vector<int> gcptr(C + 1, 0), gcobs(N);
@@ -1119,8 +1277,21 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
                 loblk[k] = e;
             }
     }
+    // flattened CG neighbour list per row: upper blocks then lower (transposed) ones; pos_up/pos_lo give each upper
+    // block's two slots in the row-contiguous copy Sn
+    std::vector<int> nptr(C + 1, 0), nj, pup(std::max(1, h->nnzb), -1), plo(std::max(1, h->nnzb), -1);
+    nj.reserve(2 * (size_t)h->nnzb);
+    for (int i = 0; i < C; ++i) {
+        for (int e = rptr[i] + 1; e < rptr[i + 1]; ++e) { pup[e] = (int)nj.size(); nj.push_back(cols[e]); }
+        for (int k = lop[i]; k < lop[i + 1]; ++k) { plo[loblk[k]] = (int)nj.size(); nj.push_back(locol[k]); }
+        nptr[i + 1] = (int)nj.size();
+    }
+    h->n_nbr = (int64_t)nj.size();
+    for (int i = 0; i < C; ++i) { pup[rptr[i]] = 0; plo[rptr[i]] = 0; }  // diagonal blocks: unused slots
+    if (nj.empty()) nj.push_back(0);
     // Schur work items: split long rows so a chunk fits the LDS budget
-    const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + 64;
+    const size_t wsh_lds = sizeof(double) * 4 * (64 / D) * D * 4;  // W^ staging for up to 4 waves
+    const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
     const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * D * D));
     std::vector<int4> work;
@@ -1138,12 +1309,15 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     }
     h->nwork = (int)work.size();
     h->max_chunk = maxc;
-    h->schur_lds = sizeof(double) * ((size_t)maxc * D * D + D) + sizeof(int) * (size_t)C;
+    h->schur_lds = sizeof(double) * ((size_t)maxc * D * D + D) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
 
     int rc;
     std::vector<double> uvl((size_t)2 * Nl);
-    std::memcpy(uvl.data(), obs_uv + 2 * (size_t)o0, sizeof(double) * 2 * Nl);
+    for (int o = 0; o < Nl; ++o) {
+        uvl[2 * (size_t)o] = obs_uv[2 * (size_t)lsrc[o]];
+        uvl[2 * (size_t)o + 1] = obs_uv[2 * (size_t)lsrc[o] + 1];
+    }
     if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pp, pp, (size_t)2 * C))) return fail(rc, "");
     if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
@@ -1154,9 +1328,16 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     if ((rc = upload(h, &h->row_ptr, rptr.data(), rptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->col, cols.data(), cols.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->blk_row, brow.data(), brow.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->lo_ptr, lop.data(), lop.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->lo_col, locol.data(), locol.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->lo_blk, loblk.data(), loblk.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->ustart, lust.data(), lust.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->nbr_ptr, nptr.data(), nptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->nbr_j, nj.data(), nj.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->pos_up, pup.data(), pup.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->pos_lo, plo.data(), plo.size()))) return fail(rc, "");
+    {
+        const int DPd = D + (D & 1);
+        if ((rc = dalloc(h, (void**)&h->Sn, sizeof(double) * (size_t)std::max<int64_t>(h->n_nbr, 1) * D * DPd)))
+            return fail(rc, "");
+    }
     if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
     auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
     if ((rc = dd(&h->W, (size_t)Nl * D * 3))) return fail(rc, "");
@@ -1175,9 +1356,9 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     if ((rc = dd(&h->Lf, (size_t)C * D * D))) return fail(rc, "");
     if ((rc = dd(&h->Li, (size_t)C * D * D))) return fail(rc, "");
     if ((rc = dd(&h->dc, (size_t)C * D))) return fail(rc, "");
-    h->cg_nwg = cdiv(C, kWaves);
+    h->cg_nwg = C;  // one workgroup (and one partial record) per camera row
     const size_t cd = (size_t)C * D;
-    const size_t cgn = 8 * cd + 2 * 3 * (size_t)h->cg_nwg + 2 * ((size_t)desc->pcg_max_iter + 2) + 8;
+    const size_t cgn = 8 * cd + 2 * 3 * (size_t)h->cg_nwg + 2 * ((size_t)desc->pcg_max_iter + 2) + 16;
     if ((rc = dd(&h->cgmem, cgn))) return fail(rc, "");
     {
         double* m = h->cgmem;
@@ -1187,6 +1368,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         h->cg.p = m; m += cd; h->cg.x = m; m += cd;
         h->cg.part[0] = m; m += 3 * (size_t)h->cg_nwg; h->cg.part[1] = m; m += 3 * (size_t)h->cg_nwg;
         h->cg.hist = m; m += 2 * ((size_t)desc->pcg_max_iter + 2);
+        h->cg.scal = m; m += 4;
     }
     if ((rc = dalloc(h, (void**)&h->cg.status, sizeof(int) * 4))) return fail(rc, "");
     const int ST = h->stride;
@@ -1224,6 +1406,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         return 0;
     });
+    if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
     h->damping = 1.0 / desc->tr_radius;
     h->down = desc->tr_down;
     *out = h;
