@@ -34,11 +34,10 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
                 + nnzb * D * D * 8     # S (upper blocks) written
                 + C * D * 8)           # b written
     if kernel == "k_cg_iter":
-        nlo = nnzb - C
-        return (nnzb * D * D * 8       # S~ upper blocks (diag blocks are I and never read)
-                - C * D * D * 8
+        off = nnzb - C                 # off-diagonal upper blocks (diagonal blocks of S~ are I and never read)
+        return (off * D * D * 8        # S~ read once (the kernel streams a full copy: 2x this)
                 + C * D * D * 8        # L_i (true-residual norm)
-                + (C + 1) * 4 * 2 + (nnzb - C) * 4 + nlo * 8   # row_ptr/lo_ptr, col, lo_col+lo_blk
+                + (C + 1) * 4 + 2 * off * 4   # nbr_ptr, nbr_j
                 + 10 * C * D * 8)      # r, w, s, p, x read + written
     raise ValueError(kernel)
 
@@ -138,24 +137,40 @@ def main():
             conv_step = k
             break
 
+    # ---- outside the timed region: per-phase breakdown (instrumented replay) and per-kernel device times ----
+    eng.reset()
+    ci, pi = cams0.clone(), pts0.clone()
+    eng.set_timing(True)
+    istats = [eng.step(ci, pi)[1] for _ in range(args.steps)]
+    eng.set_timing(False)
+    us_cg = eng.debug_time_kernel(0, 100)
+    us_schur = eng.debug_time_kernel(1, 5)
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
     nnzb = eng.nnzb()
-    ph = np.sum([s["time_ms"] for s in stats], axis=0)
+    ph = np.sum([s["time_ms"] for s in istats], axis=0)
     trials = sum(s["trials"] for s in stats)
     cg_launches = sum(s["cg_launches"] for s in stats)
     kern = {
-        "k_schur": (ph[1], trials, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb)),
-        "k_cg_iter": (ph[5], cg_launches, algorithmic_bytes("k_cg_iter", C, Pl, Nl, D, nnzb)),
+        "k_cg_iter": (us_cg * cg_launches, cg_launches, us_cg, algorithmic_bytes("k_cg_iter", C, Pl, Nl, D, nnzb)),
+        "k_schur": (us_schur * trials, trials, us_schur, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb)),
     }
     name = max(kern, key=lambda k: kern[k][0])
-    tot_ms, launches, nbytes = kern[name]
-    avg_s = tot_ms / 1e3 / max(launches, 1)
-    achieved = nbytes / avg_s / 1e9 if avg_s > 0 else 0.0
+    _, launches, avg_us, nbytes = kern[name]
+    achieved = nbytes / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0
+    traffic = None
+    try:
+        with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
+            tr = json.load(f)
+        if tr.get("config") == args.config and name in tr.get("kernels", {}):
+            traffic = tr["kernels"][name]["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
     roof = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": int(nbytes), "launches": int(launches)}
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(nbytes), "launches_per_run": int(launches),
+            "timing": "hipEvents on the library stream around 100 back-to-back launches (insfm_ba_debug_time_kernel)"}
 
     out = {
         "metric": "LM-BA iterations/sec (+ final reprojection RMSE)",
@@ -180,7 +195,9 @@ def main():
         "pcg_iters": [s["pcg_iters"] for s in stats],
         "trials": trials,
         "phase_ms_per_step": {k: round(float(v) / args.steps, 3) for k, v in
-                              zip(["linearize", "k_schur", "linear_solve", "backsub_update", "trial_cost", "k_cg_iter"], ph)},
+                              zip(["linearize", "k_schur", "linear_solve", "backsub_update", "trial_cost",
+                                   "cg_iterations"], ph)},
+        "kernel_us": {"k_cg_iter": round(us_cg, 3), "k_schur": round(us_schur, 2)},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

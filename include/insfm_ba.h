@@ -72,7 +72,8 @@ typedef struct {
     double time_ms[8];      /* device time per phase (hipEvent on the library stream), filled when stats != NULL:
                                [0] linearize  [1] k_schur  [2] whole linear solve (point prep .. CG finish, incl. the
                                host polls of the CG status)  [3] back-substitution + update  [4] trial cost
-                               [5] k_cg_iter launches only (back-to-back chunks, no host gaps)  [6..7] 0 */
+                               [5] CG iteration launches (k_cg_dots + k_cg_iter chunks, no host gaps)  [6..7] 0
+                               Only filled after insfm_ba_set_timing(h, 1): the events cost a little. */
 } insfm_ba_stats;
 
 /* Fill `desc` with the reference's defaults (TorchBA + BUNDLE_ADJUSTER_OPTIONS, config/colmap.py:47-54). */
@@ -88,6 +89,9 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
  * points [P,3] are DEVICE pointers, read at the start and updated in place at the end (on a multi-rank run each
  * rank updates only its shard's points).  `stats` may be NULL.  Blocks for one 64-byte device->host copy per trial. */
 int insfm_ba_step(insfm_ba* h, double* cam_params, double* points, insfm_ba_stats* stats);
+
+/* Enable (1) / disable (0, default) the per-phase hipEvent timing reported in insfm_ba_stats.time_ms. */
+int insfm_ba_set_timing(insfm_ba* h, int32_t on);
 
 /* Robust loss and raw reprojection RMSE (sqrt(sum ||r||^2 / N)) at the given DEVICE parameters. */
 int insfm_ba_cost(insfm_ba* h, const double* cam_params, const double* points, double* loss, double* rmse);
@@ -112,6 +116,9 @@ int insfm_ba_debug_solve(insfm_ba* h, double f);
 /* Copy an internal buffer to HOST memory: 0 W[N,D,3] 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
  * solve)[nnzb,D,D] 6 b[C,D] 7 dc[C,D] 8 dp[P,3].  Returns the number of doubles copied or a negative code. */
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
+/* Device time per launch (us, hipEvents on the library stream) of `reps` back-to-back launches of one kernel on the
+ * data of the last solve: which = 0 k_cg_iter (one CG iteration), 1 k_schur.  Overwrites CG scratch state. */
+int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch);
 /* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */
 int64_t insfm_ba_nnzb(const insfm_ba* h);
 

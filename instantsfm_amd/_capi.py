@@ -52,7 +52,8 @@ class Stats(ctypes.Structure):
 # exported symbols (every one declared in include/insfm_ba.h)
 SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
-           "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange")
+           "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
+           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing")
 
 _lib = None
 
@@ -99,6 +100,10 @@ def load(path=LIB_PATH):
     L.insfm_ba_exchange_count.restype = ctypes.c_int64
     L.insfm_ba_set_exchange.argtypes = [vp, vp, ctypes.c_int64]
     L.insfm_ba_set_exchange.restype = ctypes.c_int
+    L.insfm_ba_debug_time_kernel.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, dp]
+    L.insfm_ba_debug_time_kernel.restype = ctypes.c_int
+    L.insfm_ba_set_timing.argtypes = [vp, ctypes.c_int32]
+    L.insfm_ba_set_timing.restype = ctypes.c_int
     _lib = L
     return L
 

@@ -833,17 +833,22 @@ __global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict
     if (threadIdx.x == 0) { part[2 * (size_t)blockIdx.x] = v[0]; part[2 * (size_t)blockIdx.x + 1] = v[1]; }
 }
 
-// result[0..3] = {loss, sum ||r||^2, gain_points, gain_cams}; fixed-order sums of the partial arrays.
+// result[0..4] = {loss, sum ||r||^2, gain_points, gain_cams, #non-PD point blocks}; fixed-order sums of the partials.
+// All five are summed across ranks, so every rank takes the same accept / reject / fail branch.
 __global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ cost_part, int ncost,
                                                     const double* __restrict__ gp_part, int ngp,
-                                                    const double* __restrict__ gc_part, int ngc, double* __restrict__ result) {
+                                                    const double* __restrict__ gc_part, int ngc, const int* __restrict__ flags,
+                                                    double* __restrict__ result) {
     __shared__ double red[2 * kThreads];
     double c2[2];
     sum_partials<2>(cost_part, ncost, c2, red);
     double a[1], b[1];
     if (gp_part) sum_partials<1>(gp_part, ngp, a, red); else a[0] = 0.0;
     if (gc_part) sum_partials<1>(gc_part, ngc, b, red); else b[0] = 0.0;
-    if (threadIdx.x == 0) { result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0]; }
+    if (threadIdx.x == 0) {
+        result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0];
+        result[4] = (double)flags[0];
+    }
 }
 
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
@@ -885,7 +890,7 @@ struct insfm_ba {
     int n_cost = 0, n_gp = 0, n_gc = 0;
     double* result = nullptr;
     int* flags = nullptr;
-    double* host_res = nullptr;  // pinned 128 B: result[0..3] | flags (ints, slot 4-5) | cg status (ints, slot 8)
+    double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
     std::vector<void*> allocs;
     // LM state
     double damping = 0.0, down = 0.0, loss = 0.0;
@@ -896,6 +901,7 @@ struct insfm_ba {
     // device time of the current step, accumulated per phase (ms): see insfm_ba_stats.time_ms
     double tms[8]{};
     int cg_launches = 0;
+    bool want_timing = false;       // insfm_ba_set_timing: hipEvent phase timing inside insfm_ba_step
 };
 
 namespace {
@@ -1113,14 +1119,13 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
             k_cost<M><<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
                                                              h->d.huber_delta, h->part_cost);
         k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
-                                               h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->result);
+                                               h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result);
         return launch_err(h, "k_cost/k_final");
     });
     if (rc) return rc;
-    rc = allreduce(h, h->result, 4);
+    rc = allreduce(h, h->result, 5);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 4, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipMemcpyAsync(h->host_res + 4, h->flags, sizeof(int) * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -1413,6 +1418,12 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     return INSFM_BA_OK;
 }
 
+int insfm_ba_set_timing(insfm_ba* h, int32_t on) {
+    if (!h) return INSFM_BA_EINVAL;
+    h->want_timing = on != 0;
+    return INSFM_BA_OK;
+}
+
 int64_t insfm_ba_exchange_count(const insfm_ba* h) { return h ? h->xcount : -1; }
 
 int insfm_ba_set_exchange(insfm_ba* h, double* buf, int64_t count) {
@@ -1438,6 +1449,7 @@ int insfm_ba_reset(insfm_ba* h) {
 
 int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* loss, double* rmse) {
     if (!h || !cams || !pts) return INSFM_BA_EINVAL;
+    HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
     int rc = run_cost(h, cams, pts + 3 * (size_t)h->p0, false);
     if (rc) return rc;
     if (loss) *loss = h->host_res[0];
@@ -1450,7 +1462,7 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
     const int C = h->C, ST = h->stride;
     const size_t cam_bytes = sizeof(double) * (size_t)C * ST;
     const size_t pt_bytes = sizeof(double) * (size_t)h->Pl * 3;
-    h->timing = st != nullptr;
+    h->timing = st != nullptr && h->want_timing;
     for (auto& v : h->tms) v = 0.0;
     h->cg_launches = 0;
     HIPCHK(hipMemcpyAsync(h->cams_cur, cams_user, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
@@ -1487,8 +1499,7 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
             acc_time(h, 4, 5, 4);
             rec(h, 1);  // the next trial starts here
         }
-        const int* flags = reinterpret_cast<const int*>(h->host_res + 4);
-        if (flags[0]) { failed = 1; h->loss = last; break; }
+        if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
         pcg_last = it;
         pcg_total += it;
         const double loss_new = h->host_res[0];
@@ -1547,6 +1558,35 @@ int insfm_ba_debug_solve(insfm_ba* h, double f) {
     int it = run_solve(h, f, h->cams_cur, h->pts_cur);
     HIPCHK(hipStreamSynchronize(h->stream));
     return it;
+}
+
+int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch) {
+    if (!h || reps <= 0 || !us_per_launch || !h->d.optimize_poses) return INSFM_BA_EINVAL;
+    // re-run one kernel `reps` times back to back on the data of the last solve; the CG state it overwrites is
+    // scratch once the solve has finished (dc already extracted).  0: k_cg_iter  1: k_schur (damping factor 1)
+    HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+    HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
+    HIPCHK(hipEventRecord(h->ev[10], h->stream));
+    int rc = with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        for (int r = 0; r < reps; ++r) {
+            if (which == 0)
+                k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
+                                                                h->Lf, h->cg, 0);
+            else
+                k_schur<DV, 4><<<h->nwork, 256, h->schur_lds, h->stream>>>(
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->Vinv, h->y, h->U, h->gc, 1.0, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+        }
+        return launch_err(h, "debug_time_kernel");
+    });
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(h->ev[11], h->stream));
+    HIPCHK(hipEventSynchronize(h->ev[11]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->ev[10], h->ev[11]));
+    *us_per_launch = 1e3 * ms / reps;
+    return INSFM_BA_OK;
 }
 
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {

@@ -18,6 +18,37 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
                    pcg_max_iter=500)
 
 
+def make_allreduce_callback(get_buffer, group=None, errors=None):
+    """The C ABI's allreduce callback (insfm_ba_allreduce_fn) over torch.distributed.
+
+    The library only ever passes sub-ranges of the exchange tensor returned by ``get_buffer()``; the slice is summed
+    in place across ranks.  RCCL ("nccl") reduces the device tensor directly on the current stream (the library's
+    stream); gloo reduces a host copy (pinned), which also lets several ranks share one GPU in tests.
+    """
+    import torch.distributed as dist
+
+    def _allreduce(ctx, ptr, count):
+        try:
+            buf = get_buffer()
+            addr = ctypes.cast(ptr, ctypes.c_void_p).value
+            off = (addr - buf.data_ptr()) // buf.element_size()
+            if off < 0 or off + count > buf.numel():
+                raise ValueError("allreduce range outside the exchange buffer")
+            view = buf[off:off + count]
+            if view.is_cuda and dist.get_backend(group) == "gloo":
+                host = view.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+                view.copy_(host)
+            else:
+                dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
+            return 0
+        except Exception as e:  # surfaced to the caller as INSFM_BA_ECOMM
+            if errors is not None:
+                errors.append(e)
+            return -1
+    return _allreduce
+
+
 def _require_gpu(device):
     dev = torch.device(device)
     if dev.type != "cuda":
@@ -51,20 +82,9 @@ class BundleAdjuster:
         d.shard_point_begin, d.shard_point_end = (0, -1) if shard is None else (int(shard[0]), int(shard[1]))
         self._xbuf = None
         self._cb = None
+        self._errors = []
         if world_size > 1:
-            import torch.distributed as dist
-            group = process_group
-
-            def _allreduce(ctx, ptr, count):
-                try:
-                    base = self._xbuf.data_ptr()
-                    off = (ctypes.cast(ptr, ctypes.c_void_p).value - base) // 8
-                    dist.all_reduce(self._xbuf[off:off + count], op=dist.ReduceOp.SUM, group=group)
-                    return 0
-                except Exception as e:  # pragma: no cover - surfaced as INSFM_BA_ECOMM
-                    self._cb_error = e
-                    return -1
-            self._cb = _capi.ALLREDUCE_FN(_allreduce)
+            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors))
             d.allreduce = self._cb
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
@@ -122,6 +142,10 @@ class BundleAdjuster:
                                              self._ptr(points, (self.n_points, 3)), ctypes.byref(loss), ctypes.byref(rmse)))
         return loss.value, rmse.value
 
+    def set_timing(self, on):
+        """Per-phase hipEvent timing in the step stats (off by default)."""
+        _capi.check(self._h, _capi.load().insfm_ba_set_timing(self._h, int(bool(on))))
+
     def reset(self):
         _capi.check(self._h, _capi.load().insfm_ba_reset(self._h))
 
@@ -133,6 +157,12 @@ class BundleAdjuster:
 
     def debug_solve(self, f):
         return _capi.check(self._h, _capi.load().insfm_ba_debug_solve(self._h, float(f)))
+
+    def debug_time_kernel(self, which, reps=50):
+        """Average device time (us) of `reps` back-to-back launches of k_cg_iter (0) or k_schur (1)."""
+        us = ctypes.c_double()
+        _capi.check(self._h, _capi.load().insfm_ba_debug_time_kernel(self._h, int(which), int(reps), ctypes.byref(us)))
+        return us.value
 
     def nnzb(self):
         return int(_capi.load().insfm_ba_nnzb(self._h))

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Track-sharded multi-rank LM vs the single-GPU LM on the same scene.
+
+    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
+        tools/dist_check.py --backend gloo --config 1 --steps 6
+
+Every rank builds the same seeded scene, owns a contiguous range of tracks (instantsfm_amd.shard.shard_ranges) and
+steps the shared LM; the camera system is summed across ranks through the engine's all-reduce callback.  Rank 0 then
+re-runs the problem on one GPU and prints the largest relative differences as one JSON line.  With --backend gloo the
+ranks may share one GPU (the 1-GPU test box); with nccl (RCCL) each rank needs its own GPU.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from instantsfm_amd.engine import BundleAdjuster  # noqa: E402
+from instantsfm_amd.shard import shard_ranges  # noqa: E402
+from instantsfm_amd.synth import make_config, make_problem  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", default="gloo")
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--small", action="store_true")
+    ap.add_argument("--steps", type=int, default=6)
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0")
+    args = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", 0 if args.same_device else local)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(args.backend)
+    prob = make_problem(24, 900, seed=9) if args.small else make_config(args.config)
+    shards = shard_ranges(prob.pt_idx, prob.n_points, world)
+    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
+                         world_size=world, rank=rank, shard=shards[rank], deterministic=True)
+    cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
+    pts = torch.from_numpy(prob.points_init.copy()).to(dev)
+    losses = []
+    for _ in range(args.steps):
+        losses.append(eng.step(cams, pts)[0])
+    loss, rmse = eng.cost(cams, pts)
+    # every rank updated only its own tracks: assemble the full point array
+    p0, p1 = shards[rank]
+    mask = torch.zeros_like(pts)
+    mask[p0:p1] = 1.0
+    full = (pts * mask).contiguous()
+    if args.backend == "gloo" and full.is_cuda:
+        host = full.cpu()
+        dist.all_reduce(host)
+        full = host
+    else:
+        dist.all_reduce(full)
+        full = full.cpu()
+    cams_all = [torch.zeros_like(cams).cpu() for _ in range(world)]
+    dist.all_gather(cams_all, cams.cpu()) if args.backend == "gloo" else None
+    if rank == 0:
+        ref = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
+                             device=dev, deterministic=True)
+        rc = torch.from_numpy(prob.cams_init.copy()).to(dev)
+        rp = torch.from_numpy(prob.points_init.copy()).to(dev)
+        ref_losses = [ref.step(rc, rp)[0] for _ in range(args.steps)]
+        _, ref_rmse = ref.cost(rc, rp)
+        rcn, rpn = rc.cpu().numpy(), rp.cpu().numpy()
+
+        def rel(a, b):
+            return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+        out = dict(world=world, backend=args.backend, shards=shards,
+                   loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
+                   cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
+                   rmse=rmse, ref_rmse=ref_rmse,
+                   cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all) if cams_all else None)
+        print(json.dumps(out), flush=True)
+        ok = out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7
+        if not ok:
+            print("MISMATCH", file=sys.stderr)
+    dist.barrier()
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
