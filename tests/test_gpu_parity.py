@@ -154,3 +154,37 @@ def test_config3_first_step_and_properties():
     assert abs(lg - lo) / lo < 1e-10
     assert rel(cg.cpu().numpy(), co) < 1e-8
     assert rel(pg.cpu().numpy(), po) < 1e-8
+
+
+@pytest.mark.parametrize("model", (2, 4))
+def test_torchba_solve_end_to_end(model):
+    """TorchBA.Solve on scene objects (reference API, bundle_adjustment.py:44-154) vs the oracle LM on the same
+    packed problem: same number of LM steps, same written-back points / poses / intrinsics."""
+    from instantsfm_amd.config.colmap import BUNDLE_ADJUSTER_OPTIONS
+    from instantsfm_amd.processors.bundle_adjustment import TorchBA, pack, _pose_matrices
+    from instantsfm_amd.synth import to_scene
+    prob = make_problem(24, 1200, seed=13, model=model)
+    cameras, images, tracks = to_scene(prob)
+    pk = pack(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)
+    ba = TorchBA(device="cuda:0")
+    ba.Solve(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
+    ora = O.OracleBA(pk.model.value, pk.points_2d, pk.camera_indices, pk.point_indices, pk.camera_pps,
+                     pk.camera_params.shape[0], pk.points_3d.shape[0])
+    c, p = pk.camera_params.copy(), pk.points_3d.copy()
+    hist = []
+    for _ in range(BUNDLE_ADJUSTER_OPTIONS['max_num_iterations']):
+        hist.append(ora.step(c, p))
+        if len(hist) >= 8:
+            a, b = np.mean(hist[-4:]), np.mean(hist[-8:-4])
+            if abs((b - a) / b) < 5e-4 or hist[-1] == hist[-2]:
+                break
+    assert len(ba.loss_history) == len(hist)
+    assert abs(ba.loss_history[-1] - hist[-1]) / hist[-1] < 1e-9
+    xyz = np.stack([tracks[pk.track_keys[i]].xyz for i in pk.unique_points])
+    assert rel(xyz, p) < 1e-8
+    M = _pose_matrices(c[:, :7])
+    for i, image_id in enumerate(pk.unique_cameras):
+        assert np.max(np.abs(images[image_id].world2cam - M[i])) < 1e-8 * max(1.0, np.max(np.abs(M[i])))
+        full = np.asarray(cameras[images[image_id].cam_id].params)
+        rest = [k for k in range(full.size) if k not in pk.pp_indices - 7]
+        assert rel(full[rest], c[i, 7:]) < 1e-8
