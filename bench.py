@@ -2,7 +2,8 @@
 """LM-BA iterations/sec + final reprojection RMSE on the synthetic 1k-camera / 200k-point / 2M-observation scene
 (BASELINE.json configs[2]; configs[3] when run on N GPUs: the same scene track-sharded, strong scaling).
 
-A "step" is one LM step (bae.optim.LM.step semantics: linearize, damped Schur solve with block-Jacobi PCG, trial,
+A "step" is one LM step (bae.optim.LM.step semantics: linearize, damped Schur solve with PCG (two-level by default, --precond 0 for
+the reference's block-Jacobi), trial,
 TrustRegion accept/reject) over the whole scene.  Inputs are resident in HBM before the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
@@ -39,6 +40,12 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
                 + C * D * D * 8        # L_i (true-residual norm)
                 + (C + 1) * 4 + 2 * off * 4   # nbr_ptr, nbr_j
                 + 10 * C * D * 8)      # r, w, s, p, x read + written
+    if kernel == "k_tl_spmv":
+        off = nnzb - C
+        return (off * D * D * 8        # S~ read once (the kernel streams the full-row copy: 2x this)
+                + (C + 1) * 4 + 2 * off * 4   # nbr_ptr, nbr_j
+                + 3 * C * D * 8        # u, r read; w written
+                + 2 * C * 8)           # row partials written
     raise ValueError(kernel)
 
 
@@ -73,6 +80,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
+    ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
     args = ap.parse_args()
 
     import numpy as np
@@ -97,7 +105,8 @@ def main():
     prob = make_config(args.config, seed=args.seed)
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
-                         deterministic=args.deterministic, world_size=world, rank=rank, shard=shards[rank])
+                         deterministic=args.deterministic, world_size=world, rank=rank, shard=shards[rank],
+                         precond=args.precond)
     cams0 = torch.from_numpy(prob.cams_init).to(dev)
     pts0 = torch.from_numpy(prob.points_init).to(dev)
     cams, pts = cams0.clone(), pts0.clone()
@@ -143,8 +152,11 @@ def main():
     eng.set_timing(True)
     istats = [eng.step(ci, pi)[1] for _ in range(args.steps)]
     eng.set_timing(False)
-    us_cg = eng.debug_time_kernel(0, 100)
+    tl = args.precond == 1
+    us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
     us_schur = eng.debug_time_kernel(1, 5)
+    us_tl_iter = eng.debug_time_kernel(2, 50) if tl else None
+    us_tl_setup = eng.debug_time_kernel(4, 10) if tl else None
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
@@ -153,7 +165,8 @@ def main():
     trials = sum(s["trials"] for s in stats)
     cg_launches = sum(s["cg_launches"] for s in stats)
     kern = {
-        "k_cg_iter": (us_cg * cg_launches, cg_launches, us_cg, algorithmic_bytes("k_cg_iter", C, Pl, Nl, D, nnzb)),
+        ("k_tl_spmv" if tl else "k_cg_iter"): (us_cg * cg_launches, cg_launches, us_cg,
+                                               algorithmic_bytes("k_tl_spmv" if tl else "k_cg_iter", C, Pl, Nl, D, nnzb)),
         "k_schur": (us_schur * trials, trials, us_schur, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb)),
     }
     name = max(kern, key=lambda k: kern[k][0])
@@ -197,7 +210,10 @@ def main():
         "phase_ms_per_step": {k: round(float(v) / args.steps, 3) for k, v in
                               zip(["linearize", "k_schur", "linear_solve", "backsub_update", "trial_cost",
                                    "cg_iterations"], ph)},
-        "kernel_us": {"k_cg_iter": round(us_cg, 3), "k_schur": round(us_schur, 2)},
+        "kernel_us": {("k_tl_spmv" if tl else "k_cg_iter"): round(us_cg, 3), "k_schur": round(us_schur, 2),
+                      "two_level_iteration": us_tl_iter and round(us_tl_iter, 3),
+                      "two_level_setup": us_tl_setup and round(us_tl_setup, 2)},
+        "preconditioner": "two-level (block-Jacobi + camera-cluster similarity coarse space)" if tl else "block-Jacobi",
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -57,6 +57,10 @@ typedef struct {
     int32_t shard_point_end;
     insfm_ba_allreduce_fn allreduce;  /* required when world_size > 1 */
     void* allreduce_ctx;
+    int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
+                              plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
+                              Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
+    int32_t cluster_size;  /* target cameras per coarse cluster (default 32; doubled until nclust*(D+1) <= 576) */
 } insfm_ba_desc;
 
 typedef struct {
@@ -74,6 +78,8 @@ typedef struct {
                                host polls of the CG status)  [3] back-substitution + update  [4] trial cost
                                [5] CG iteration launches (k_cg_dots + k_cg_iter chunks, no host gaps)  [6..7] 0
                                Only filled after insfm_ba_set_timing(h, 1): the events cost a little. */
+    int32_t coarse_used;    /* two-level preconditioner: 1 if the coarse correction was active in the final trial
+                               (0 with precond 0, or when the coarse matrix was not positive definite) */
 } insfm_ba_stats;
 
 /* Fill `desc` with the reference's defaults (TorchBA + BUNDLE_ADJUSTER_OPTIONS, config/colmap.py:47-54). */
@@ -117,8 +123,12 @@ int insfm_ba_debug_solve(insfm_ba* h, double f);
  * solve)[nnzb,D,D] 6 b[C,D] 7 dc[C,D] 8 dp[P,3].  Returns the number of doubles copied or a negative code. */
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
 /* Device time per launch (us, hipEvents on the library stream) of `reps` back-to-back launches of one kernel on the
- * data of the last solve: which = 0 k_cg_iter (one CG iteration), 1 k_schur.  Overwrites CG scratch state. */
+ * data of the last solve: which = 0 k_cg_iter (one block-Jacobi CG iteration), 1 k_schur, 2 one two-level CG
+ * iteration (k_tl_update + k_tl_coarse + k_tl_spmv), 3 k_tl_spmv alone, 4 the two-level setup (basis .. E^-1).
+ * Overwrites CG scratch state. */
 int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch);
+/* Camera cluster labels [C] of the two-level preconditioner's coarse space (HOST out); returns the cluster count. */
+int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);
 /* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */
 int64_t insfm_ba_nnzb(const insfm_ba* h);
 

@@ -32,6 +32,7 @@ class Desc(ctypes.Structure):
         ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32),
         ("shard_point_begin", ctypes.c_int32), ("shard_point_end", ctypes.c_int32),
         ("allreduce", ALLREDUCE_FN), ("allreduce_ctx", ctypes.c_void_p),
+        ("precond", ctypes.c_int32), ("cluster_size", ctypes.c_int32),
     ]
 
 
@@ -40,20 +41,21 @@ class Stats(ctypes.Structure):
         ("loss", ctypes.c_double), ("loss_before", ctypes.c_double), ("damping", ctypes.c_double),
         ("trials", ctypes.c_int32), ("rejects", ctypes.c_int32), ("pcg_iters_last", ctypes.c_int32),
         ("pcg_iters_total", ctypes.c_int32), ("solver_failed", ctypes.c_int32), ("cg_launches", ctypes.c_int32),
-        ("time_ms", ctypes.c_double * 8),
+        ("time_ms", ctypes.c_double * 8), ("coarse_used", ctypes.c_int32),
     ]
 
     def as_dict(self):
         return dict(loss=self.loss, loss_before=self.loss_before, damping=self.damping, trials=self.trials,
                     rejects=self.rejects, pcg_iters=self.pcg_iters_last, pcg_total=self.pcg_iters_total,
-                    failed=self.solver_failed, cg_launches=self.cg_launches, time_ms=list(self.time_ms)[:6])
+                    failed=self.solver_failed, cg_launches=self.cg_launches, time_ms=list(self.time_ms)[:6],
+                    coarse_used=self.coarse_used)
 
 
 # exported symbols (every one declared in include/insfm_ba.h)
 SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
-           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing")
+           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters")
 
 _lib = None
 
@@ -104,6 +106,8 @@ def load(path=LIB_PATH):
     L.insfm_ba_debug_time_kernel.restype = ctypes.c_int
     L.insfm_ba_set_timing.argtypes = [vp, ctypes.c_int32]
     L.insfm_ba_set_timing.restype = ctypes.c_int
+    L.insfm_ba_debug_clusters.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
+    L.insfm_ba_debug_clusters.restype = ctypes.c_int32
     _lib = L
     return L
 

@@ -498,27 +498,37 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
 // One 512-thread workgroup per camera row.  The row's neighbour blocks are contiguous in Sn (padded D x DP); lane l of
 // a wave owns 16-byte piece (l mod PPB) of block (l / PPB): every load instruction is a contiguous 1 KiB stream.
 // Loads that do not depend on alpha / beta (blocks, neighbour vectors, partials, history, own row) are issued first.
-// Recurrence scalars for step i = it-1: one 1024-thread workgroup sums the per-row partial dots of launch it-1 in a
-// fixed order, tests convergence on the true residual and publishes {alpha, beta, flag} (+ history) for k_cg_iter.
-__global__ __launch_bounds__(1024) void k_cg_dots(int it, int C, int maxit, double tol2_rel, CgBufs cg) {
-    __shared__ double red[3][1024];
-    const int t = threadIdx.x;
+// Recurrence scalars for step i = it-1: ONE wave sums the per-row partial dots of launch it-1 in a fixed order
+// (16 independent loads in flight per lane per quantity, butterfly across lanes; no barriers), tests convergence on the
+// true residual and publishes {alpha, beta, flag} (+ history) for k_cg_iter.
+__global__ __launch_bounds__(64) void k_cg_dots(int it, int C, int maxit, double tol2_rel, CgBufs cg) {
+    const int lane = threadIdx.x;
     if (cg.status[0] != 0) return;
     const int i = it - 1;
     const double* P0 = cg.part[it & 1 ? 0 : 1];
     const double* P1 = P0 + C;
     const double* P2 = P1 + C;
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    for (int k = t; k < C; k += 1024) { g0 += P0[k]; g1 += P1[k]; g2 += P2[k]; }
-    red[0][t] = g0; red[1][t] = g1; red[2][t] = g2;
-    __syncthreads();
-    for (int st = 512; st >= 1; st >>= 1) {
-        if (t < st) { red[0][t] += red[0][t + st]; red[1][t] += red[1][t + st]; red[2][t] += red[2][t + st]; }
-        __syncthreads();
+    for (int base = lane; base < C; base += 64 * 16) {
+        double a0[16], a1[16], a2[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int k = base + 64 * u;
+            const bool ok = k < C;
+            a0[u] = ok ? P0[k] : 0.0;
+            a1[u] = ok ? P1[k] : 0.0;
+            a2[u] = ok ? P2[k] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) { g0 += a0[u]; g1 += a1[u]; g2 += a2[u]; }
     }
-    if (t == 0) {
-        const double gam = red[0][0], del = red[1][0], rho = red[2][0];
-        const double bb = (i == 0) ? rho : cg.hist[2 * (maxit + 1)];
+    g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+    const double h_alpha = (i >= 1) ? cg.hist[2 * (i - 1)] : 1.0;
+    const double h_gam = (i >= 1) ? cg.hist[2 * (i - 1) + 1] : 1.0;
+    const double h_bb = cg.hist[2 * (maxit + 1)];
+    if (lane == 0) {
+        const double gam = g0, del = g1, rho = g2;
+        const double bb = (i == 0) ? rho : h_bb;
         double flag = 0.0, al = 0.0, be = 0.0;
         if (rho <= tol2_rel * bb || i >= maxit) {
             flag = 1.0;
@@ -527,8 +537,8 @@ __global__ __launch_bounds__(1024) void k_cg_dots(int it, int C, int maxit, doub
             double den;
             if (i == 0) { be = 0.0; den = del; }
             else {
-                be = gam / cg.hist[2 * (i - 1) + 1];
-                den = del - be * gam / cg.hist[2 * (i - 1)];
+                be = gam / h_gam;
+                den = del - be * gam / h_alpha;
             }
             if (!(den > 0.0)) {
                 flag = 2.0;
@@ -720,6 +730,8 @@ __global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __r
     dc[k] = s;
 }
 
+#include "ba_twolevel.h"
+
 // ------------------------------------------------------------------------------------------------------------
 // back-substitution, parameter update, cost
 // ------------------------------------------------------------------------------------------------------------
@@ -902,6 +914,12 @@ struct insfm_ba {
     double tms[8]{};
     int cg_launches = 0;
     bool want_timing = false;       // insfm_ba_set_timing: hipEvent phase timing inside insfm_ba_step
+    // two-level preconditioner (desc.precond == 1)
+    bool tlon = false;
+    TlBufs tl{};
+    std::vector<int> clab_host;
+    size_t chol_lds = 0, trinv_lds = 0;
+    int coarse_used = 0;
 };
 
 namespace {
@@ -998,6 +1016,101 @@ void acc_time(insfm_ba* h, int a, int b, int slot) {
     if (hipEventElapsedTime(&ms, h->ev[a], h->ev[b]) == hipSuccess) h->tms[slot] += ms;
 }
 
+// ---- camera clusters of the two-level preconditioner (same rules as oracle/ba_oracle.c: ora_aggregate) ----------
+// Co-visibility weight w(i,j) = number of (obs of i, obs of j) pairs sharing a track.  Greedy aggregation from seeds
+// in increasing id, growing by the most-connected unassigned camera (ties: smallest id) up to K members; aggregates
+// smaller than K/2 are dissolved into the most-connected aggregate of size >= K/2 (ties: smallest aggregate id);
+// labels renumbered by first appearance.
+struct CovisGraph {
+    std::vector<int> ptr, nb;
+    std::vector<long long> w;
+};
+
+CovisGraph covis_graph(int C, const std::vector<int>& gcptr, const std::vector<int>& gcobs, const std::vector<int>& gptr,
+                       const int32_t* cam_idx, const int32_t* pt_idx) {
+    CovisGraph g;
+    g.ptr.assign(C + 1, 0);
+    std::vector<int> mark(C, -1), buf;
+    std::vector<long long> acc(C, 0);
+    for (int i = 0; i < C; ++i) {
+        buf.clear();
+        for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
+            const int o = gcobs[e], p = pt_idx[o];
+            for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
+                if (q == o) continue;
+                const int j = cam_idx[q];
+                if (j == i) continue;
+                if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf.push_back(j); }
+                acc[j] += 1;
+            }
+        }
+        std::sort(buf.begin(), buf.end());
+        for (int j : buf) { g.nb.push_back(j); g.w.push_back(acc[j]); }
+        g.ptr[i + 1] = (int)g.nb.size();
+    }
+    return g;
+}
+
+int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
+    lab.assign(C, -1);
+    std::vector<long long> score(C, 0);
+    std::vector<char> incand(C, 0);
+    std::vector<int> cand, asize;
+    int nagg = 0;
+    for (int seed = 0; seed < C; ++seed) {
+        if (lab[seed] >= 0) continue;
+        cand.clear();
+        int size = 0, cur = seed;
+        for (;;) {
+            lab[cur] = nagg;
+            ++size;
+            for (int e = g.ptr[cur]; e < g.ptr[cur + 1]; ++e) {
+                const int j = g.nb[e];
+                if (lab[j] >= 0) continue;
+                if (!incand[j]) { incand[j] = 1; score[j] = 0; cand.push_back(j); }
+                score[j] += g.w[e];
+            }
+            if (size >= K) break;
+            int best = -1;
+            long long bs = 0;
+            for (int j : cand) {
+                if (lab[j] >= 0) continue;
+                if (score[j] > bs || (score[j] == bs && bs > 0 && j < best)) { bs = score[j]; best = j; }
+            }
+            if (best < 0) break;
+            cur = best;
+        }
+        for (int j : cand) incand[j] = 0;
+        asize.push_back(size);
+        ++nagg;
+    }
+    const int minsz = K / 2 > 1 ? K / 2 : 1;
+    std::vector<long long> to(nagg, 0);
+    std::vector<int> nl(lab);
+    for (int i = 0; i < C; ++i) {
+        if (asize[lab[i]] >= minsz) continue;
+        for (int e = g.ptr[i]; e < g.ptr[i + 1]; ++e) {
+            const int a = lab[g.nb[e]];
+            if (asize[a] >= minsz) to[a] += g.w[e];
+        }
+        int best = -1;
+        long long bs = 0;
+        for (int e = g.ptr[i]; e < g.ptr[i + 1]; ++e) {
+            const int a = lab[g.nb[e]];
+            if (asize[a] >= minsz && to[a] > 0 && (to[a] > bs || (to[a] == bs && a < best))) { bs = to[a]; best = a; }
+        }
+        for (int e = g.ptr[i]; e < g.ptr[i + 1]; ++e) to[lab[g.nb[e]]] = 0;
+        if (best >= 0) nl[i] = best;
+    }
+    std::vector<int> ren(nagg, -1);
+    int nc = 0;
+    for (int i = 0; i < C; ++i) {
+        if (ren[nl[i]] < 0) ren[nl[i]] = nc++;
+        lab[i] = ren[nl[i]];
+    }
+    return nc;
+}
+
 // ---- phases --------------------------------------------------------------------------------------------------
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     int rc = with_model(h->model, [&](auto mc) -> int {
@@ -1013,6 +1126,41 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     });
     if (rc) return rc;
     return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
+}
+
+// Two-level setup for the current S~ (after k_cg_factor / k_cg_scale): coarse basis, E, E^-1.
+int run_tl_setup(insfm_ba* h, const double* cams) {
+    const int C = h->C, m = h->tl.m;
+    const int nB = (m + kNB - 1) / kNB;
+    int rc = with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        constexpr int MC = kD<M> + 1;
+        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, h->stream>>>(C, cams, h->Lf, h->b, h->cg.r[0], h->tl);
+        return launch_err(h, "k_tl_basis");
+    });
+    if (rc) return rc;
+    return with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        constexpr int MC = DV + 1;
+        const int64_t nthr = (h->n_nbr + C) * MC;
+        k_tl_opart<DV><<<(unsigned)((nthr + kThreads - 1) / kThreads), kThreads, 0, h->stream>>>(C, h->n_nbr, h->nbr_j, h->Sn,
+                                                                                                h->tl);
+        k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, h->stream>>>(h->tl);
+        k_tl_chol<<<1, 1024, h->chol_lds, h->stream>>>(m, h->tl.E, h->tl.Dinv, h->tl.ok);
+        k_tl_trinv<<<nB, 1024, h->trinv_lds, h->stream>>>(m, h->tl.E, h->tl.Dinv, h->tl.Linv, h->tl.ok);
+        k_tl_gram<<<nB * nB, 1024, 0, h->stream>>>(m, h->tl.Linv, h->tl.Einv, h->tl.ok);
+        return launch_err(h, "two-level setup");
+    });
+}
+
+// Launch `it` of the two-level CG: update (it >= 1), coarse correction, S~ u.
+template <int D>
+void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
+    constexpr int RPW = kThreads / D;
+    if (it > 0)
+        k_tl_update<D><<<cdiv(h->C, RPW), kThreads, 0, h->stream>>>(it, h->C, maxit, tol2, h->Lf, h->cg, h->tl);
+    k_tl_coarse<D><<<h->tl.nc, kThreads, sizeof(double) * (h->tl.m + D + 1), h->stream>>>(h->cg, h->tl, h->tl.Einv);
+    k_tl_spmv<D><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
 }
 
 // Build S/b for factor f, solve, back-substitute and form the trial parameters.  Returns PCG iterations (>= 0),
@@ -1054,6 +1202,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             return launch_err(h, "k_cg_factor/scale");
         });
         if (rc) return rc;
+        if (h->tlon && (rc = run_tl_setup(h, cams))) return rc;
         const int maxit = h->d.pcg_max_iter;
         const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
         int it = 0;
@@ -1066,7 +1215,11 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             rc = with_D(D, [&](auto dc_) -> int {
                 constexpr int DV = decltype(dc_)::value;
                 for (int k = it; k < stop; ++k) {
-                    if (k > 0) k_cg_dots<<<1, 1024, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
+                    if (h->tlon) {
+                        launch_tl_iter<DV>(h, k, maxit, tol2);
+                        continue;
+                    }
+                    if (k > 0) k_cg_dots<<<1, 64, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
                     k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(k, h->C, maxit, tol2, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                     h->Lf, h->cg, h->probe);
                 }
@@ -1075,7 +1228,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             if (rc) return rc;
             rec(h, 9);
             it = stop;
-            HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 2, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
             HIPCHK(hipStreamSynchronize(h->stream));
             acc_time(h, 8, 9, 5);
             h->cg_launches += stop - first;
@@ -1083,6 +1236,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         }
         if (st[0] != 1) return INSFM_BA_ESOLVER;
         iters = st[1];
+        h->coarse_used = h->tlon ? st[2] : 0;
         h->last_cg_iters = iters;
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
@@ -1151,6 +1305,8 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->pcg_tol = 1e-5;
     d->world_size = 1; d->rank = 0;
     d->shard_point_begin = 0; d->shard_point_end = -1;
+    d->precond = 1;
+    d->cluster_size = 32;
 }
 
 const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() : "null handle"; }
@@ -1411,6 +1567,90 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         return 0;
     });
+    if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
+    if (desc->precond == 1 && desc->optimize_poses) {
+        // ---- two-level preconditioner: clusters, source lists of E, buffers ----
+        const int MC = D + 1;
+        CovisGraph g = covis_graph(C, gcptr, gcobs, gptr, cam_idx, pt_idx);
+        int K = desc->cluster_size > 0 ? desc->cluster_size : 32;
+        std::vector<int>& lab = h->clab_host;
+        int nc = aggregate(g, C, K, lab);
+        while (nc * MC > kCoarseMax) {
+            K *= 2;
+            nc = aggregate(g, C, K, lab);
+        }
+        const int m = nc * MC;
+        std::vector<int> clp(nc + 1, 0), clc(C), alone(C), nrow(std::max<int64_t>(h->n_nbr, 1), 0);
+        for (int i = 0; i < C; ++i) clp[lab[i] + 1]++;
+        for (int c = 0; c < nc; ++c) clp[c + 1] += clp[c];
+        {
+            std::vector<int> fill(clp.begin(), clp.end() - 1);
+            for (int i = 0; i < C; ++i) clc[fill[lab[i]]++] = i;
+        }
+        for (int i = 0; i < C; ++i) alone[i] = (clp[lab[i] + 1] - clp[lab[i]]) < 2;
+        for (int i = 0; i < C; ++i)
+            for (int nn = nptr[i]; nn < nptr[i + 1]; ++nn) nrow[nn] = i;
+        // E source lists per cluster pair (row cluster c', column cluster c): members of c' ascending, each with its
+        // diagonal term (c == c') then its neighbour slots in row order
+        std::vector<int> eptr((size_t)nc * nc + 1, 0), esrc;
+        esrc.reserve((size_t)h->n_nbr + C);
+        {
+            std::vector<std::vector<int>> bucket(nc);
+            for (int cr = 0; cr < nc; ++cr) {
+                for (auto& v : bucket) v.clear();
+                for (int e = clp[cr]; e < clp[cr + 1]; ++e) {
+                    const int i = clc[e];
+                    bucket[cr].push_back(-(i + 1));
+                    for (int nn = nptr[i]; nn < nptr[i + 1]; ++nn) bucket[lab[nj[nn]]].push_back(nn);
+                }
+                for (int c = 0; c < nc; ++c) {
+                    esrc.insert(esrc.end(), bucket[c].begin(), bucket[c].end());
+                    eptr[(size_t)cr * nc + c + 1] = (int)esrc.size();
+                }
+            }
+        }
+        TlBufs& tl = h->tl;
+        tl.nc = nc;
+        tl.m = m;
+        const int nB = (m + kNB - 1) / kNB;
+        int* ip = nullptr;
+        if ((rc = upload(h, &ip, lab.data(), lab.size()))) return fail(rc, "");
+        tl.clab = ip;
+        if ((rc = upload(h, &ip, clp.data(), clp.size()))) return fail(rc, "");
+        tl.cl_ptr = ip;
+        if ((rc = upload(h, &ip, clc.data(), clc.size()))) return fail(rc, "");
+        tl.cl_cams = ip;
+        if ((rc = upload(h, &ip, alone.data(), alone.size()))) return fail(rc, "");
+        tl.alone = ip;
+        if ((rc = upload(h, &ip, nrow.data(), nrow.size()))) return fail(rc, "");
+        tl.nbr_row = ip;
+        if ((rc = upload(h, &ip, eptr.data(), eptr.size()))) return fail(rc, "");
+        tl.ered_ptr = ip;
+        if (esrc.empty()) esrc.push_back(0);
+        if ((rc = upload(h, &ip, esrc.data(), esrc.size()))) return fail(rc, "");
+        tl.ered_src = ip;
+        if ((rc = dd(&tl.u, cd))) return fail(rc, "");
+        if ((rc = dd(&tl.Zt, cd * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.Rp, (size_t)C * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.gd, 2 * (size_t)C))) return fail(rc, "");
+        if ((rc = dd(&tl.rho[0], 2 * (size_t)C))) return fail(rc, "");
+        tl.rho[1] = tl.rho[0] + C;
+        if ((rc = dd(&tl.Opart, (size_t)std::max<int64_t>(h->n_nbr, 1) * MC * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.Odiag, (size_t)C * MC * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.E, (size_t)m * m))) return fail(rc, "");
+        if ((rc = dd(&tl.Linv, (size_t)m * m))) return fail(rc, "");
+        if ((rc = dd(&tl.Einv, (size_t)m * m))) return fail(rc, "");
+        if ((rc = dd(&tl.Dinv, (size_t)nB * kNB * kNB))) return fail(rc, "");
+        tl.ok = h->cg.status + 2;
+        hipError_t e = hipMemsetAsync(tl.Linv, 0, sizeof(double) * (size_t)m * m, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
+        h->chol_lds = sizeof(double) * (size_t)m * kPS;
+        h->trinv_lds = sizeof(double) * (size_t)(m + kNB) * kPS;
+        (void)hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->chol_lds);
+        (void)hipFuncSetAttribute((const void*)k_tl_trinv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->trinv_lds);
+        h->tlon = true;
+    }
     if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
     h->damping = 1.0 / desc->tr_radius;
     h->down = desc->tr_down;
@@ -1535,6 +1775,7 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
         st->solver_failed = failed;
         for (int k = 0; k < 8; ++k) st->time_ms[k] = h->tms[k];
         st->cg_launches = h->cg_launches;
+        st->coarse_used = h->coarse_used;
     }
     h->timing = false;
     return INSFM_BA_OK;
@@ -1566,11 +1807,19 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     // scratch once the solve has finished (dc already extracted).  0: k_cg_iter  1: k_schur (damping factor 1)
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
+    if (which >= 2 && !h->tlon) return INSFM_BA_EINVAL;
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
     int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         for (int r = 0; r < reps; ++r) {
-            if (which == 0)
+            if (which == 2) {
+                launch_tl_iter<DV>(h, 1, h->d.pcg_max_iter, 0.0);
+            } else if (which == 3) {
+                k_tl_spmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
+            } else if (which == 4) {
+                int rc2 = run_tl_setup(h, h->cams_cur);
+                if (rc2) return rc2;
+            } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                 h->Lf, h->cg, 0);
             else
@@ -1587,6 +1836,13 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     HIPCHK(hipEventElapsedTime(&ms, h->ev[10], h->ev[11]));
     *us_per_launch = 1e3 * ms / reps;
     return INSFM_BA_OK;
+}
+
+int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels) {
+    if (!h) return INSFM_BA_EINVAL;
+    if (!h->tlon) return 0;
+    if (labels) std::memcpy(labels, h->clab_host.data(), sizeof(int32_t) * h->C);
+    return h->tl.nc;
 }
 
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {

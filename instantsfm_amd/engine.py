@@ -15,7 +15,7 @@ from . import _capi
 # TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.
 LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4, tr_factor=0.5,
                    tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, max_rejects=30, pcg_tol=1e-5,
-                   pcg_max_iter=500)
+                   pcg_max_iter=500, precond=1, cluster_size=32)
 
 
 def make_allreduce_callback(get_buffer, group=None, errors=None):
@@ -159,13 +159,21 @@ class BundleAdjuster:
         return _capi.check(self._h, _capi.load().insfm_ba_debug_solve(self._h, float(f)))
 
     def debug_time_kernel(self, which, reps=50):
-        """Average device time (us) of `reps` back-to-back launches of k_cg_iter (0) or k_schur (1)."""
+        """Average device time (us) of `reps` back-to-back launches: 0 k_cg_iter, 1 k_schur, 2 one two-level CG
+        iteration (3 launches), 3 k_tl_spmv, 4 the two-level setup (6 launches)."""
         us = ctypes.c_double()
         _capi.check(self._h, _capi.load().insfm_ba_debug_time_kernel(self._h, int(which), int(reps), ctypes.byref(us)))
         return us.value
 
     def nnzb(self):
         return int(_capi.load().insfm_ba_nnzb(self._h))
+
+    def clusters(self):
+        """Camera cluster labels of the two-level preconditioner and the cluster count (0 when it is off)."""
+        lab = np.zeros(self.n_cams, dtype=np.int32)
+        nc = _capi.load().insfm_ba_debug_clusters(self._h, lab.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        _capi.check(self._h, nc)
+        return lab, int(nc)
 
     def debug_get(self, which, shape):
         out = np.zeros(shape, dtype=np.float64)

@@ -291,6 +291,10 @@ typedef struct {
     /* options */
     double delta, radius0, rmax, rmin, up, down0, factor, high, low, cmin, cmax, pcg_tol;
     int max_rejects, pcg_max_iter, optimize_poses;
+    int precond, cluster_size;   /* 0 block-Jacobi, 1 two-level (block-Jacobi + camera-cluster similarity coarse space) */
+    int *clab, nclust;           /* cluster label per camera, number of clusters */
+    int *csize;                  /* cameras per cluster */
+    double* lin_cams;            /* copy of the linearization point (coarse basis) */
     /* LM state */
     double damping, down, loss;
     int have_loss;
@@ -320,6 +324,160 @@ static double det_sum(const double* v, size_t n) {
 
 static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *(const int*)b; return (x > y) - (x < y); }
 
+
+/* ------------------------------------------------------------------------------------------ */
+/* camera clustering for the two-level preconditioner                                          */
+/* ------------------------------------------------------------------------------------------ */
+/* Co-visibility weight w(i,j) = number of (obs of i, obs of j) pairs that share a track.  Greedy aggregation:
+ * seeds in increasing camera id; an aggregate grows by the unassigned camera with the largest summed weight to it
+ * (ties: smallest id) until it has K members or no connected unassigned camera is left.  Aggregates smaller than
+ * K/2 are then dissolved: each member joins the aggregate of size >= K/2 it is most connected to (ties: smallest
+ * aggregate id).  Labels are renumbered in order of first appearance by camera id. */
+static int ora_aggregate(ora_t* h, int K);
+/* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU factorizes E in one workgroup's LDS):
+ * while the aggregation yields more clusters, it is redone with twice the target size. */
+#define COARSE_MAX 576
+static void ora_cluster_cameras(ora_t* h) {
+    int K = h->cluster_size;
+    while (ora_aggregate(h, K) * (h->D + 1) > COARSE_MAX) K *= 2;
+}
+
+static int ora_aggregate(ora_t* h, int K) {
+    const int C = h->C;
+    /* symmetric weighted adjacency (CSR) */
+    int* deg = (int*)calloc(C + 1, sizeof(int));
+    long* wsum = NULL;
+    int* mark = (int*)malloc(sizeof(int) * C);
+    long* acc = (long*)calloc(C, sizeof(long));
+    for (int c = 0; c < C; ++c) mark[c] = -1;
+    /* pass 1: neighbour lists per camera (both directions), weights by counting (o,q) pairs */
+    int** nb = (int**)calloc(C, sizeof(int*));
+    long** nw = (long**)calloc(C, sizeof(long*));
+    int* nn = (int*)calloc(C, sizeof(int));
+    int* buf = (int*)malloc(sizeof(int) * C);
+    for (int i = 0; i < C; ++i) {
+        int n = 0;
+        for (int e = h->cam_ptr[i]; e < h->cam_ptr[i + 1]; ++e) {
+            int o = h->cam_obs[e], p = h->pt[o];
+            for (int q = h->pt_ptr[p]; q < h->pt_ptr[p + 1]; ++q) {
+                if (q == o) continue;
+                int j = h->cam[q];
+                if (j == i) continue;
+                if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf[n++] = j; }
+                acc[j] += 1;
+            }
+        }
+        qsort(buf, n, sizeof(int), cmp_int);
+        nb[i] = (int*)malloc(sizeof(int) * (n ? n : 1));
+        nw[i] = (long*)malloc(sizeof(long) * (n ? n : 1));
+        for (int k = 0; k < n; ++k) { nb[i][k] = buf[k]; nw[i][k] = acc[buf[k]]; }
+        nn[i] = n;
+    }
+    (void)deg; (void)wsum;
+    int* lab = h->clab;
+    for (int c = 0; c < C; ++c) lab[c] = -1;
+    long* score = (long*)calloc(C, sizeof(long));
+    int* cand = (int*)malloc(sizeof(int) * C);
+    char* incand = (char*)calloc(C, 1);
+    int nagg = 0;
+    int* asize = (int*)calloc(C, sizeof(int));
+    for (int seed = 0; seed < C; ++seed) {
+        if (lab[seed] >= 0) continue;
+        int ncand = 0, size = 0;
+        int cur = seed;
+        for (;;) {
+            lab[cur] = nagg; ++size;
+            for (int k = 0; k < nn[cur]; ++k) {
+                int j = nb[cur][k];
+                if (lab[j] >= 0) continue;
+                if (!incand[j]) { incand[j] = 1; score[j] = 0; cand[ncand++] = j; }
+                score[j] += nw[cur][k];
+            }
+            if (size >= K) break;
+            int best = -1; long bs = 0;
+            for (int k = 0; k < ncand; ++k) {
+                int j = cand[k];
+                if (lab[j] >= 0) continue;
+                if (score[j] > bs || (score[j] == bs && bs > 0 && j < best)) { bs = score[j]; best = j; }
+            }
+            if (best < 0) break;
+            cur = best;
+        }
+        for (int k = 0; k < ncand; ++k) incand[cand[k]] = 0;
+        asize[nagg] = size;
+        ++nagg;
+    }
+    /* dissolve small aggregates */
+    const int minsz = K / 2 > 1 ? K / 2 : 1;
+    long* to = (long*)calloc(nagg, sizeof(long));
+    int* newlab = (int*)malloc(sizeof(int) * C);
+    for (int i = 0; i < C; ++i) newlab[i] = lab[i];
+    for (int i = 0; i < C; ++i) {
+        if (asize[lab[i]] >= minsz) continue;
+        int best = -1; long bs = 0;
+        for (int k = 0; k < nn[i]; ++k) { int a = lab[nb[i][k]]; if (asize[a] >= minsz) to[a] += nw[i][k]; }
+        for (int k = 0; k < nn[i]; ++k) {
+            int a = lab[nb[i][k]];
+            if (asize[a] >= minsz && to[a] > 0) {
+                if (to[a] > bs || (to[a] == bs && a < best)) { bs = to[a]; best = a; }
+            }
+        }
+        for (int k = 0; k < nn[i]; ++k) to[lab[nb[i][k]]] = 0;
+        if (best >= 0) newlab[i] = best;
+    }
+    /* renumber by first appearance */
+    int* ren = (int*)malloc(sizeof(int) * nagg);
+    for (int a = 0; a < nagg; ++a) ren[a] = -1;
+    int nc = 0;
+    for (int i = 0; i < C; ++i) {
+        if (ren[newlab[i]] < 0) ren[newlab[i]] = nc++;
+        lab[i] = ren[newlab[i]];
+    }
+    h->nclust = nc;
+    for (int c = 0; c < C; ++c) h->csize[c] = 0;
+    for (int i = 0; i < C; ++i) h->csize[lab[i]]++;
+    for (int i = 0; i < C; ++i) { free(nb[i]); free(nw[i]); }
+    free(nb); free(nw); free(nn); free(buf); free(mark); free(acc); free(score); free(cand); free(incand);
+    free(asize); free(to); free(newlab); free(ren); free(deg);
+    return nc;
+}
+
+int ora_clusters(const ora_t* h, int* lab) {
+    if (lab) memcpy(lab, h->clab, sizeof(int) * h->C);
+    return h->nclust;
+}
+
+/* Coarse basis of camera i (D x MC, row-major, MC = D + 1): the camera's tangent [rho, phi, intr] induced by an
+ * infinitesimal similarity of the world (tau, omega, sigma) that leaves every projection unchanged
+ *   rho = -R tau - [t]x R omega + sigma t,   phi = -R omega,
+ * plus one column per intrinsic.  A camera alone in its cluster gets [I_D | 0] instead (the 7 similarity modes of a
+ * single camera are linearly dependent). */
+static void coarse_basis(int D, const double* cam, int alone, double* G) {
+    const int MC = D + 1;
+    for (int k = 0; k < D * MC; ++k) G[k] = 0.0;
+    if (alone) { for (int a = 0; a < D; ++a) G[a * MC + a] = 1.0; return; }
+    const double *t = cam, *q = cam + 3;
+    double qx = q[0], qy = q[1], qz = q[2], w = q[3];
+    double Kq[9] = {0, -qz, qy, qz, 0, -qx, -qy, qx, 0}, R[9];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            double kk = 0;
+            for (int l = 0; l < 3; ++l) kk += Kq[i * 3 + l] * Kq[l * 3 + j];
+            R[i * 3 + j] = (i == j ? 1.0 : 0.0) + 2.0 * w * Kq[i * 3 + j] + 2.0 * kk;
+        }
+    double tx[9] = {0, -t[2], t[1], t[2], 0, -t[0], -t[1], t[0], 0};
+    for (int a = 0; a < 3; ++a)
+        for (int k = 0; k < 3; ++k) {
+            G[a * MC + k] = -R[a * 3 + k];
+            double s = 0;
+            for (int l = 0; l < 3; ++l) s += tx[a * 3 + l] * R[l * 3 + k];
+            G[a * MC + 3 + k] = -s;
+            G[(3 + a) * MC + 3 + k] = -R[a * 3 + k];
+        }
+    for (int a = 0; a < 3; ++a) G[a * MC + 6] = t[a];
+    for (int k = 0; k < D - 6; ++k) G[(6 + k) * MC + 7 + k] = 1.0;
+}
+
 ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* cam, const int* pt, const double* pp,
                   const double* dopt, const int* iopt) {
     if (ora_n_intr(model) < 0 || C <= 0 || P <= 0 || N <= 0) return NULL;
@@ -331,6 +489,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     h->down0 = dopt[5]; h->factor = dopt[6]; h->high = dopt[7]; h->low = dopt[8]; h->cmin = dopt[9];
     h->cmax = dopt[10]; h->pcg_tol = dopt[11];
     h->max_rejects = iopt[0]; h->pcg_max_iter = iopt[1]; h->optimize_poses = iopt[2];
+    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 32;
 #ifdef _OPENMP
     if (iopt[3] > 0) omp_set_num_threads(iopt[3]);
 #endif
@@ -383,10 +542,14 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     }
     h->row_ptr = (int*)calloc(C + 1, sizeof(int));
     for (int i = 0; i < C; ++i) h->row_ptr[i + 1] = h->row_ptr[i] + cnt[i];
+    (void)0;
     h->nnzb = h->row_ptr[C];
     h->col = (int*)malloc(sizeof(int) * (h->nnzb ? h->nnzb : 1));
     for (int i = 0; i < C; ++i) { memcpy(h->col + h->row_ptr[i], cols[i], sizeof(int) * cnt[i]); free(cols[i]); }
     free(cols); free(cnt);
+    h->clab = (int*)malloc(sizeof(int) * C);
+    h->csize = (int*)calloc(C, sizeof(int));
+    ora_cluster_cameras(h);
     /* lower references: row j lists (i < j, blk of (i,j)) in increasing i */
     h->lo_ptr = (int*)calloc(C + 1, sizeof(int));
     for (int i = 0; i < C; ++i)
@@ -433,7 +596,8 @@ void ora_destroy(ora_t* h) {
     if (!h) return;
     void* ptrs[] = {h->uv, h->pp, h->cam, h->pt, h->pt_ptr, h->cam_ptr, h->cam_obs, h->row_ptr, h->col, h->lo_ptr,
                     h->lo_col, h->lo_blk, h->W, h->V, h->gp, h->U, h->gc, h->Vinv, h->y, h->S, h->b, h->Minv, h->x,
-                    h->r, h->z, h->p, h->q, h->dp, h->cams_new, h->pts_new, h->partial};
+                    h->r, h->z, h->p, h->q, h->dp, h->cams_new, h->pts_new, h->partial,
+                    h->clab, h->csize, h->lin_cams};
     for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
     free(h);
 }
@@ -467,6 +631,8 @@ double ora_cost(ora_t* h, const double* cams, const double* pts, double* sq_out)
 /* Linearize at (cams, pts): W_o = J~c^T J~p (D x 3), V_p = sum J~p^T J~p (sym6), g_p = -sum J~p^T r~,
  * U_c = sum J~c^T J~c (D x D), g_c = -sum J~c^T r~.  Unclamped, undamped. */
 void ora_linearize(ora_t* h, const double* cams, const double* pts) {
+    if (!h->lin_cams) h->lin_cams = (double*)malloc(sizeof(double) * (size_t)h->C * h->stride);
+    memcpy(h->lin_cams, cams, sizeof(double) * (size_t)h->C * h->stride);
     int D = h->D, model = h->model;
     double delta = h->delta;
     #pragma omp parallel for schedule(static)
@@ -655,7 +821,111 @@ static void tri_inv(int n, const double* L, double* Li) {
     }
 }
 
-/* Block-Jacobi PCG on S x = b, as conjugate gradients on the symmetrically scaled system
+
+/* Coarse operator of the two-level preconditioner (scaled space).  Z~_i = L_i^T G_i (D x MC) with G_i the coarse
+ * basis of camera i at the linearization point; E = Z~^T S~ Z~ (m x m, m = nclust * MC), accumulated per camera row
+ * in increasing row order: diagonal term Z~_i^T Z~_i, then for every upper block (i,j>i) Z~_i^T S~_ij Z~_j into
+ * (c_i,c_j) and its transpose into (c_j,c_i).  A zero diagonal entry (unused column of a single-camera cluster)
+ * becomes 1.  E^-1 is formed explicitly from its Cholesky factor.  Returns 0 when E is not positive definite (the
+ * solve then runs with plain block-Jacobi). */
+static int ora_coarse_setup(ora_t* h, const double* Lfac, double* Zt, double* Einv) {
+    const int D = h->D, C = h->C, MC = D + 1, nc = h->nclust, m = nc * MC;
+    const size_t DD = (size_t)D * D;
+    for (int i = 0; i < C; ++i) {
+        double G[MAXD * (MAXD + 1)];
+        coarse_basis(D, h->lin_cams + (size_t)i * h->stride, h->csize[h->clab[i]] < 2, G);
+        const double* L = Lfac + (size_t)i * DD;
+        double* Z = Zt + (size_t)i * D * MC;
+        for (int a = 0; a < D; ++a)
+            for (int k = 0; k < MC; ++k) {
+                double s = 0;
+                for (int l = a; l < D; ++l) s += L[l * D + a] * G[l * MC + k];
+                Z[a * MC + k] = s;
+            }
+    }
+    double* E = (double*)calloc((size_t)m * m, sizeof(double));
+    for (int i = 0; i < C; ++i) {
+        const double* Zi = Zt + (size_t)i * D * MC;
+        const int ci = h->clab[i];
+        for (int k = 0; k < MC; ++k)
+            for (int l = 0; l < MC; ++l) {
+                double s = 0;
+                for (int a = 0; a < D; ++a) s += Zi[a * MC + k] * Zi[a * MC + l];
+                E[(size_t)(ci * MC + k) * m + ci * MC + l] += s;
+            }
+        for (int e = h->row_ptr[i] + 1; e < h->row_ptr[i + 1]; ++e) {
+            const int j = h->col[e], cj = h->clab[j];
+            const double* B = h->S + (size_t)e * DD;
+            const double* Zj = Zt + (size_t)j * D * MC;
+            double T[MAXD * (MAXD + 1)];            /* T = S~_ij Z~_j  (D x MC) */
+            for (int a = 0; a < D; ++a)
+                for (int l = 0; l < MC; ++l) {
+                    double s = 0;
+                    for (int bb = 0; bb < D; ++bb) s += B[a * D + bb] * Zj[bb * MC + l];
+                    T[a * MC + l] = s;
+                }
+            for (int k = 0; k < MC; ++k)
+                for (int l = 0; l < MC; ++l) {
+                    double s = 0;
+                    for (int a = 0; a < D; ++a) s += Zi[a * MC + k] * T[a * MC + l];
+                    E[(size_t)(ci * MC + k) * m + cj * MC + l] += s;
+                    E[(size_t)(cj * MC + l) * m + ci * MC + k] += s;
+                }
+        }
+    }
+    for (int k = 0; k < m; ++k)
+        if (E[(size_t)k * m + k] == 0.0) E[(size_t)k * m + k] = 1.0;
+    double* Lc = (double*)malloc(sizeof(double) * (size_t)m * m);
+    int ok = chol(m, E, Lc) == 0;
+    if (ok) {
+        double* Li = E;                             /* reuse: L^-1 */
+        tri_inv(m, Lc, Li);
+        /* Einv = L^-T L^-1 : Einv_kl = sum_{r >= max(k,l)} Li_rk Li_rl */
+        for (int k = 0; k < m; ++k)
+            for (int l = 0; l < m; ++l) {
+                double s = 0;
+                for (int r = k > l ? k : l; r < m; ++r) s += Li[(size_t)r * m + k] * Li[(size_t)r * m + l];
+                Einv[(size_t)k * m + l] = s;
+            }
+    }
+    free(Lc); free(E);
+    return ok;
+}
+
+/* u = r + Z~ E^-1 Z~^T r.  Restriction per cluster sums camera rows in increasing camera order. */
+static void coarse_apply(ora_t* h, const double* Zt, const double* Einv, double* Rc, double* yc, const double* r,
+                         double* u) {
+    const int D = h->D, C = h->C, MC = D + 1, m = h->nclust * MC;
+    for (int k = 0; k < m; ++k) Rc[k] = 0.0;
+    for (int i = 0; i < C; ++i) {
+        const double* Zi = Zt + (size_t)i * D * MC;
+        const double* ri = r + (size_t)i * D;
+        double* R = Rc + (size_t)h->clab[i] * MC;
+        for (int k = 0; k < MC; ++k) {
+            double s = 0;
+            for (int a = 0; a < D; ++a) s += Zi[a * MC + k] * ri[a];
+            R[k] += s;
+        }
+    }
+    #pragma omp parallel for schedule(static)
+    for (int k = 0; k < m; ++k) {
+        double s = 0;
+        for (int l = 0; l < m; ++l) s += Einv[(size_t)k * m + l] * Rc[l];
+        yc[k] = s;
+    }
+    #pragma omp parallel for schedule(static)
+    for (int i = 0; i < C; ++i) {
+        const double* Zi = Zt + (size_t)i * D * MC;
+        const double* y = yc + (size_t)h->clab[i] * MC;
+        for (int a = 0; a < D; ++a) {
+            double s = 0;
+            for (int k = 0; k < MC; ++k) s += Zi[a * MC + k] * y[k];
+            u[(size_t)i * D + a] = r[(size_t)i * D + a] + s;
+        }
+    }
+}
+
+/* Block-Jacobi (precond 0) or two-level (precond 1) PCG on S x = b, as conjugate gradients on the symmetrically scaled system
  * S~ = L^-1 S L^-T (S_ii = L_i L_i^T, so diag blocks of S~ are I) with the single-reduction
  * Chronopoulos-Gear recurrence.  In exact arithmetic this is the standard block-Jacobi PCG;
  * convergence is tested on the true residual ||b - S x|| = ||L r~|| <= tol ||b||, x0 = 0.
@@ -704,6 +974,18 @@ int ora_pcg(ora_t* h, double* xout) {
     double* w = h->q;
     double* sv = h->z;
     double* rt = (double*)malloc(sizeof(double) * n);
+    /* two-level preconditioner M~^-1 = I + Z~ E^-1 Z~^T in the scaled space (block-Jacobi + coarse correction) */
+    const int MC = D + 1, nc = h->nclust, m = nc * MC;
+    int twolev = h->precond == 1 && nc > 0;
+    double *Zt = NULL, *Einv = NULL, *Rc = NULL, *yc = NULL, *u = h->r;
+    if (twolev) {
+        Zt = (double*)malloc(sizeof(double) * (size_t)C * D * MC);
+        Einv = (double*)malloc(sizeof(double) * (size_t)m * m);
+        Rc = (double*)malloc(sizeof(double) * (size_t)m);
+        yc = (double*)malloc(sizeof(double) * (size_t)m);
+        u = (double*)malloc(sizeof(double) * n);
+        if (!ora_coarse_setup(h, Lfac, Zt, Einv)) twolev = 0;
+    }
     for (int i = 0; i < C; ++i) {
         const double* Li = h->Minv + (size_t)i * DD;
         for (int a = 0; a < D; ++a) {
@@ -713,9 +995,10 @@ int ora_pcg(ora_t* h, double* xout) {
         }
     }
     for (size_t e = 0; e < n; ++e) { h->x[e] = 0; h->p[e] = 0; sv[e] = 0; }
-    spmv_scaled(h, h->r, w);
+    if (twolev) coarse_apply(h, Zt, Einv, Rc, yc, h->r, u);
+    spmv_scaled(h, u, w);
     double bb2 = dot(h->b, h->b, n, tmp);
-    double gam = dot(h->r, h->r, n, tmp), del = dot(w, h->r, n, tmp), rho = bb2;
+    double gam = dot(h->r, u, n, tmp), del = dot(w, u, n, tmp), rho = bb2;
     double gam_prev = 1.0, alpha_prev = 1.0;
     double tol2 = h->pcg_tol * h->pcg_tol * bb2;
     int k = 0, fail = 0;
@@ -727,15 +1010,16 @@ int ora_pcg(ora_t* h, double* xout) {
         if (!(den > 0.0)) { fail = 1; break; }
         alpha = gam / den;
         for (size_t e = 0; e < n; ++e) {
-            h->p[e] = h->r[e] + beta * h->p[e];
+            h->p[e] = u[e] + beta * h->p[e];
             sv[e] = w[e] + beta * sv[e];
             h->x[e] += alpha * h->p[e];
             h->r[e] -= alpha * sv[e];
         }
-        spmv_scaled(h, h->r, w);
+        if (twolev) coarse_apply(h, Zt, Einv, Rc, yc, h->r, u);
+        spmv_scaled(h, u, w);
         gam_prev = gam; alpha_prev = alpha;
-        gam = dot(h->r, h->r, n, tmp);
-        del = dot(w, h->r, n, tmp);
+        gam = dot(h->r, u, n, tmp);
+        del = dot(w, u, n, tmp);
         /* true residual norm^2 = ||L r~||^2 */
         for (int i = 0; i < C; ++i) {
             const double* L = Lfac + (size_t)i * DD;
@@ -749,6 +1033,8 @@ int ora_pcg(ora_t* h, double* xout) {
     }
     free(rt);
     free(Lfac);
+    if (Zt) { free(Zt); free(Einv); free(Rc); free(yc); free(u); }
+    h->stats[7] = twolev;
     if (fail) return -1;
     /* x = L^-T x~ */
     for (int i = 0; i < C; ++i) {
@@ -808,6 +1094,13 @@ static double model_decrease(ora_t* h, const double* cams, const double* pts, co
         e[o] = jd[0] * (2.0 * sw * r[0] + jd[0]) + jd[1] * (2.0 * sw * r[1] + jd[1]);
     }
     return -det_sum(e, h->N);
+}
+
+/* Build (without solving) the reduced camera system S (upper blocks, unscaled) and b for factor f. */
+int ora_build_reduced(ora_t* h, double f) {
+    if (prep_points(h, f)) return -1;
+    ora_schur(h, f);
+    return 0;
 }
 
 /* Solve the damped system for factor f; fills h->x (dc) and h->dp.  Returns pcg iterations or -1. */

@@ -37,6 +37,7 @@ def lib():
         L.ora_cost.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
         L.ora_linearize.argtypes = [ctypes.c_void_p, _dp, _dp]
         L.ora_solve.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.ora_build_reduced.argtypes = [ctypes.c_void_p, ctypes.c_double]
         L.ora_get.argtypes = [ctypes.c_void_p, ctypes.c_int, _dp]
         L.ora_nnzb.argtypes = [ctypes.c_void_p]
         L.ora_pattern.argtypes = [ctypes.c_void_p, _ip, _ip]
@@ -44,6 +45,7 @@ def lib():
         L.ora_eval.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.ora_retract_pose.argtypes = [_dp, _dp, _dp]
         L.ora_n_intr.argtypes = [ctypes.c_int]
+        L.ora_clusters.argtypes = [ctypes.c_void_p, _ip]
         _lib = L
     return _lib
 
@@ -86,7 +88,7 @@ def retract_pose(x7, d6):
 
 DEFAULTS = dict(huber_delta=1.0, tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4,
                 tr_factor=0.5, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
-                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0)
+                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=32)
 
 
 class OracleBA:
@@ -104,7 +106,8 @@ class OracleBA:
         self.D = 6 + n_intr(self.model)
         dopt = np.array([o['huber_delta'], o['tr_radius'], o['tr_max'], o['tr_min'], o['tr_up'], o['tr_down'],
                          o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
-        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], o['optimize_poses'], o['threads']], np.int32)
+        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], o['optimize_poses'], o['threads'], o['precond'],
+                         o['cluster_size']], np.int32)
         self.h = lib().ora_create(self.model, self.C, self.P, self.N, _d(self.uv), _i(self.cam), _i(self.pt),
                                   _d(self.pp), _d(dopt), _i(iopt))
         if not self.h:
@@ -126,7 +129,7 @@ class OracleBA:
         s = np.zeros(8)
         lib().ora_stats(self.h, _d(s))
         return dict(trials=int(s[0]), pcg_iters=int(s[1]), pcg_total=int(s[2]), damp_factor=s[3],
-                    damping=s[4], failed=int(s[5]), rejects=int(s[6]))
+                    damping=s[4], failed=int(s[5]), rejects=int(s[6]), coarse_used=int(s[7]))
 
     def cost(self, cams, pts):
         sq = ctypes.c_double()
@@ -138,6 +141,18 @@ class OracleBA:
 
     def solve(self, f):
         return lib().ora_solve(self.h, float(f))
+
+    def build_reduced(self, f):
+        """Unscaled reduced camera system for damping factor f: (S upper blocks, b)."""
+        if lib().ora_build_reduced(self.h, float(f)) != 0:
+            raise RuntimeError("non-PD point block")
+        return self.get(S), self.get(B)
+
+    def clusters(self):
+        """Camera cluster labels of the two-level preconditioner's coarse space and the cluster count."""
+        lab = np.zeros(self.C, np.int32)
+        nc = lib().ora_clusters(self.h, _i(lab))
+        return lab, nc
 
     def nnzb(self):
         return lib().ora_nnzb(self.h)

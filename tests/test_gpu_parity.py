@@ -29,7 +29,8 @@ def engines(prob, **kw):
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=DEV,
                          **kw)
     ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
-                     optimize_poses=int(kw.get("optimize_poses", True)))
+                     optimize_poses=int(kw.get("optimize_poses", True)), precond=kw.get("precond", 1),
+                     cluster_size=kw.get("cluster_size", 32))
     return eng, ora
 
 
@@ -53,9 +54,10 @@ def test_linearize_parity(model):
 
 @pytest.mark.parametrize("model", (2, 4, 6))
 @pytest.mark.parametrize("deterministic", (True, False))
-def test_solve_parity(model, deterministic):
+@pytest.mark.parametrize("precond,cluster", [(0, 32), (1, 32), (1, 6)])
+def test_solve_parity(model, deterministic, precond, cluster):
     prob = make_problem(30, 800, seed=5, model=model)
-    eng, ora = engines(prob, deterministic=deterministic)
+    eng, ora = engines(prob, deterministic=deterministic, precond=precond, cluster_size=cluster)
     eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
     ora.linearize(prob.cams_init, prob.points_init)
     f = 1.0 + 1e-4
@@ -71,10 +73,10 @@ def test_solve_parity(model, deterministic):
     assert rel(eng.debug_get(8, (P, 3)), ora.get(O.DP)) < 1e-8
 
 
-@pytest.mark.parametrize("cfg,steps", [(1, 6), (2, 2)])
-def test_step_parity(cfg, steps):
+@pytest.mark.parametrize("cfg,steps,precond", [(1, 6, 1), (2, 2, 1), (2, 2, 0)])
+def test_step_parity(cfg, steps, precond):
     prob = make_config(cfg)
-    eng, ora = engines(prob)
+    eng, ora = engines(prob, precond=precond)
     cg, pg = dev(prob.cams_init), dev(prob.points_init)
     co, po = prob.cams_init.copy(), prob.points_init.copy()
     for s in range(steps):
@@ -188,3 +190,44 @@ def test_torchba_solve_end_to_end(model):
         full = np.asarray(cameras[images[image_id].cam_id].params)
         rest = [k for k in range(full.size) if k not in pk.pp_indices - 7]
         assert rel(full[rest], c[i, 7:]) < 1e-8
+
+
+@pytest.mark.parametrize("shuffle", (False, True))
+def test_clusters_match_oracle(shuffle):
+    """The coarse space is the same on both sides: identical camera clusters (greedy co-visibility aggregation)."""
+    prob = make_problem(150, 6000, seed=8)
+    cam_idx = prob.cam_idx
+    if shuffle:
+        perm = np.random.default_rng(3).permutation(prob.n_cams).astype(np.int32)
+        cam_idx = perm[cam_idx]
+    for K in (4, 16, 32):
+        eng = BundleAdjuster(prob.model, prob.uv, cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=DEV,
+                             cluster_size=K)
+        ora = O.OracleBA(prob.model, prob.uv, cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, cluster_size=K)
+        lg, ng = eng.clusters()
+        lo, no = ora.clusters()
+        assert ng == no and np.array_equal(lg, lo), K
+        eng.close()
+
+
+def test_two_level_step_with_coarse_active_and_fewer_iterations():
+    """Config 2: the coarse correction is active, matches the oracle's iteration counts and needs far fewer CG
+    iterations than block-Jacobi for the same stopping rule; both reach the same loss after 4 steps (1e-6)."""
+    prob = make_config(2)
+    res = {}
+    for pc in (0, 1):
+        eng, ora = engines(prob, precond=pc)
+        cg = dev(prob.cams_init)
+        pg = dev(prob.points_init)
+        co, po = prob.cams_init.copy(), prob.points_init.copy()
+        its = []
+        for _ in range(4):
+            lg, st = eng.step(cg, pg)
+            lo = ora.step(co, po)
+            so = ora.stats()
+            assert st["pcg_iters"] == so["pcg_iters"], (pc, st, so)
+            assert st["coarse_used"] == so["coarse_used"] == pc
+            its.append(st["pcg_iters"])
+        res[pc] = (lg, sum(its))
+    assert res[1][1] * 2 < res[0][1], res
+    assert abs(res[1][0] - res[0][0]) / res[0][0] < 1e-6, res

@@ -119,11 +119,13 @@ def test_lm_thread_count_independent():
     assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
 
 
-def test_schur_system_is_exact_on_small_problem():
-    """Schur reduction + back-substitution solves the full damped normal equations (dense check)."""
+@pytest.mark.parametrize("precond,cluster", [(0, 32), (1, 32), (1, 2)])
+def test_schur_system_is_exact_on_small_problem(precond, cluster):
+    """Schur reduction + back-substitution solves the full damped normal equations (dense check), with either
+    preconditioner (cluster 2: several clusters on 6 cameras)."""
     prob = make_problem(6, 40, track_len=4, seed=2)
     ba = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, pcg_tol=1e-14,
-                    pcg_max_iter=2000)
+                    pcg_max_iter=2000, precond=precond, cluster_size=cluster)
     ba.linearize(prob.cams_init, prob.points_init)
     f = 1.01
     assert ba.solve(f) >= 0
@@ -150,3 +152,47 @@ def test_schur_system_is_exact_on_small_problem():
     x = np.linalg.solve(A, g)
     np.testing.assert_allclose(ba.get(O.DC).reshape(-1), x[:C * D], rtol=1e-7, atol=1e-9 * np.max(np.abs(x)))
     np.testing.assert_allclose(ba.get(O.DP).reshape(-1), x[C * D:], rtol=1e-7, atol=1e-9 * np.max(np.abs(x)))
+
+
+def _shuffled(prob, seed=1):
+    perm = np.random.default_rng(seed).permutation(prob.n_cams)
+    inv = np.argsort(perm)
+    return perm[prob.cam_idx].astype(np.int32), prob.cams_init[inv].copy(), prob.pp[inv].copy()
+
+
+@pytest.mark.parametrize("K", (2, 4, 8, 32))
+def test_clusters_partition_and_cap(K):
+    """Every camera gets a label 0..nc-1, no degenerate singleton clusters on a connected scene, and the coarse
+    dimension nc*(D+1) stays within the 576 cap (cluster size doubled as needed)."""
+    prob = make_problem(200, 4000, seed=1)
+    cam_idx, _, pp = _shuffled(prob)
+    ba = O.OracleBA(prob.model, prob.uv, cam_idx, prob.pt_idx, pp, prob.n_cams, prob.n_points, cluster_size=K)
+    lab, nc = ba.clusters()
+    assert lab.min() == 0 and lab.max() == nc - 1
+    sizes = np.bincount(lab)
+    assert sizes.min() >= 2
+    assert nc * ba.D + nc <= 576
+    # first-appearance numbering
+    first = [int(np.argmax(lab == c)) for c in range(nc)]
+    assert first == sorted(first)
+
+
+def test_two_level_converges_like_block_jacobi():
+    """Same stopping rule, far fewer iterations, same LM trajectory up to the PCG tolerance (camera-shuffled scene:
+    the clusters do not follow camera order)."""
+    prob = make_problem(120, 6000, seed=3)
+    cam_idx, cams0, pp = _shuffled(prob)
+    out = {}
+    for pc in (0, 1):
+        ba = O.OracleBA(prob.model, prob.uv, cam_idx, prob.pt_idx, pp, prob.n_cams, prob.n_points, precond=pc)
+        c, p = cams0.copy(), prob.points_init.copy()
+        its, hist = [], []
+        for _ in range(5):
+            hist.append(ba.step(c, p))
+            st = ba.stats()
+            assert st["coarse_used"] == pc
+            its.append(st["pcg_iters"])
+        out[pc] = (hist, sum(its), ba.cost(c, p)[1])
+    assert out[1][1] * 2 < out[0][1], (out[0][1], out[1][1])
+    assert abs(out[1][2] - out[0][2]) < 1e-4
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-6)
