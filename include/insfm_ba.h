@@ -60,7 +60,7 @@ typedef struct {
     int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
                               plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
                               Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
-    int32_t cluster_size;  /* target cameras per coarse cluster (default 32; doubled until nclust*(D+1) <= 576) */
+    int32_t cluster_size;  /* target cameras per coarse cluster (default 32; doubled until nclust*(D+1) <= 288) */
 } insfm_ba_desc;
 
 typedef struct {

@@ -1,0 +1,44 @@
+// Shared definitions of the BA kernels (ba_kernels.hip, ba_twolevel.h, tools/bench_dense.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace insfm {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+
+struct CgBufs {
+    double* r[2];
+    double* w[2];
+    double* s[2];
+    double* p;
+    double* x;
+    double* part[2];  // [nwg][3]: gamma, delta, rho
+    double* hist;     // [maxit + 2][2]: alpha_i, gamma_i ; hist_bb at the end
+    double* scal;     // [4]: alpha, beta, flag of the current recurrence step (written by k_cg_dots)
+    int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
+};
+
+
+constexpr int kCgThreads = 512;
+constexpr int kCgWaves = kCgThreads / 64;
+
+template <int D>
+struct CgGeom {
+    static constexpr int DP = D + (D & 1);     // padded row length
+    static constexpr int HP = DP / 2;          // 16-byte pieces per block row
+    static constexpr int PPB = D * HP;         // pieces per block
+    static constexpr int BPW = PPB <= 64 ? 64 / PPB : 1;          // blocks per wave per round
+    static constexpr int PPL = PPB <= 64 ? 1 : (PPB + 63) / 64;   // pieces per lane
+    static constexpr int BPR = BPW * kCgWaves;                    // blocks per round per workgroup
+};
+
+
+}  // namespace insfm

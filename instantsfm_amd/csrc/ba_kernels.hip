@@ -27,24 +27,18 @@
 
 #include "../../include/insfm_ba.h"
 #include "ba_device.h"
+#include "ba_common.h"
+#include "ba_twolevel.h"
 
 using namespace insfm;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
 constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgroup
 
 // ------------------------------------------------------------------------------------------------------------
 // reductions
 // ------------------------------------------------------------------------------------------------------------
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
 // Fixed-order block reduction of NV values per thread; result valid in thread 0 (and returned to all).
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= kThreads*NV doubles */) {
@@ -362,18 +356,6 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
 // ------------------------------------------------------------------------------------------------------------
 // PCG on the reduced camera system
 // ------------------------------------------------------------------------------------------------------------
-struct CgBufs {
-    double* r[2];
-    double* w[2];
-    double* s[2];
-    double* p;
-    double* x;
-    double* part[2];  // [nwg][3]: gamma, delta, rho
-    double* hist;     // [maxit + 2][2]: alpha_i, gamma_i ; hist_bb at the end
-    double* scal;     // [4]: alpha, beta, flag of the current recurrence step (written by k_cg_dots)
-    int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
-};
-
 // One wave per camera: Cholesky S_ii = L L^T and L^-1 (lane 0 on an LDS copy), r0 = L^-1 b, zero p/x/s.
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, const double* __restrict__ S,
@@ -554,19 +536,6 @@ __global__ __launch_bounds__(64) void k_cg_dots(int it, int C, int maxit, double
     }
 }
 
-constexpr int kCgThreads = 512;
-constexpr int kCgWaves = kCgThreads / 64;
-
-template <int D>
-struct CgGeom {
-    static constexpr int DP = D + (D & 1);     // padded row length
-    static constexpr int HP = DP / 2;          // 16-byte pieces per block row
-    static constexpr int PPB = D * HP;         // pieces per block
-    static constexpr int BPW = PPB <= 64 ? 64 / PPB : 1;          // blocks per wave per round
-    static constexpr int PPL = PPB <= 64 ? 1 : (PPB + 63) / 64;   // pieces per lane
-    static constexpr int BPR = BPW * kCgWaves;                    // blocks per round per workgroup
-};
-
 template <int D>
 __global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit, double tol2_rel,
                                                         const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_j,
@@ -729,8 +698,6 @@ __global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __r
     for (int m = a; m < D; ++m) s += L[m * D + a] * xt[(size_t)i * D + m];
     dc[k] = s;
 }
-
-#include "ba_twolevel.h"
 
 // ------------------------------------------------------------------------------------------------------------
 // back-substitution, parameter update, cost
@@ -918,7 +885,15 @@ struct insfm_ba {
     bool tlon = false;
     TlBufs tl{};
     std::vector<int> clab_host;
-    size_t chol_lds = 0, trinv_lds = 0;
+    size_t chol_lds = 0, trinv_lds = 0, erow_lds = 0, update_lds = 0;
+    // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
+    double *Ebuf[2]{}, *Dinvbuf[2]{}, *Linvbuf[2]{}, *Einvbuf[2]{};
+    int* okbuf = nullptr;  // [2]
+    hipStream_t side = nullptr;
+    hipEvent_t ev_E = nullptr, ev_fact[2]{};
+    long long tl_solves = 0;
+    bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
+    bool tl_sync = false;  // INSFM_TL_SYNC=1: factorize on the main stream (debug)
     int coarse_used = 0;
 };
 
@@ -1113,6 +1088,7 @@ int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
 
 // ---- phases --------------------------------------------------------------------------------------------------
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
+    h->tl_fresh = true;
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
@@ -1128,38 +1104,65 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
 }
 
-// Two-level setup for the current S~ (after k_cg_factor / k_cg_scale): coarse basis, E, E^-1.
-int run_tl_setup(insfm_ba* h, const double* cams) {
+// Two-level setup, part 1 (main stream, after k_cg_factor / k_cg_scale): coarse basis and E into slot `slot`.
+int run_tl_build(insfm_ba* h, const double* cams, int slot) {
     const int C = h->C, m = h->tl.m;
-    const int nB = (m + kNB - 1) / kNB;
+    TlBufs tl = h->tl;
+    tl.E = h->Ebuf[slot];
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int MC = kD<M> + 1;
-        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, h->stream>>>(C, cams, h->Lf, h->b, h->cg.r[0], h->tl);
+        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, h->stream>>>(C, cams, h->Lf, tl);
         return launch_err(h, "k_tl_basis");
     });
     if (rc) return rc;
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
-        constexpr int MC = DV + 1;
-        const int64_t nthr = (h->n_nbr + C) * MC;
-        k_tl_opart<DV><<<(unsigned)((nthr + kThreads - 1) / kThreads), kThreads, 0, h->stream>>>(C, h->n_nbr, h->nbr_j, h->Sn,
-                                                                                                h->tl);
-        k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, h->stream>>>(h->tl);
-        k_tl_chol<<<1, 1024, h->chol_lds, h->stream>>>(m, h->tl.E, h->tl.Dinv, h->tl.ok);
-        k_tl_trinv<<<nB, 1024, h->trinv_lds, h->stream>>>(m, h->tl.E, h->tl.Dinv, h->tl.Linv, h->tl.ok);
-        k_tl_gram<<<nB * nB, 1024, 0, h->stream>>>(m, h->tl.Linv, h->tl.Einv, h->tl.ok);
-        return launch_err(h, "two-level setup");
+        k_tl_erow<DV><<<C, kThreads, h->erow_lds, h->stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
+        k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, h->stream>>>(tl);
+        return launch_err(h, "k_tl_erow/ereduce");
     });
 }
 
-// Launch `it` of the two-level CG: update (it >= 1), coarse correction, S~ u.
+// Two-level setup, part 2: Cholesky of E[slot], diagonal-block inverses, L^-1, E^-1 = L^-T L^-1 on `stream`.
+int run_tl_factor(insfm_ba* h, int slot, hipStream_t stream) {
+    const int m = h->tl.m;
+    const int nB = (m + kNB - 1) / kNB;
+    int* ok = h->okbuf + slot;
+    k_tl_chol<<<1, 1024, h->chol_lds, stream>>>(m, h->Ebuf[slot], ok);
+    k_tl_dinv<<<nB, 64, 0, stream>>>(m, h->Ebuf[slot], h->Dinvbuf[slot], ok);
+    k_tl_trinv<<<nB, 256, h->trinv_lds, stream>>>(m, h->Ebuf[slot], h->Dinvbuf[slot], h->Linvbuf[slot], ok);
+    k_tl_gram<<<nB * nB, 256, 0, stream>>>(m, h->Linvbuf[slot], h->Einvbuf[slot], ok);
+    return launch_err(h, "two-level factorization");
+}
+
+// Per solve: build E_n on the main stream, factorize it on the side stream, and point the CG at the coarse inverse of
+// the previous solve when this is the first solve after a linearization (otherwise at its own, waiting for the
+// factorization) -- the oracle's lag rule (ora_pcg).
+int run_tl_setup(insfm_ba* h, const double* cams) {
+    const int slot = (int)(h->tl_solves & 1);
+    int rc = run_tl_build(h, cams, slot);
+    if (rc) return rc;
+    hipStream_t fs = h->tl_sync ? h->stream : h->side;
+    HIPCHK(hipEventRecord(h->ev_E, h->stream));
+    HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
+    if ((rc = run_tl_factor(h, slot, fs))) return rc;
+    HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
+    const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
+    h->tl_fresh = false;
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_fact[use], 0));
+    h->tl.Einv = h->Einvbuf[use];
+    h->tl.ok = h->okbuf + use;
+    ++h->tl_solves;
+    return 0;
+}
+
+// Launch `it` of the two-level CG: update (recurrence step it-1 when it >= 1; restriction always), coarse
+// correction, S~ u.
 template <int D>
 void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
-    constexpr int RPW = kThreads / D;
-    if (it > 0)
-        k_tl_update<D><<<cdiv(h->C, RPW), kThreads, 0, h->stream>>>(it, h->C, maxit, tol2, h->Lf, h->cg, h->tl);
-    k_tl_coarse<D><<<h->tl.nc, kThreads, sizeof(double) * (h->tl.m + D + 1), h->stream>>>(h->cg, h->tl, h->tl.Einv);
+    k_tl_update<D><<<h->tl.nc, kCgThreads, h->update_lds, h->stream>>>(it, h->C, maxit, tol2, h->Lf, h->cg, h->tl);
+    k_tl_coarse<D><<<h->tl.nc, kThreads, 0, h->stream>>>(h->cg, h->tl, h->tl.Einv);
     k_tl_spmv<D><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
 }
 
@@ -1234,7 +1237,12 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             h->cg_launches += stop - first;
             if (st[0] != 0 || it >= maxit + 2) break;
         }
-        if (st[0] != 1) return INSFM_BA_ESOLVER;
+        if (st[0] != 1) {
+            h->err = std::string("PCG ") + (st[0] == 2 ? "breakdown" : "did not finish") + " at iteration " +
+                     std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
+                     (h->tlon ? std::to_string(st[2]) : std::string("off")) + ", launches " + std::to_string(it) + ")";
+            return INSFM_BA_ESOLVER;
+        }
         iters = st[1];
         h->coarse_used = h->tlon ? st[2] : 0;
         h->last_cg_iters = iters;
@@ -1313,9 +1321,17 @@ const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() :
 
 void insfm_ba_destroy(insfm_ba* h) {
     if (!h) return;
+    if (h->side) (void)hipStreamSynchronize(h->side);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->host_res) (void)hipHostFree(h->host_res);
     for (auto& e : h->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (h->side) {
+        (void)hipStreamSynchronize(h->side);
+        (void)hipStreamDestroy(h->side);
+    }
+    if (h->ev_E) (void)hipEventDestroy(h->ev_E);
+    for (auto& e : h->ev_fact)
         if (e) (void)hipEventDestroy(e);
     delete h;
 }
@@ -1580,78 +1596,138 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
             nc = aggregate(g, C, K, lab);
         }
         const int m = nc * MC;
-        std::vector<int> clp(nc + 1, 0), clc(C), alone(C), nrow(std::max<int64_t>(h->n_nbr, 1), 0);
+        std::vector<int> clp(nc + 1, 0), clc(C), alone(C);
         for (int i = 0; i < C; ++i) clp[lab[i] + 1]++;
         for (int c = 0; c < nc; ++c) clp[c + 1] += clp[c];
         {
             std::vector<int> fill(clp.begin(), clp.end() - 1);
             for (int i = 0; i < C; ++i) clc[fill[lab[i]]++] = i;
         }
+        int maxmem = 1;
+        for (int c = 0; c < nc; ++c) maxmem = std::max(maxmem, clp[c + 1] - clp[c]);
         for (int i = 0; i < C; ++i) alone[i] = (clp[lab[i] + 1] - clp[lab[i]]) < 2;
-        for (int i = 0; i < C; ++i)
-            for (int nn = nptr[i]; nn < nptr[i + 1]; ++nn) nrow[nn] = i;
-        // E source lists per cluster pair (row cluster c', column cluster c): members of c' ascending, each with its
-        // diagonal term (c == c') then its neighbour slots in row order
-        std::vector<int> eptr((size_t)nc * nc + 1, 0), esrc;
-        esrc.reserve((size_t)h->n_nbr + C);
+        // per row: neighbour slots ordered by (cluster of the neighbour, slot) and one segment per neighbour cluster
+        // (the row's own cluster always has one: it carries the diagonal term)
+        std::vector<int> sperm(std::max<int64_t>(h->n_nbr, 1), 0), rsp(C + 1, 0);
+        std::vector<int4> segs;
+        int maxseg = 1;
+        for (int i = 0; i < C; ++i) {
+            const int n0 = nptr[i], n1 = nptr[i + 1];
+            std::vector<int> ord(n1 - n0);
+            for (int q = 0; q < n1 - n0; ++q) ord[q] = n0 + q;
+            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lab[nj[x]] < lab[nj[y]]; });
+            for (int q = 0; q < n1 - n0; ++q) sperm[n0 + q] = ord[q];
+            const int own = lab[i];
+            bool own_done = false;
+            int q = 0;
+            const int before = (int)segs.size();
+            while (q < n1 - n0 || !own_done) {
+                const int cq = q < n1 - n0 ? lab[nj[ord[q]]] : nc;
+                if (!own_done && own < cq) {  // own cluster without neighbours in it
+                    segs.push_back(make_int4(own, q, q, 1));
+                    own_done = true;
+                    continue;
+                }
+                int qe = q;
+                while (qe < n1 - n0 && lab[nj[ord[qe]]] == cq) ++qe;
+                segs.push_back(make_int4(cq, q, qe, cq == own ? 1 : 0));
+                if (cq == own) own_done = true;
+                q = qe;
+            }
+            rsp[i + 1] = (int)segs.size();
+            maxseg = std::max(maxseg, (int)segs.size() - before);
+        }
+        // E source lists per cluster pair (row cluster c', column cluster c): the segments of c's rows, rows ascending
+        std::vector<int> eptr((size_t)nc * nc + 1, 0), eseg;
+        eseg.reserve(segs.size());
         {
             std::vector<std::vector<int>> bucket(nc);
             for (int cr = 0; cr < nc; ++cr) {
                 for (auto& v : bucket) v.clear();
                 for (int e = clp[cr]; e < clp[cr + 1]; ++e) {
                     const int i = clc[e];
-                    bucket[cr].push_back(-(i + 1));
-                    for (int nn = nptr[i]; nn < nptr[i + 1]; ++nn) bucket[lab[nj[nn]]].push_back(nn);
+                    for (int sidx = rsp[i]; sidx < rsp[i + 1]; ++sidx) bucket[segs[sidx].x].push_back(sidx);
                 }
                 for (int c = 0; c < nc; ++c) {
-                    esrc.insert(esrc.end(), bucket[c].begin(), bucket[c].end());
-                    eptr[(size_t)cr * nc + c + 1] = (int)esrc.size();
+                    eseg.insert(eseg.end(), bucket[c].begin(), bucket[c].end());
+                    eptr[(size_t)cr * nc + c + 1] = (int)eseg.size();
                 }
             }
         }
         TlBufs& tl = h->tl;
         tl.nc = nc;
         tl.m = m;
+        tl.maxmem = maxmem;
         const int nB = (m + kNB - 1) / kNB;
         int* ip = nullptr;
-        if ((rc = upload(h, &ip, lab.data(), lab.size()))) return fail(rc, "");
-        tl.clab = ip;
         if ((rc = upload(h, &ip, clp.data(), clp.size()))) return fail(rc, "");
         tl.cl_ptr = ip;
         if ((rc = upload(h, &ip, clc.data(), clc.size()))) return fail(rc, "");
         tl.cl_cams = ip;
         if ((rc = upload(h, &ip, alone.data(), alone.size()))) return fail(rc, "");
         tl.alone = ip;
-        if ((rc = upload(h, &ip, nrow.data(), nrow.size()))) return fail(rc, "");
-        tl.nbr_row = ip;
+        if ((rc = upload(h, &ip, sperm.data(), sperm.size()))) return fail(rc, "");
+        tl.sperm = ip;
+        if ((rc = upload(h, &ip, rsp.data(), rsp.size()))) return fail(rc, "");
+        tl.rseg_ptr = ip;
         if ((rc = upload(h, &ip, eptr.data(), eptr.size()))) return fail(rc, "");
         tl.ered_ptr = ip;
-        if (esrc.empty()) esrc.push_back(0);
-        if ((rc = upload(h, &ip, esrc.data(), esrc.size()))) return fail(rc, "");
-        tl.ered_src = ip;
+        if (eseg.empty()) eseg.push_back(0);
+        if ((rc = upload(h, &ip, eseg.data(), eseg.size()))) return fail(rc, "");
+        tl.ered_seg = ip;
+        {
+            int4* sp = nullptr;
+            if ((rc = upload(h, &sp, segs.data(), segs.size()))) return fail(rc, "");
+            tl.seg = sp;
+        }
         if ((rc = dd(&tl.u, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Zt, cd * MC))) return fail(rc, "");
-        if ((rc = dd(&tl.Rp, (size_t)C * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
         if ((rc = dd(&tl.gd, 2 * (size_t)C))) return fail(rc, "");
-        if ((rc = dd(&tl.rho[0], 2 * (size_t)C))) return fail(rc, "");
-        tl.rho[1] = tl.rho[0] + C;
-        if ((rc = dd(&tl.Opart, (size_t)std::max<int64_t>(h->n_nbr, 1) * MC * MC))) return fail(rc, "");
-        if ((rc = dd(&tl.Odiag, (size_t)C * MC * MC))) return fail(rc, "");
-        if ((rc = dd(&tl.E, (size_t)m * m))) return fail(rc, "");
-        if ((rc = dd(&tl.Linv, (size_t)m * m))) return fail(rc, "");
-        if ((rc = dd(&tl.Einv, (size_t)m * m))) return fail(rc, "");
-        if ((rc = dd(&tl.Dinv, (size_t)nB * kNB * kNB))) return fail(rc, "");
-        tl.ok = h->cg.status + 2;
-        hipError_t e = hipMemsetAsync(tl.Linv, 0, sizeof(double) * (size_t)m * m, h->stream);
+        if ((rc = dd(&tl.rho[0], 2 * (size_t)nc))) return fail(rc, "");
+        tl.rho[1] = tl.rho[0] + nc;
+        if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
+        for (int sl = 0; sl < 2; ++sl) {
+            if ((rc = dd(&h->Ebuf[sl], (size_t)m * m))) return fail(rc, "");
+            if ((rc = dd(&h->Linvbuf[sl], (size_t)m * m))) return fail(rc, "");
+            if ((rc = dd(&h->Einvbuf[sl], (size_t)m * m))) return fail(rc, "");
+            if ((rc = dd(&h->Dinvbuf[sl], (size_t)nB * kNB * kNB))) return fail(rc, "");
+        }
+        if ((rc = dalloc(h, (void**)&h->okbuf, sizeof(int) * 2))) return fail(rc, "");
+        tl.E = h->Ebuf[0];
+        tl.Einv = h->Einvbuf[0];
+        tl.ok = h->okbuf;
+        hipError_t e = hipMemsetAsync(h->Linvbuf[0], 0, sizeof(double) * (size_t)m * m, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->Linvbuf[1], 0, sizeof(double) * (size_t)m * m, h->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
+        for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
-        h->chol_lds = sizeof(double) * (size_t)m * kPS;
-        h->trinv_lds = sizeof(double) * (size_t)(m + kNB) * kPS;
+        h->chol_lds = sizeof(double) * (size_t)m * kCPS;
+        h->trinv_lds = sizeof(double) * ((size_t)m * kPS + (size_t)kNB * (m + 1));
+        const int DPd = D + (D & 1), CH = D <= 9 ? 32 : 16;
+        h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
+                                        (size_t)maxseg * MC * MC);
+        const int RPWd = kCgThreads / D;
+        h->update_lds = sizeof(double) * (2 * (size_t)RPWd * D + (size_t)maxmem * (MC + 1));
+        if (h->erow_lds > 160 * 1024 || h->update_lds > 160 * 1024)
+            return fail(INSFM_BA_EINVAL, "two-level preconditioner: scene too connected for the LDS budget (use precond 0)");
         (void)hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->chol_lds);
         (void)hipFuncSetAttribute((const void*)k_tl_trinv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->trinv_lds);
+        with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            (void)hipFuncSetAttribute((const void*)k_tl_erow<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->erow_lds);
+            (void)hipFuncSetAttribute((const void*)k_tl_update<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->update_lds);
+            return 0;
+        });
         h->tlon = true;
     }
     if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
+    if (const char* ts = std::getenv("INSFM_TL_SYNC")) h->tl_sync = std::atoi(ts) != 0;
     h->damping = 1.0 / desc->tr_radius;
     h->down = desc->tr_down;
     *out = h;
@@ -1817,7 +1893,8 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 3) {
                 k_tl_spmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
             } else if (which == 4) {
-                int rc2 = run_tl_setup(h, h->cams_cur);
+                int rc2 = run_tl_build(h, h->cams_cur, 0);
+                if (!rc2) rc2 = run_tl_factor(h, 0, h->stream);
                 if (rc2) return rc2;
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
@@ -1860,9 +1937,22 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 6: src = h->b; n = C * D; break;
         case 7: src = h->dc; n = C * D; break;
         case 8: src = h->dp; n = Pl * 3; break;
+        // two-level internals (debug): 9 u, 10 w, 11 Rc, 12/13 E^-1 slot 0/1, 14 row partials [r.u | w.u], 15 r
+        case 9: src = h->tl.u; n = h->tlon ? C * D : 0; break;
+        case 10: src = h->cg.w[0]; n = C * D; break;
+        case 11: src = h->tl.Rc; n = h->tlon ? (size_t)h->tl.m : 0; break;
+        case 12: src = h->Einvbuf[0]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
+        case 13: src = h->Einvbuf[1]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
+        case 14: src = h->tl.gd; n = h->tlon ? 2 * C : 0; break;
+        case 15: src = h->cg.r[0]; n = C * D; break;
+        // 16/17 factor (E slot 0/1, lower = L), 18/19 Dinv slot 0/1 [nB*32*32], 20/21 L^-1 slot 0/1
+        case 16: case 17: src = h->Ebuf[which - 16]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
+        case 18: case 19: src = h->Dinvbuf[which - 18]; n = h->tlon ? (size_t)((h->tl.m + kNB - 1) / kNB) * kNB * kNB : 0; break;
+        case 20: case 21: src = h->Linvbuf[which - 20]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         default: return INSFM_BA_EINVAL;
     }
-    HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (h->side) HIPCHK(hipStreamSynchronize(h->side));
+    if (n) HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return (int64_t)n;
 }

@@ -295,6 +295,8 @@ typedef struct {
     int *clab, nclust;           /* cluster label per camera, number of clusters */
     int *csize;                  /* cameras per cluster */
     double* lin_cams;            /* copy of the linearization point (coarse basis) */
+    double* prev_einv;           /* coarse inverse of the previous solve (lag rule: see ora_pcg) */
+    int prev_ok, have_prev, fresh_lin;
     /* LM state */
     double damping, down, loss;
     int have_loss;
@@ -336,7 +338,7 @@ static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *
 static int ora_aggregate(ora_t* h, int K);
 /* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU factorizes E in one workgroup's LDS):
  * while the aggregation yields more clusters, it is redone with twice the target size. */
-#define COARSE_MAX 576
+#define COARSE_MAX 288
 static void ora_cluster_cameras(ora_t* h) {
     int K = h->cluster_size;
     while (ora_aggregate(h, K) * (h->D + 1) > COARSE_MAX) K *= 2;
@@ -597,7 +599,7 @@ void ora_destroy(ora_t* h) {
     void* ptrs[] = {h->uv, h->pp, h->cam, h->pt, h->pt_ptr, h->cam_ptr, h->cam_obs, h->row_ptr, h->col, h->lo_ptr,
                     h->lo_col, h->lo_blk, h->W, h->V, h->gp, h->U, h->gc, h->Vinv, h->y, h->S, h->b, h->Minv, h->x,
                     h->r, h->z, h->p, h->q, h->dp, h->cams_new, h->pts_new, h->partial,
-                    h->clab, h->csize, h->lin_cams};
+                    h->clab, h->csize, h->lin_cams, h->prev_einv};
     for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
     free(h);
 }
@@ -631,6 +633,7 @@ double ora_cost(ora_t* h, const double* cams, const double* pts, double* sq_out)
 /* Linearize at (cams, pts): W_o = J~c^T J~p (D x 3), V_p = sum J~p^T J~p (sym6), g_p = -sum J~p^T r~,
  * U_c = sum J~c^T J~c (D x D), g_c = -sum J~c^T r~.  Unclamped, undamped. */
 void ora_linearize(ora_t* h, const double* cams, const double* pts) {
+    h->fresh_lin = 1;
     if (!h->lin_cams) h->lin_cams = (double*)malloc(sizeof(double) * (size_t)h->C * h->stride);
     memcpy(h->lin_cams, cams, sizeof(double) * (size_t)h->C * h->stride);
     int D = h->D, model = h->model;
@@ -984,7 +987,22 @@ int ora_pcg(ora_t* h, double* xout) {
         Rc = (double*)malloc(sizeof(double) * (size_t)m);
         yc = (double*)malloc(sizeof(double) * (size_t)m);
         u = (double*)malloc(sizeof(double) * n);
-        if (!ora_coarse_setup(h, Lfac, Zt, Einv)) twolev = 0;
+        /* Lag rule: the first solve after a linearization runs with the coarse inverse of the previous solve, so the
+         * GPU factorizes E_k on a side stream while that CG runs; later solves at the same linearization (rejected LM
+         * trials, whose damping can jump by 16x per retry) and the very first solve use their own E.  Any SPD E^-1
+         * keeps M~ SPD, so the lag only changes the iteration count (a few percent). */
+        int okc = ora_coarse_setup(h, Lfac, Zt, Einv);
+        if (!h->prev_einv) h->prev_einv = (double*)malloc(sizeof(double) * (size_t)m * m);
+        if (h->have_prev && h->fresh_lin) {
+            for (size_t e = 0; e < (size_t)m * m; ++e) { double tmp = Einv[e]; Einv[e] = h->prev_einv[e]; h->prev_einv[e] = tmp; }
+            int o = h->prev_ok; h->prev_ok = okc; okc = o;
+        } else {
+            memcpy(h->prev_einv, Einv, sizeof(double) * (size_t)m * m);
+            h->prev_ok = okc;
+            h->have_prev = 1;
+        }
+        h->fresh_lin = 0;
+        if (!okc) twolev = 0;
     }
     for (int i = 0; i < C; ++i) {
         const double* Li = h->Minv + (size_t)i * DD;

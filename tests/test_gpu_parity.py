@@ -231,3 +231,31 @@ def test_two_level_step_with_coarse_active_and_fewer_iterations():
         res[pc] = (lg, sum(its))
     assert res[1][1] * 2 < res[0][1], res
     assert abs(res[1][0] - res[0][0]) / res[0][0] < 1e-6, res
+
+
+@pytest.mark.parametrize("model", (2, 4, 6))
+def test_repeated_solves_lagged_coarse_inverse(model):
+    """Consecutive solves on one engine under the lag rule: the first solve after a linearization runs with the coarse
+    inverse of the previous solve (factorized on the side stream while that CG ran), retries at the same
+    linearization use their own.  Every solve matches the oracle's (same rule): iterations and dc.  The coarse sizes
+    here (m = 45 / 65 / 85) end in a partial dense block."""
+    prob = make_problem(30, 800, seed=5, model=model)
+    cams, pts = prob.cams_init.copy(), prob.points_init.copy()
+    for rep in range(3):
+        eng, ora = engines(prob, cluster_size=6)
+        # (relinearize?, damping factor): LM-like sequences -- fresh trials change f by <= 16x, retries by more
+        for k, (relin, f) in enumerate([(1, 1 + 1e-4), (1, 1 + 5e-5), (1, 1 + 8e-4), (0, 1 + 1.3e-2), (0, 1.2),
+                                        (1, 1 + 6e-4)]):
+            if relin:
+                eng.debug_linearize(dev(cams), dev(pts))
+                ora.linearize(cams, pts)
+            it_g = eng.debug_solve(f)
+            it_o = ora.solve(f)
+            assert it_g == it_o, (rep, k, it_g, it_o)
+            err = rel(eng.debug_get(7, (prob.n_cams, eng.D)), ora.get(O.DC))
+            # own-E solves: 1e-8 like every other solve.  Lagged solves run with the previous solve's E^-1, a worse
+            # fit to the current S~, which amplifies the (last-bit) differences of the two E^-1 computations: up to
+            # ~1e-7 seen with D = 16 (cond(E) ~ 4e11); still 100x inside the PCG tolerance (1e-5).
+            lagged = relin and k > 0
+            assert err < (1e-6 if lagged else 1e-8), (rep, k, err)
+        eng.close()
