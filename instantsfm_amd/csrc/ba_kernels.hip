@@ -890,7 +890,8 @@ struct insfm_ba {
     double *Ebuf[2]{}, *Dinvbuf[2]{}, *Linvbuf[2]{}, *Einvbuf[2]{};
     int* okbuf = nullptr;  // [2]
     hipStream_t side = nullptr;
-    hipEvent_t ev_E = nullptr, ev_fact[2]{};
+    hipEvent_t ev_E = nullptr, ev_built = nullptr, ev_fact[2]{};
+    bool built_pending = false;
     long long tl_solves = 0;
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
     bool tl_sync = false;  // INSFM_TL_SYNC=1: factorize on the main stream (debug)
@@ -1104,22 +1105,26 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
 }
 
-// Two-level setup, part 1 (main stream, after k_cg_factor / k_cg_scale): coarse basis and E into slot `slot`.
-int run_tl_build(insfm_ba* h, const double* cams, int slot) {
+// Two-level setup, part 1: coarse basis Z~ (on `basis_stream`, the CG needs it) and E into slot `slot` (on
+// `build_stream`, which must already be ordered after the basis).
+int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
+    const int C = h->C;
+    return with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        constexpr int MC = kD<M> + 1;
+        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl);
+        return launch_err(h, "k_tl_basis");
+    });
+}
+
+int run_tl_build(insfm_ba* h, int slot, hipStream_t stream) {
     const int C = h->C, m = h->tl.m;
     TlBufs tl = h->tl;
     tl.E = h->Ebuf[slot];
-    int rc = with_model(h->model, [&](auto mc) -> int {
-        constexpr int M = decltype(mc)::value;
-        constexpr int MC = kD<M> + 1;
-        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, h->stream>>>(C, cams, h->Lf, tl);
-        return launch_err(h, "k_tl_basis");
-    });
-    if (rc) return rc;
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
-        k_tl_erow<DV><<<C, kThreads, h->erow_lds, h->stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
-        k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, h->stream>>>(tl);
+        k_tl_erow<DV><<<C, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
+        k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, stream>>>(tl);
         return launch_err(h, "k_tl_erow/ereduce");
     });
 }
@@ -1136,16 +1141,21 @@ int run_tl_factor(insfm_ba* h, int slot, hipStream_t stream) {
     return launch_err(h, "two-level factorization");
 }
 
-// Per solve: build E_n on the main stream, factorize it on the side stream, and point the CG at the coarse inverse of
-// the previous solve when this is the first solve after a linearization (otherwise at its own, waiting for the
-// factorization) -- the oracle's lag rule (ora_pcg).
+// Per solve (after k_cg_factor / k_cg_scale on the main stream): the basis Z~ on the main stream, then E_n's build
+// (reads S~ and Z~) and factorization on the side stream.  The CG is pointed at the coarse inverse of the previous
+// solve when this is the first solve after a linearization (it starts right away), otherwise at its own (it waits
+// for the factorization) -- the oracle's lag rule (ora_pcg).  The next solve's k_cg_scale / k_tl_basis overwrite
+// S~ / Z~, so they wait for ev_built (run_solve).
 int run_tl_setup(insfm_ba* h, const double* cams) {
     const int slot = (int)(h->tl_solves & 1);
-    int rc = run_tl_build(h, cams, slot);
-    if (rc) return rc;
     hipStream_t fs = h->tl_sync ? h->stream : h->side;
+    int rc = run_tl_basis(h, cams, h->stream);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(h->ev_E, h->stream));
     HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
+    if ((rc = run_tl_build(h, slot, fs))) return rc;
+    HIPCHK(hipEventRecord(h->ev_built, fs));
+    h->built_pending = true;
     if ((rc = run_tl_factor(h, slot, fs))) return rc;
     HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
@@ -1197,6 +1207,10 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
         if (rc) return rc;
         HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+        if (h->built_pending) {  // the side stream's E build of the previous solve still reads S~ / Z~
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_built, 0));
+            h->built_pending = false;
+        }
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg);
@@ -1331,6 +1345,7 @@ void insfm_ba_destroy(insfm_ba* h) {
         (void)hipStreamDestroy(h->side);
     }
     if (h->ev_E) (void)hipEventDestroy(h->ev_E);
+    if (h->ev_built) (void)hipEventDestroy(h->ev_built);
     for (auto& e : h->ev_fact)
         if (e) (void)hipEventDestroy(e);
     delete h;
@@ -1702,6 +1717,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         if (e == hipSuccess) e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_built, hipEventDisableTiming);
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
@@ -1884,6 +1900,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
     if (which >= 2 && !h->tlon) return INSFM_BA_EINVAL;
+    if (h->side) HIPCHK(hipStreamSynchronize(h->side));  // its pending E build / factorization must not interleave
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
     int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
@@ -1893,7 +1910,8 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 3) {
                 k_tl_spmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
             } else if (which == 4) {
-                int rc2 = run_tl_build(h, h->cams_cur, 0);
+                int rc2 = run_tl_basis(h, h->cams_cur, h->stream);
+                if (!rc2) rc2 = run_tl_build(h, 0, h->stream);
                 if (!rc2) rc2 = run_tl_factor(h, 0, h->stream);
                 if (rc2) return rc2;
             } else if (which == 0)
