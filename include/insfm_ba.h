@@ -119,7 +119,7 @@ const char* insfm_ba_last_error(const insfm_ba* h);
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cam_params, const double* points);
 /* Build and solve the damped system for cumulative damping factor f; returns PCG iterations or a negative code. */
 int insfm_ba_debug_solve(insfm_ba* h, double f);
-/* Copy an internal buffer to HOST memory: 0 W[N,D,3] 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
+/* Copy an internal buffer to HOST memory: 0 W[N,3,D] (column-major blocks) 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
  * solve)[nnzb,D,D] 6 b[C,D] 7 dc[C,D] 8 dp[P,3].  Returns the number of doubles copied or a negative code. */
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
 /* Device time per launch (us, hipEvents on the library stream) of `reps` back-to-back launches of one kernel on the

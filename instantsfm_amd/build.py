@@ -1,4 +1,5 @@
 """Build the in-tree HIP library for gfx950 (hipcc cross-compiles without a GPU)."""
+import glob
 import os
 import subprocess
 import sys
@@ -6,7 +7,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "ba_kernels.hip")
-DEPS = [SRC, os.path.join(HERE, "csrc", "ba_device.h"), os.path.join(REPO, "include", "insfm_ba.h")]
+DEPS = [SRC, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), os.path.join(REPO, "include", "insfm_ba.h")]
 OUT = os.path.join(HERE, "_lib", "libinsfm_ba.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")

@@ -35,6 +35,10 @@ using namespace insfm;
 namespace {
 
 constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgroup
+#ifndef INSFM_SCHUR_WAVES
+#define INSFM_SCHUR_WAVES 8
+#endif
+constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (non-deterministic mode)
 
 // ------------------------------------------------------------------------------------------------------------
 // reductions
@@ -81,7 +85,8 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // ------------------------------------------------------------------------------------------------------------
 // linearization
 // ------------------------------------------------------------------------------------------------------------
-// One thread per (local) track: every observation's weighted J gives W_o = J~c^T J~p (stored [o][D][3]); the track
+// One thread per (local) track: every observation's weighted J gives W_o = J~c^T J~p (stored [o][3][D]: a group of D
+// lanes reads each column of W_o as one contiguous segment in k_schur); the track
 // reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~ in registers.
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_lin_points(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_points(int Pl, const int* __re
 #pragma unroll
         for (int a = 0; a < D; ++a)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) Wo[a * 3 + k] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+            for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
         Vs[0] += Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
         Vs[1] += Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
         Vs[2] += Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
@@ -237,6 +242,13 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 // and adds column b of -W^_o W_q^T into slot(cam[q]) with LDS f64 atomics (ds_add_f64).  Each camera's
 // observation list is sorted by partner count so the groups of a wave stay balanced.
 // ------------------------------------------------------------------------------------------------------------
+// LDS strides of k_schur.  The D groups of a wave add into D different blocks at the same (row, column): with a
+// block stride that is a multiple of the 64-bank period (D*D = 64 doubles = 512 B for D = 8) every group lands on the
+// same banks (8-way conflicts, SQ_LDS_BANK_CONFLICT ~1.6x the busy cycles); 8 extra doubles spread the groups over 4
+// bank quarters.  The W^ staging of each group gets an odd stride for the same reason.
+__host__ __device__ constexpr int schur_bs(int D) { return D * D + ((D * D) % 16 == 0 ? 8 : 0); }
+__host__ __device__ constexpr int schur_ws(int D) { return D * 4 + 1; }
+
 template <int D, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
@@ -248,17 +260,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                                                       double cmin, double cmax, int add_diag, double* __restrict__ S,
                                                       double* __restrict__ b) {
     constexpr int DD = D * D;
+    constexpr int BS = schur_bs(D);  // LDS stride of an accumulated block (padded off the 64-bank period)
+    constexpr int WS = schur_ws(D);  // LDS stride of a group's W^ staging
     constexpr int NG = 64 / D;  // observation groups per wave
     constexpr int NT = WAVES * 64;
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int4 wk = work[blockIdx.x];
     const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
     double* acc = sh;
-    double* wsh = acc + (size_t)nb * DD;           // [WAVES][NG][D][4]  W^ rows (padded)
-    double* bacc = wsh + (size_t)WAVES * NG * D * 4;  // [D]
+    double* wsh = acc + (size_t)nb * BS;           // [WAVES][NG][WS]  W^ rows ([D][4], padded group stride)
+    double* bacc = wsh + (size_t)WAVES * NG * WS;  // [D]
     int* slot = reinterpret_cast<int*>(bacc + D);  // [C]
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    for (int k = t; k < nb * DD; k += NT) acc[k] = 0.0;
+    for (int k = t; k < nb * BS; k += NT) acc[k] = 0.0;
     for (int k = t; k < C; k += NT) slot[k] = -1;
     if (t < D) bacc[t] = 0.0;
     __syncthreads();
@@ -267,7 +281,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
     const bool diag_chunk = (kb == row_ptr[i]);
     const int g = lane / D, cb = lane - g * D;
     const bool active = g < NG;
-    double* my_wh = wsh + ((size_t)(wv * NG + (active ? g : 0)) * D) * 4;
+    double* my_wh = wsh + (size_t)(wv * NG + (active ? g : 0)) * WS;
     double breg = 0.0;
     const int ob = cam_ptr[i], oe = cam_ptr[i + 1];
     for (int base = ob + wv * NG; base < oe; base += WAVES * NG) {
@@ -279,8 +293,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
             const int p = ptl[o];
             const double* vi = Vinv + 6 * (size_t)p;
             const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
-            const double* wo = W + (size_t)o * D * 3 + cb * 3;
-            const double w0 = wo[0], w1 = wo[1], w2 = wo[2];
+            const double* wo = W + (size_t)o * D * 3 + cb;
+            const double w0 = wo[0], w1 = wo[D], w2 = wo[2 * D];
             my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
             my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
             my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
@@ -316,8 +330,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                 cj[u] = -1;
                 if (k0 + u < n) {
                     const int q = qs + k0 + u;
-                    const double* wq = W + (size_t)q * D * 3 + cb * 3;
-                    x[u][0] = wq[0]; x[u][1] = wq[1]; x[u][2] = wq[2];
+                    const double* wq = W + (size_t)q * D * 3 + cb;
+                    x[u][0] = wq[0]; x[u][1] = wq[D]; x[u][2] = wq[2 * D];
                     cj[u] = cam[q];
                 }
             }
@@ -326,7 +340,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                 if (cj[u] >= 0) {
                     const int sl = slot[cj[u]];
                     if (sl >= 0) {
-                        double* dst = acc + (size_t)sl * DD + cb;
+                        double* dst = acc + (size_t)sl * BS + cb;
 #pragma unroll
                         for (int a2 = 0; a2 < D; ++a2)
                             atomicAdd(dst + a2 * D, -(wh[a2][0] * x[u][0] + wh[a2][1] * x[u][1] + wh[a2][2] * x[u][2]));
@@ -341,7 +355,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
     double* Sout = S + (size_t)kb * DD;
     const double* Ui = U + (size_t)i * DD;
     for (int k = t; k < nb * DD; k += NT) {
-        double v = acc[k];
+        double v = acc[(k / DD) * BS + k % DD];
         if (diag_chunk && add_diag && k < DD) {
             const int a2 = k / D, bb = k % D;
             double u = Ui[k];
@@ -722,9 +736,9 @@ __global__ __launch_bounds__(kThreads) void k_backsub(int Pl, const int* __restr
                 double s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
-                    s0 += Wo[a * 3 + 0] * d[a];
-                    s1 += Wo[a * 3 + 1] * d[a];
-                    s2 += Wo[a * 3 + 2] * d[a];
+                    s0 += Wo[a] * d[a];
+                    s1 += Wo[D + a] * d[a];
+                    s2 += Wo[2 * D + a] * d[a];
                 }
                 t0 -= s0; t1 -= s1; t2 -= s2;
             }
@@ -1196,7 +1210,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                     h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
             else
-                k_schur<DV, 4><<<h->nwork, 256, h->schur_lds, h->stream>>>(
+                k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
                     h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
                     h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
@@ -1482,10 +1496,10 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     for (int i = 0; i < C; ++i) { pup[rptr[i]] = 0; plo[rptr[i]] = 0; }  // diagonal blocks: unused slots
     if (nj.empty()) nj.push_back(0);
     // Schur work items: split long rows so a chunk fits the LDS budget
-    const size_t wsh_lds = sizeof(double) * 4 * (64 / D) * D * 4;  // W^ staging for up to 4 waves
+    const size_t wsh_lds = sizeof(double) * kSchurWaves * (64 / D) * schur_ws(D);  // W^ staging, up to kSchurWaves waves
     const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
-    const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * D * D));
+    const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * schur_bs(D)));
     std::vector<int4> work;
     int maxc = 1;
     for (int i = 0; i < C; ++i) {
@@ -1499,9 +1513,11 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
             maxc = std::max(maxc, ke - kb);
         }
     }
+    // Row order is kept: measured against heaviest-first (LPT) and XCD-contiguous orders it is the fastest
+    // (651 vs 667 / 688 us on config 3): neighbouring rows launched together share partner W records in L2/MALL.
     h->nwork = (int)work.size();
     h->max_chunk = maxc;
-    h->schur_lds = sizeof(double) * ((size_t)maxc * D * D + D) + wsh_lds + sizeof(int) * (size_t)C;
+    h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
 
     int rc;
@@ -1595,7 +1611,8 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
-        (void)hipFuncSetAttribute((const void*)k_schur<DV, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)h->schur_lds);
         return 0;
     });
     if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
@@ -1727,7 +1744,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
                                         (size_t)maxseg * MC * MC);
         const int RPWd = kCgThreads / D;
-        h->update_lds = sizeof(double) * (2 * (size_t)RPWd * D + (size_t)maxmem * (MC + 1));
+        h->update_lds = sizeof(double) * (2 * (size_t)RPWd * D + (size_t)RPWd * D * MC + (size_t)maxmem * (MC + 1));
         if (h->erow_lds > 160 * 1024 || h->update_lds > 160 * 1024)
             return fail(INSFM_BA_EINVAL, "two-level preconditioner: scene too connected for the LDS budget (use precond 0)");
         (void)hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->chol_lds);
@@ -1918,7 +1935,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                 h->Lf, h->cg, 0);
             else
-                k_schur<DV, 4><<<h->nwork, 256, h->schur_lds, h->stream>>>(
+                k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
                     h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
                     h->Vinv, h->y, h->U, h->gc, 1.0, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
         }

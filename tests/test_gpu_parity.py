@@ -45,7 +45,7 @@ def test_linearize_parity(model):
     eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
     ora.linearize(prob.cams_init, prob.points_init)
     N, P, C, D = prob.n_obs, prob.n_points, prob.n_cams, eng.D
-    assert rel(eng.debug_get(0, (N, D, 3)), ora.get(O.W)) < 1e-12
+    assert rel(eng.debug_get(0, (N, 3, D)).transpose(0, 2, 1), ora.get(O.W)) < 1e-12  # stored [o][3][D]
     assert rel(eng.debug_get(1, (P, 6)), ora.get(O.V)) < 1e-12
     assert rel(eng.debug_get(2, (P, 3)), ora.get(O.GP)) < 1e-12
     assert rel(eng.debug_get(3, (C, D, D)), ora.get(O.U)) < 1e-10
