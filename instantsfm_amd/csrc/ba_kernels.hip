@@ -39,6 +39,9 @@ constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgr
 #define INSFM_SCHUR_WAVES 8
 #endif
 constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (non-deterministic mode)
+#ifndef SCHUR_UP
+#define SCHUR_UP 10
+#endif
 
 // ------------------------------------------------------------------------------------------------------------
 // reductions
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
         int nmax = n;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-        constexpr int UP = 4;  // partners in flight per group
+        constexpr int UP = SCHUR_UP;  // partners in flight per group
         for (int k0 = 0; k0 < nmax; k0 += UP) {
             double x[UP][3];
             int cj[UP];
