@@ -243,7 +243,10 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 // group owns column b.  The group forms W^_o = W_o V_p^-1 (row b per lane, shared through LDS), then walks the
 // upper partners q of track p -- tracks are sorted by camera at create, so they are exactly [ustart[o], end) --
 // and adds column b of -W^_o W_q^T into slot(cam[q]) with LDS f64 atomics (ds_add_f64).  Each camera's
-// observation list is sorted by partner count so the groups of a wave stay balanced.
+// observation list is sorted by partner count so the groups of a wave stay balanced.  The kernel is bound by the
+// chain of dependent loads per round, not by bytes (cache-resident partner data: no faster): every own-observation
+// index comes from one descriptor {o, p, partner range} prefetched a round ahead.  Measured and rejected: a
+// precomputed per-pair block position (36 MB streamed per trial, slower than cam[] from cache + an LDS lookup).
 // ------------------------------------------------------------------------------------------------------------
 // LDS strides of k_schur.  The D groups of a wave add into D different blocks at the same (row, column): with a
 // block stride that is a multiple of the 64-bank period (D*D = 64 doubles = 512 B for D = 8) every group lands on the
@@ -257,6 +260,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
                                                       const int* __restrict__ pt_ptr, const int* __restrict__ ustart,
+                                                      const int4* __restrict__ sdesc,
                                                       const int* __restrict__ cam, const double* __restrict__ W,
                                                       const double* __restrict__ Vinv, const double* __restrict__ y,
                                                       const double* __restrict__ U, const double* __restrict__ gc, double f,
@@ -287,13 +291,25 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
     double* my_wh = wsh + (size_t)(wv * NG + (active ? g : 0)) * WS;
     double breg = 0.0;
     const int ob = cam_ptr[i], oe = cam_ptr[i + 1];
+    // per own observation one descriptor {o, p, partner begin, partner end}: one load gives every index, and the next
+    // round's descriptor is loaded while the current round runs (the round chain is latency-bound, not byte-bound)
+    int4 dnext = make_int4(0, 0, 0, 0);
+    {
+        const int e0 = ob + wv * NG + g;
+        if (active && e0 < oe) dnext = sdesc[e0];
+    }
     for (int base = ob + wv * NG; base < oe; base += WAVES * NG) {
         const int e = base + g;
         const bool has = active && e < oe;
+        const int4 dcur = dnext;
+        {
+            const int en = e + WAVES * NG;
+            if (active && en < oe) dnext = sdesc[en];
+        }
         int qs = 0, qe = 0;
         if (has) {
-            const int o = cam_obs[e];
-            const int p = ptl[o];
+            const int o = dcur.x;
+            const int p = dcur.y;
             const double* vi = Vinv + 6 * (size_t)p;
             const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
             const double* wo = W + (size_t)o * D * 3 + cb;
@@ -305,8 +321,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                 const double* yp = y + 3 * (size_t)p;
                 breg -= w0 * yp[0] + w1 * yp[1] + w2 * yp[2];
             }
-            qs = ustart[o];
-            qe = pt_ptr[p + 1];
+            qs = dcur.z;
+            qe = dcur.w;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -866,6 +882,7 @@ struct insfm_ba {
     int *cam = nullptr, *ptl = nullptr, *pt_ptr = nullptr, *cam_ptr = nullptr, *cam_obs = nullptr;
     int *row_ptr = nullptr, *col = nullptr, *blk_row = nullptr, *ustart = nullptr;
     int *nbr_ptr = nullptr, *nbr_j = nullptr, *pos_up = nullptr, *pos_lo = nullptr;
+    int4* sdesc = nullptr;  // k_schur: per camera-major own observation {o, p, partner begin, partner end}
     double* Sn = nullptr;  // row-contiguous scaled neighbour blocks for the CG (both triangles, padded rows)
     int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
@@ -1209,12 +1226,12 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             constexpr int DV = decltype(dc_)::value;
             if (h->d.deterministic)
                 k_schur<DV, 1><<<h->nwork, 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
                     h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
             else
                 k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
                     h->Vinv, h->y,
                     h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
             return launch_err(h, "k_schur");
@@ -1440,6 +1457,11 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
                 return (lptr[lptl[x] + 1] - lust[x]) > (lptr[lptl[y] + 1] - lust[y]);
             });
     }
+    std::vector<int4> sdesc(std::max(Nl, 1));
+    for (int e = 0; e < Nl; ++e) {
+        const int o = cobs[e], p = lptl[o];
+        sdesc[e] = make_int4(o, p, lust[o], lptr[p + 1]);
+    }
     // global upper pattern (identical on every rank)
     std::vector<int> gcptr(C + 1, 0), gcobs(N);
     for (int i = 0; i < N; ++i) gcptr[cam_idx[i] + 1]++;
@@ -1540,6 +1562,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     if ((rc = upload(h, &h->col, cols.data(), cols.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->blk_row, brow.data(), brow.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->ustart, lust.data(), lust.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->sdesc, sdesc.data(), sdesc.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->nbr_ptr, nptr.data(), nptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->nbr_j, nj.data(), nj.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pos_up, pup.data(), pup.size()))) return fail(rc, "");
@@ -1939,7 +1962,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                                                                 h->Lf, h->cg, 0);
             else
                 k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->cam, h->W,
+                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
                     h->Vinv, h->y, h->U, h->gc, 1.0, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
         }
         return launch_err(h, "debug_time_kernel");
