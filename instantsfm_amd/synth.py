@@ -242,3 +242,79 @@ def to_scene(problem: BAProblem, use_init=True, image_features_dtype=np.float64)
         tracks[p] = Track(id=p, xyz=pts[p].copy(), observations=obs_pairs[L_ptr[p]:L_ptr[p + 1]].copy(),
                           is_initialized=True)
     return cameras, images, tracks
+
+
+# ------------------------------------------------------------------------------------------------------------
+# global positioning scenes (TorchGP.Optimize, global_positioning.py:45-206)
+# ------------------------------------------------------------------------------------------------------------
+@dataclass
+class GPProblem:
+    trans: np.ndarray        # [N, 3] world-frame ray of each observation (R_img^T features_undist, unit norm)
+    cam_idx: np.ndarray      # [N] int32
+    pt_idx: np.ndarray       # [N] int32, nondecreasing
+    fcam: np.ndarray         # [C] 1.0 calibrated camera (has_prior_focal_length), 0.5 otherwise
+    sfree: np.ndarray        # [N] int32: 1 scale optimized, 0 fixed (valid depth)
+    cams_gt: np.ndarray      # [C, 3] camera positions
+    points_gt: np.ndarray    # [P, 3]
+    cams_init: np.ndarray
+    points_init: np.ndarray
+    scales_init: np.ndarray  # [N] (1 where free, 1/depth where fixed, as TorchGP builds them)
+
+    @property
+    def n_cams(self):
+        return self.cams_init.shape[0]
+
+    @property
+    def n_points(self):
+        return self.points_init.shape[0]
+
+    @property
+    def n_obs(self):
+        return self.trans.shape[0]
+
+
+def make_gp_problem(n_cams, n_points, track_len=10, seed=0, window=30, ray_sigma=0.002, outlier_frac=0.01,
+                    calibrated_frac=0.8, depth_frac=0.0, init="random", scene_scale=100.0, init_sigma=0.5):
+    """Seeded global-positioning scene on the same ring geometry as make_problem: rays from camera centres to points
+    (angular noise ray_sigma, outlier_frac of rays off by 0.05-0.2 rad), a calibrated_frac of cameras with factor 1
+    (else 0.5), a depth_frac of observations with a fixed scale 1/depth.  init="random" follows
+    TorchGP.InitializeRandomPositions (uniform in +-scene_scale, global_positioning.py:22-39); "perturbed" starts
+    from ground truth + N(0, init_sigma)."""
+    rng = np.random.default_rng(seed)
+    C, P, L = int(n_cams), int(n_points), int(track_len)
+    ang = 2 * np.pi * np.arange(C) / C
+    centers = np.stack([30 * np.cos(ang), 30 * np.sin(ang), rng.uniform(-2, 2, C)], axis=1)
+    d = rng.normal(size=(P, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    points = d * (8.0 * rng.uniform(0, 1, (P, 1)) ** (1.0 / 3.0))
+    if C <= 2 * window + 1:
+        cams_of = np.argsort(rng.uniform(size=(P, C)), axis=1)[:, :L]
+    else:
+        home = rng.integers(0, C, P)
+        offs = np.argsort(rng.uniform(size=(P, 2 * window + 1)), axis=1)[:, :L] - window
+        cams_of = (home[:, None] + offs) % C
+    cams_of = np.sort(cams_of, axis=1)
+    cam_idx = cams_of.reshape(-1).astype(np.int32)
+    pt_idx = np.repeat(np.arange(P, dtype=np.int32), L)
+    v = points[pt_idx] - centers[cam_idx]
+    depth = np.linalg.norm(v, axis=1)
+    rays = v / depth[:, None]
+    n = rays.shape[0]
+    sig = np.full(n, ray_sigma)
+    n_out = int(round(outlier_frac * n))
+    if n_out:
+        sig[rng.choice(n, n_out, replace=False)] = rng.uniform(0.05, 0.2, n_out)
+    rays = rays + rng.normal(size=rays.shape) * sig[:, None]
+    rays /= np.linalg.norm(rays, axis=1, keepdims=True)
+    fcam = np.where(rng.uniform(size=C) < calibrated_frac, 1.0, 0.5)
+    has_depth = rng.uniform(size=n) < depth_frac
+    sfree = (~has_depth).astype(np.int32)
+    scales_init = np.where(has_depth, 1.0 / depth, 1.0)
+    if init == "random":
+        cams_init = scene_scale * rng.uniform(-1, 1, (C, 3))
+        points_init = scene_scale * rng.uniform(-1, 1, (P, 3))
+    else:
+        cams_init = centers + rng.normal(0, init_sigma, (C, 3))
+        points_init = points + rng.normal(0, init_sigma, (P, 3))
+    return GPProblem(np.ascontiguousarray(rays), cam_idx, pt_idx, fcam, sfree, centers, points,
+                     np.ascontiguousarray(cams_init), np.ascontiguousarray(points_init), np.ascontiguousarray(scales_init))

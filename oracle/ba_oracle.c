@@ -31,6 +31,7 @@
 #endif
 
 #define MAXD 16
+#define ORA_GP 100   /* ora_create "model" of the global-positioning problem (ora_gp_create) */
 #define CHUNK 4096
 
 /* ------------------------------------------------------------------------------------------ */
@@ -296,6 +297,12 @@ typedef struct {
     int *csize;                  /* cameras per cluster */
     double* lin_cams;            /* copy of the linearization point (coarse basis) */
     double* prev_einv;           /* coarse inverse of the previous solve (lag rule: see ora_pcg) */
+    int kind;                    /* 0 bundle adjustment, 1 global positioning (ora_gp_*) */
+    int u_predamped;             /* U already holds the damped camera blocks (global positioning) */
+    /* global positioning (TorchGP.Optimize): per obs ray t, factor f, scale-free flag, linearization terms */
+    double *gp_t, *gp_f, *gp_beta, *gp_a, *gp_r, *gp_hss, *gp_gs, *gp_ds, *gp_hx, *gp_hc, *gp_gx, *gp_gc;
+    double *gp_scales_new;
+    int* gp_sfree;
     int prev_ok, have_prev, fresh_lin;
     /* LM state */
     double damping, down, loss;
@@ -454,10 +461,14 @@ int ora_clusters(const ora_t* h, int* lab) {
  *   rho = -R tau - [t]x R omega + sigma t,   phi = -R omega,
  * plus one column per intrinsic.  A camera alone in its cluster gets [I_D | 0] instead (the 7 similarity modes of a
  * single camera are linearly dependent). */
-static void coarse_basis(int D, const double* cam, int alone, double* G) {
+static void coarse_basis(int D, const double* cam, int alone, double* G, int kind) {
     const int MC = D + 1;
     for (int k = 0; k < D * MC; ++k) G[k] = 0.0;
     if (alone) { for (int a = 0; a < D; ++a) G[a * MC + a] = 1.0; return; }
+    if (kind == 1) {  /* global positioning: camera position c; gauge = translation (I) and scaling about 0 (c) */
+        for (int a = 0; a < 3; ++a) { G[a * MC + a] = 1.0; G[a * MC + 3] = cam[a]; }
+        return;
+    }
     const double *t = cam, *q = cam + 3;
     double qx = q[0], qy = q[1], qz = q[2], w = q[3];
     double Kq[9] = {0, -qz, qy, qz, 0, -qx, -qy, qx, 0}, R[9];
@@ -482,10 +493,12 @@ static void coarse_basis(int D, const double* cam, int alone, double* G) {
 
 ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* cam, const int* pt, const double* pp,
                   const double* dopt, const int* iopt) {
-    if (ora_n_intr(model) < 0 || C <= 0 || P <= 0 || N <= 0) return NULL;
+    const int gpk = (model == ORA_GP);
+    if ((!gpk && ora_n_intr(model) < 0) || C <= 0 || P <= 0 || N <= 0) return NULL;
     for (int i = 1; i < N; ++i) if (pt[i] < pt[i - 1]) return NULL; /* track-major required */
     ora_t* h = (ora_t*)calloc(1, sizeof(ora_t));
-    h->model = model; h->ni = ora_n_intr(model); h->D = 6 + h->ni; h->stride = 7 + h->ni;
+    h->model = model; h->kind = gpk;
+    h->ni = gpk ? 0 : ora_n_intr(model); h->D = gpk ? 3 : 6 + h->ni; h->stride = gpk ? 3 : 7 + h->ni;
     h->C = C; h->P = P; h->N = N;
     h->delta = dopt[0]; h->radius0 = dopt[1]; h->rmax = dopt[2]; h->rmin = dopt[3]; h->up = dopt[4];
     h->down0 = dopt[5]; h->factor = dopt[6]; h->high = dopt[7]; h->low = dopt[8]; h->cmin = dopt[9];
@@ -497,8 +510,10 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
 #endif
     h->damping = 1.0 / h->radius0; h->down = h->down0;
     int D = h->D;
-    h->uv = (double*)malloc(sizeof(double) * 2 * N); memcpy(h->uv, uv, sizeof(double) * 2 * N);
-    h->pp = (double*)malloc(sizeof(double) * 2 * C); memcpy(h->pp, pp, sizeof(double) * 2 * C);
+    if (!gpk) {
+        h->uv = (double*)malloc(sizeof(double) * 2 * N); memcpy(h->uv, uv, sizeof(double) * 2 * N);
+        h->pp = (double*)malloc(sizeof(double) * 2 * C); memcpy(h->pp, pp, sizeof(double) * 2 * C);
+    }
     h->cam = (int*)malloc(sizeof(int) * N); memcpy(h->cam, cam, sizeof(int) * N);
     h->pt = (int*)malloc(sizeof(int) * N); memcpy(h->pt, pt, sizeof(int) * N);
     /* track pointers */
@@ -599,7 +614,9 @@ void ora_destroy(ora_t* h) {
     void* ptrs[] = {h->uv, h->pp, h->cam, h->pt, h->pt_ptr, h->cam_ptr, h->cam_obs, h->row_ptr, h->col, h->lo_ptr,
                     h->lo_col, h->lo_blk, h->W, h->V, h->gp, h->U, h->gc, h->Vinv, h->y, h->S, h->b, h->Minv, h->x,
                     h->r, h->z, h->p, h->q, h->dp, h->cams_new, h->pts_new, h->partial,
-                    h->clab, h->csize, h->lin_cams, h->prev_einv};
+                    h->clab, h->csize, h->lin_cams, h->prev_einv, h->gp_t, h->gp_f, h->gp_beta, h->gp_a,
+                    h->gp_r, h->gp_hss, h->gp_gs, h->gp_ds, h->gp_hx, h->gp_hc, h->gp_gx, h->gp_gc,
+                    h->gp_scales_new, h->gp_sfree};
     for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) free(ptrs[i]);
     free(h);
 }
@@ -748,7 +765,7 @@ void ora_schur(ora_t* h, double f) {
             for (int a = 0; a < D; ++a)
                 for (int bb = 0; bb < D; ++bb) {
                     double u = Ui[a * D + bb];
-                    if (a == bb) u = clampd(u, h->cmin, h->cmax) * f;
+                    if (a == bb && !h->u_predamped) u = clampd(u, h->cmin, h->cmax) * f;
                     Srow[a * D + bb] += u;
                 }
             memcpy(h->b + (size_t)i * D, bi, sizeof(double) * D);
@@ -836,7 +853,7 @@ static int ora_coarse_setup(ora_t* h, const double* Lfac, double* Zt, double* Ei
     const size_t DD = (size_t)D * D;
     for (int i = 0; i < C; ++i) {
         double G[MAXD * (MAXD + 1)];
-        coarse_basis(D, h->lin_cams + (size_t)i * h->stride, h->csize[h->clab[i]] < 2, G);
+        coarse_basis(D, h->lin_cams + (size_t)i * h->stride, h->csize[h->clab[i]] < 2, G, h->kind);
         const double* L = Lfac + (size_t)i * DD;
         double* Z = Zt + (size_t)i * D * MC;
         for (int a = 0; a < D; ++a)
@@ -1188,6 +1205,282 @@ int ora_step(ora_t* h, double* cams, double* pts, double* loss_out) {
     *loss_out = h->loss;
     return 0;
 }
+
+
+/* ------------------------------------------------------------------------------------------ */
+/* global positioning (TorchGP.Optimize, global_positioning.py:45-206)                         */
+/* ------------------------------------------------------------------------------------------ */
+/* Residual per observation o (pairwise_cost, cost_function.py:22-29):
+ *     r_o = f_o (t_o - s_o (X_p - c_c))          (3-D; f_o = 1 calibrated camera, 0.5 otherwise)
+ * Parameters: camera positions c [C,3], points X [P,3], per-observation scales s [N] (those with a valid depth are
+ * fixed: TorchGP's scale_indices / depth_only).  LM as bundle adjustment (Huber + Triggs, diag clamp, cumulative
+ * damping, TrustRegion, rejects), additive updates.  Linear solve: with the weighted Jacobian rows
+ *     J_c = beta I,  J_X = -beta I,  J_s = a = -f (X - c) sqrt(w),   beta = s f sqrt(w)
+ * the scale blocks (1x1) are eliminated first (h_ss = clamp(a.a) * damping), which leaves, per observation, the
+ * camera-point block W_o = -beta^2 (I - a a^T / h_ss) and rank-1 corrections of the damped camera and point diagonals;
+ * the points are then eliminated exactly as in bundle adjustment (S = U' - sum W V^-1 W^T, D = 3), the reduced
+ * camera system is solved by the same PCG, and the back-substitution also returns the scale steps. */
+ora_t* ora_gp_create(int C, int P, int N, const double* trans, const int* cam, const int* pt, const double* fcam,
+                     const int* sfree, const double* dopt, const int* iopt) {
+    ora_t* h = ora_create(ORA_GP, C, P, N, NULL, cam, pt, NULL, dopt, iopt);
+    if (!h) return NULL;
+    h->u_predamped = 1;
+    h->gp_t = (double*)malloc(sizeof(double) * 3 * (size_t)N); memcpy(h->gp_t, trans, sizeof(double) * 3 * (size_t)N);
+    h->gp_f = (double*)malloc(sizeof(double) * (size_t)N);
+    for (int o = 0; o < N; ++o) h->gp_f[o] = fcam[cam[o]];
+    h->gp_sfree = (int*)malloc(sizeof(int) * (size_t)N); memcpy(h->gp_sfree, sfree, sizeof(int) * (size_t)N);
+    h->gp_beta = (double*)malloc(sizeof(double) * (size_t)N);
+    h->gp_a = (double*)malloc(sizeof(double) * 3 * (size_t)N);
+    h->gp_r = (double*)malloc(sizeof(double) * 3 * (size_t)N);
+    h->gp_hss = (double*)malloc(sizeof(double) * (size_t)N);
+    h->gp_gs = (double*)malloc(sizeof(double) * (size_t)N);
+    h->gp_ds = (double*)malloc(sizeof(double) * (size_t)N);
+    h->gp_hx = (double*)malloc(sizeof(double) * (size_t)P);
+    h->gp_hc = (double*)malloc(sizeof(double) * (size_t)C);
+    h->gp_gx = (double*)malloc(sizeof(double) * 3 * (size_t)P);
+    h->gp_gc = (double*)malloc(sizeof(double) * 3 * (size_t)C);
+    h->gp_scales_new = (double*)malloc(sizeof(double) * (size_t)N);
+    return h;
+}
+
+static void gp_residual(const ora_t* h, int o, const double* cams, const double* pts, const double* scales, double r[3],
+                        double e[3]) {
+    const double* c = cams + 3 * (size_t)h->cam[o];
+    const double* X = pts + 3 * (size_t)h->pt[o];
+    const double* t = h->gp_t + 3 * (size_t)o;
+    const double f = h->gp_f[o], s = scales[o];
+    for (int k = 0; k < 3; ++k) {
+        e[k] = X[k] - c[k];
+        r[k] = f * (t[k] - s * e[k]);
+    }
+}
+
+double ora_gp_cost(ora_t* h, const double* cams, const double* pts, const double* scales, double* sq_out) {
+    double* e2 = h->partial;
+    double* q2 = h->partial + h->N;
+    const double delta = h->delta;
+    #pragma omp parallel for schedule(static)
+    for (int o = 0; o < h->N; ++o) {
+        double r[3], e[3];
+        gp_residual(h, o, cams, pts, scales, r, e);
+        const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        e2[o] = sqrt(s) < delta ? s : 2.0 * delta * sqrt(s) - delta * delta;
+        q2[o] = s;
+    }
+    double loss = det_sum(e2, h->N);
+    if (sq_out) *sq_out = det_sum(q2, h->N);
+    return loss;
+}
+
+void ora_gp_linearize(ora_t* h, const double* cams, const double* pts, const double* scales) {
+    h->fresh_lin = 1;
+    if (!h->lin_cams) h->lin_cams = (double*)malloc(sizeof(double) * (size_t)h->C * 3);
+    memcpy(h->lin_cams, cams, sizeof(double) * (size_t)h->C * 3);
+    const double delta = h->delta;
+    #pragma omp parallel for schedule(static)
+    for (int o = 0; o < h->N; ++o) {
+        double r[3], e[3];
+        gp_residual(h, o, cams, pts, scales, r, e);
+        const double s2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2];
+        const double wgt = sqrt(s2) < delta ? 1.0 : delta / sqrt(s2);
+        const double sw = sqrt(wgt);
+        const double f = h->gp_f[o];
+        h->gp_beta[o] = scales[o] * f * sw;
+        for (int k = 0; k < 3; ++k) {
+            h->gp_r[3 * (size_t)o + k] = sw * r[k];
+            h->gp_a[3 * (size_t)o + k] = h->gp_sfree[o] ? -f * e[k] * sw : 0.0;
+        }
+    }
+    #pragma omp parallel for schedule(static)
+    for (int p = 0; p < h->P; ++p) {
+        double hx = 0, g[3] = {0, 0, 0};
+        for (int o = h->pt_ptr[p]; o < h->pt_ptr[p + 1]; ++o) {
+            const double b = h->gp_beta[o];
+            hx += b * b;
+            for (int k = 0; k < 3; ++k) g[k] += b * h->gp_r[3 * (size_t)o + k];
+        }
+        h->gp_hx[p] = hx;
+        for (int k = 0; k < 3; ++k) h->gp_gx[3 * (size_t)p + k] = g[k];
+    }
+    #pragma omp parallel for schedule(static)
+    for (int c = 0; c < h->C; ++c) {
+        double hc = 0, g[3] = {0, 0, 0};
+        for (int e = h->cam_ptr[c]; e < h->cam_ptr[c + 1]; ++e) {
+            const int o = h->cam_obs[e];
+            const double b = h->gp_beta[o];
+            hc += b * b;
+            for (int k = 0; k < 3; ++k) g[k] -= b * h->gp_r[3 * (size_t)o + k];
+        }
+        h->gp_hc[c] = hc;
+        for (int k = 0; k < 3; ++k) h->gp_gc[3 * (size_t)c + k] = g[k];
+    }
+}
+
+/* Damped system after the scale elimination: W_o, V_p (packed sym), g'_x (into gp), U'_c (into U), g'_c (into gc). */
+static void gp_prep(ora_t* h, double f) {
+    #pragma omp parallel for schedule(static)
+    for (int o = 0; o < h->N; ++o) {
+        const double* a = h->gp_a + 3 * (size_t)o;
+        const double* r = h->gp_r + 3 * (size_t)o;
+        const double b2 = h->gp_beta[o] * h->gp_beta[o];
+        double hss = 0.0, gs = 0.0;
+        if (h->gp_sfree[o]) {
+            hss = clampd(a[0] * a[0] + a[1] * a[1] + a[2] * a[2], h->cmin, h->cmax) * f;
+            gs = -(a[0] * r[0] + a[1] * r[1] + a[2] * r[2]);
+        }
+        h->gp_hss[o] = hss;
+        h->gp_gs[o] = gs;
+        double* Wo = h->W + (size_t)o * 9;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                const double q = (i == j ? 1.0 : 0.0) - (hss > 0.0 ? a[i] * a[j] / hss : 0.0);
+                Wo[i * 3 + j] = -b2 * q;
+            }
+    }
+    #pragma omp parallel for schedule(static)
+    for (int p = 0; p < h->P; ++p) {
+        const double d = clampd(h->gp_hx[p], h->cmin, h->cmax) * f;
+        double Vs[6] = {d, 0, 0, d, 0, d};
+        double g[3];
+        for (int k = 0; k < 3; ++k) g[k] = h->gp_gx[3 * (size_t)p + k];
+        for (int o = h->pt_ptr[p]; o < h->pt_ptr[p + 1]; ++o) {
+            const double hss = h->gp_hss[o];
+            if (!(hss > 0.0)) continue;
+            const double* a = h->gp_a + 3 * (size_t)o;
+            const double b = h->gp_beta[o], c2 = b * b / hss, cg = b * h->gp_gs[o] / hss;
+            Vs[0] -= c2 * a[0] * a[0]; Vs[1] -= c2 * a[0] * a[1]; Vs[2] -= c2 * a[0] * a[2];
+            Vs[3] -= c2 * a[1] * a[1]; Vs[4] -= c2 * a[1] * a[2]; Vs[5] -= c2 * a[2] * a[2];
+            for (int k = 0; k < 3; ++k) g[k] += cg * a[k];
+        }
+        memcpy(h->V + 6 * (size_t)p, Vs, sizeof(Vs));
+        for (int k = 0; k < 3; ++k) h->gp[3 * (size_t)p + k] = g[k];
+    }
+    #pragma omp parallel for schedule(static)
+    for (int c = 0; c < h->C; ++c) {
+        const double d = clampd(h->gp_hc[c], h->cmin, h->cmax) * f;
+        double Uc[9] = {d, 0, 0, 0, d, 0, 0, 0, d};
+        double g[3];
+        for (int k = 0; k < 3; ++k) g[k] = h->gp_gc[3 * (size_t)c + k];
+        for (int e = h->cam_ptr[c]; e < h->cam_ptr[c + 1]; ++e) {
+            const int o = h->cam_obs[e];
+            const double hss = h->gp_hss[o];
+            if (!(hss > 0.0)) continue;
+            const double* a = h->gp_a + 3 * (size_t)o;
+            const double b = h->gp_beta[o], c2 = b * b / hss, cg = b * h->gp_gs[o] / hss;
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) Uc[i * 3 + j] -= c2 * a[i] * a[j];
+            for (int k = 0; k < 3; ++k) g[k] -= cg * a[k];
+        }
+        memcpy(h->U + 9 * (size_t)c, Uc, sizeof(Uc));
+        memcpy(h->gc + 3 * (size_t)c, g, sizeof(g));
+    }
+}
+
+/* V^-1, y = V^-1 g'_x for the (already damped) point blocks. */
+static int gp_prep_points(ora_t* h) {
+    int bad = 0;
+    #pragma omp parallel for schedule(static) reduction(|:bad)
+    for (int p = 0; p < h->P; ++p) {
+        double full[9], inv[9];
+        sym3_full(h->V + 6 * (size_t)p, full);
+        if (spd_inverse(3, full, inv)) { bad = 1; continue; }
+        memcpy(h->Vinv + 9 * (size_t)p, inv, sizeof(inv));
+        const double* g = h->gp + 3 * (size_t)p;
+        for (int k = 0; k < 3; ++k) h->y[3 * (size_t)p + k] = inv[k * 3 + 0] * g[0] + inv[k * 3 + 1] * g[1] + inv[k * 3 + 2] * g[2];
+    }
+    return bad ? -1 : 0;
+}
+
+/* scale steps: ds_o = (g_s - beta a.(dc_c - dX_p)) / h_ss */
+static void gp_scale_steps(ora_t* h, const double* dc) {
+    #pragma omp parallel for schedule(static)
+    for (int o = 0; o < h->N; ++o) {
+        const double hss = h->gp_hss[o];
+        if (!(hss > 0.0)) { h->gp_ds[o] = 0.0; continue; }
+        const double* a = h->gp_a + 3 * (size_t)o;
+        const double* d = dc + 3 * (size_t)h->cam[o];
+        const double* dX = h->dp + 3 * (size_t)h->pt[o];
+        double s = 0.0;
+        for (int k = 0; k < 3; ++k) s += a[k] * (d[k] - dX[k]);
+        h->gp_ds[o] = (h->gp_gs[o] - h->gp_beta[o] * s) / hss;
+    }
+}
+
+int ora_gp_solve(ora_t* h, double f) {
+    gp_prep(h, f);
+    if (gp_prep_points(h)) return -1;
+    ora_schur(h, f);
+    int it = ora_pcg(h, h->x);
+    if (it < 0) return -1;
+    backsub(h, h->x);
+    gp_scale_steps(h, h->x);
+    return it;
+}
+
+static double gp_model_decrease(ora_t* h) {
+    double* e = h->partial;
+    #pragma omp parallel for schedule(static)
+    for (int o = 0; o < h->N; ++o) {
+        const double* a = h->gp_a + 3 * (size_t)o;
+        const double* r = h->gp_r + 3 * (size_t)o;
+        const double* d = h->x + 3 * (size_t)h->cam[o];
+        const double* dX = h->dp + 3 * (size_t)h->pt[o];
+        const double b = h->gp_beta[o], ds = h->gp_ds[o];
+        double acc = 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const double jd = b * (d[k] - dX[k]) + a[k] * ds;
+            acc += jd * (2.0 * r[k] + jd);
+        }
+        e[o] = acc;
+    }
+    return -det_sum(e, h->N);
+}
+
+/* One LM step of TorchGP's optimizer (LM semantics as ora_step); cams [C,3], pts [P,3], scales [N] in place. */
+int ora_gp_step(ora_t* h, double* cams, double* pts, double* scales, double* loss_out) {
+    const int C = h->C, P = h->P, N = h->N;
+    if (!h->have_loss) { h->loss = ora_gp_cost(h, cams, pts, scales, NULL); h->have_loss = 1; }
+    const double last = h->loss;
+    ora_gp_linearize(h, cams, pts, scales);
+    double f = 1.0;
+    int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
+    for (;;) {
+        f *= (1.0 + h->damping);
+        const int it = ora_gp_solve(h, f);
+        trials++;
+        if (it < 0) { failed = 1; h->loss = last; break; }
+        pcg_last = it; pcg_total += it;
+        for (size_t k = 0; k < (size_t)C * 3; ++k) h->cams_new[k] = cams[k] + h->x[k];
+        for (size_t k = 0; k < (size_t)P * 3; ++k) h->pts_new[k] = pts[k] + h->dp[k];
+        for (int o = 0; o < N; ++o) h->gp_scales_new[o] = scales[o] + h->gp_ds[o];
+        const double loss_new = ora_gp_cost(h, h->cams_new, h->pts_new, h->gp_scales_new, NULL);
+        const double denom = gp_model_decrease(h);
+        const double quality = (last - loss_new) / denom;
+        double radius = 1.0 / h->damping;
+        if (quality > h->high) { radius = h->up * radius; h->down = h->down0; }
+        else if (quality > h->low) { h->down = h->down0; }
+        else { radius = radius * h->down; h->down = h->down * h->factor; }
+        radius = clampd(radius, h->rmin, h->rmax);
+        h->damping = 1.0 / radius;
+        if (last < loss_new && rejects < h->max_rejects) {
+            rejects++;
+            h->loss = last;
+            continue;
+        }
+        memcpy(cams, h->cams_new, sizeof(double) * (size_t)C * 3);
+        memcpy(pts, h->pts_new, sizeof(double) * (size_t)P * 3);
+        memcpy(scales, h->gp_scales_new, sizeof(double) * (size_t)N);
+        h->loss = loss_new;
+        break;
+    }
+    h->stats[0] = trials; h->stats[1] = pcg_last; h->stats[2] = pcg_total; h->stats[3] = f;
+    h->stats[4] = h->damping; h->stats[5] = failed; h->stats[6] = rejects;
+    *loss_out = h->loss;
+    return 0;
+}
+
+/* scale steps of the last solve */
+void ora_gp_get_ds(const ora_t* h, double* out) { memcpy(out, h->gp_ds, sizeof(double) * (size_t)h->N); }
 
 void ora_stats(const ora_t* h, double* out) { memcpy(out, h->stats, sizeof(h->stats)); }
 double ora_damping(const ora_t* h) { return h->damping; }

@@ -46,6 +46,14 @@ def lib():
         L.ora_retract_pose.argtypes = [_dp, _dp, _dp]
         L.ora_n_intr.argtypes = [ctypes.c_int]
         L.ora_clusters.argtypes = [ctypes.c_void_p, _ip]
+        L.ora_gp_create.restype = ctypes.c_void_p
+        L.ora_gp_create.argtypes = [ctypes.c_int] * 3 + [_dp, _ip, _ip, _dp, _ip, _dp, _ip]
+        L.ora_gp_step.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp]
+        L.ora_gp_cost.restype = ctypes.c_double
+        L.ora_gp_cost.argtypes = [ctypes.c_void_p, _dp, _dp, _dp, _dp]
+        L.ora_gp_linearize.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
+        L.ora_gp_solve.argtypes = [ctypes.c_void_p, ctypes.c_double]
+        L.ora_gp_get_ds.argtypes = [ctypes.c_void_p, _dp]
         _lib = L
     return _lib
 
@@ -190,3 +198,80 @@ def solve_to_convergence(problem, max_iters=200, ftol=5e-4, window=4, **opts):
                 break
     loss, rmse = ba.cost(cams, pts)
     return cams, pts, hist, rmse
+
+
+# TorchGP LM options (global_positioning.py:157-160): TrustRegion(radius=1e3, max=1e8, up=2.0, down=0.5**4), PCG(1e-5),
+# Huber(thres_loss_function), reject=30; pypose defaults for the rest.
+# TorchGP.Optimize (global_positioning.py:158-161): TrustRegion(radius=1e3, max=1e8), PCG(tol=1e-5), reject=30;
+# Huber threshold GLOBAL_POSITIONER_OPTIONS['thres_loss_function'] = 0.1 (config/colmap.py:41-46)
+GP_DEFAULTS = dict(DEFAULTS, huber_delta=0.1, tr_radius=1e3, tr_max=1e8)
+
+
+class OracleGP:
+    """CPU restatement of TorchGP's LM (oracle/ba_oracle.c ora_gp_*) on a packed global-positioning problem:
+    rays t [N,3] (world frame), camera index / point index per observation (track-major), per-camera factor
+    (1.0 calibrated, 0.5 otherwise), per-observation scale-free flag."""
+
+    def __init__(self, trans, cam_idx, pt_idx, fcam, sfree, n_cams, n_points, **opts):
+        o = dict(GP_DEFAULTS, **opts)
+        self.C, self.P = int(n_cams), int(n_points)
+        self.t = np.ascontiguousarray(trans, np.float64)
+        self.cam = np.ascontiguousarray(cam_idx, np.int32)
+        self.pt = np.ascontiguousarray(pt_idx, np.int32)
+        self.fcam = np.ascontiguousarray(fcam, np.float64)
+        self.sfree = np.ascontiguousarray(sfree, np.int32)
+        self.N = self.t.shape[0]
+        self.D = 3
+        dopt = np.array([o['huber_delta'], o['tr_radius'], o['tr_max'], o['tr_min'], o['tr_up'], o['tr_down'],
+                         o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
+        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], 1, o['threads'], o['precond'], o['cluster_size']],
+                        np.int32)
+        self.h = lib().ora_gp_create(self.C, self.P, self.N, _d(self.t), _i(self.cam), _i(self.pt), _d(self.fcam),
+                                     _i(self.sfree), _d(dopt), _i(iopt))
+        if not self.h:
+            raise ValueError("ora_gp_create failed")
+
+    __del__ = OracleBA.__del__
+    stats = OracleBA.stats
+    clusters = OracleBA.clusters
+    nnzb = OracleBA.nnzb
+    get = OracleBA.get
+
+    def step(self, cams, pts, scales):
+        assert cams.flags.c_contiguous and pts.flags.c_contiguous and scales.flags.c_contiguous
+        loss = ctypes.c_double()
+        lib().ora_gp_step(self.h, _d(cams), _d(pts), _d(scales), ctypes.byref(loss))
+        return loss.value
+
+    def cost(self, cams, pts, scales):
+        sq = ctypes.c_double()
+        loss = lib().ora_gp_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
+                                 _d(np.ascontiguousarray(scales)), ctypes.byref(sq))
+        return loss, float(np.sqrt(sq.value / self.N))
+
+    def linearize(self, cams, pts, scales):
+        lib().ora_gp_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
+                               _d(np.ascontiguousarray(scales)))
+
+    def solve(self, f):
+        return lib().ora_gp_solve(self.h, float(f))
+
+    def ds(self):
+        out = np.zeros(self.N)
+        lib().ora_gp_get_ds(self.h, _d(out))
+        return out
+
+
+def gp_solve_to_convergence(problem, max_iters=100, ftol=5e-4, window=4, **opts):
+    """TorchGP.Optimize's loop (global_positioning.py:176-186): window 4, |improvement| < function_tolerance."""
+    gp = OracleGP(problem.trans, problem.cam_idx, problem.pt_idx, problem.fcam, problem.sfree, problem.n_cams,
+                  problem.n_points, **opts)
+    cams, pts, scales = problem.cams_init.copy(), problem.points_init.copy(), problem.scales_init.copy()
+    hist = []
+    for _ in range(max_iters):
+        hist.append(gp.step(cams, pts, scales))
+        if len(hist) >= 2 * window:
+            recent, prev = np.mean(hist[-window:]), np.mean(hist[-2 * window:-window])
+            if abs((prev - recent) / prev) < ftol:
+                break
+    return cams, pts, scales, hist
