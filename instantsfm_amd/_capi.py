@@ -1,4 +1,4 @@
-"""ctypes binding of the C ABI in include/insfm_ba.h (libinsfm_ba.so, built in-tree for gfx950).
+"""ctypes binding of the C ABI in include/insfm_ba.h and include/insfm_gp.h (libinsfm_ba.so, built in-tree for gfx950).
 
 There is no CPU fallback: if the HIP library is missing or no GPU is visible, every entry point raises.
 """
@@ -51,11 +51,13 @@ class Stats(ctypes.Structure):
                     coarse_used=self.coarse_used)
 
 
-# exported symbols (every one declared in include/insfm_ba.h)
+# exported symbols (every one declared in include/insfm_ba.h and include/insfm_gp.h)
 SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
-           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters")
+           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters",
+           "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
+           "insfm_gp_debug_get_ds")
 
 _lib = None
 
@@ -108,6 +110,19 @@ def load(path=LIB_PATH):
     L.insfm_ba_set_timing.restype = ctypes.c_int
     L.insfm_ba_debug_clusters.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
     L.insfm_ba_debug_clusters.restype = ctypes.c_int32
+    ip = ctypes.POINTER(ctypes.c_int32)
+    L.insfm_gp_default_desc.argtypes = [ctypes.POINTER(Desc)]
+    L.insfm_gp_default_desc.restype = None
+    L.insfm_gp_create.argtypes = [ctypes.POINTER(Desc), dp, ip, ip, dp, ip, vp, ctypes.POINTER(vp)]
+    L.insfm_gp_create.restype = ctypes.c_int
+    L.insfm_gp_step.argtypes = [vp, vp, vp, vp, ctypes.POINTER(Stats)]
+    L.insfm_gp_step.restype = ctypes.c_int
+    L.insfm_gp_cost.argtypes = [vp, vp, vp, vp, dp, dp]
+    L.insfm_gp_cost.restype = ctypes.c_int
+    L.insfm_gp_debug_linearize.argtypes = [vp, vp, vp, vp]
+    L.insfm_gp_debug_linearize.restype = ctypes.c_int
+    L.insfm_gp_debug_get_ds.argtypes = [vp, dp]
+    L.insfm_gp_debug_get_ds.restype = ctypes.c_int64
     _lib = L
     return L
 
@@ -115,6 +130,12 @@ def load(path=LIB_PATH):
 def default_desc():
     d = Desc()
     load().insfm_ba_default_desc(ctypes.byref(d))
+    return d
+
+
+def gp_default_desc():
+    d = Desc()
+    load().insfm_gp_default_desc(ctypes.byref(d))
     return d
 
 

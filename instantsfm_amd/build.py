@@ -7,7 +7,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "ba_kernels.hip")
-DEPS = [SRC, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), os.path.join(REPO, "include", "insfm_ba.h")]
+DEPS = [SRC, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), *sorted(glob.glob(os.path.join(REPO, "include", "*.h")))]
 OUT = os.path.join(HERE, "_lib", "libinsfm_ba.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")

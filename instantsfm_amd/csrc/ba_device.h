@@ -21,8 +21,13 @@ template <> struct Model<6> { static constexpr int NI = 10, NF = 2; };  // FULL_
 template <> struct Model<8> { static constexpr int NI = 2, NF = 1; };   // SIMPLE_RADIAL_FISHEYE [f, k]
 template <> struct Model<9> { static constexpr int NI = 3, NF = 1; };   // RADIAL_FISHEYE  [f, k1, k2]
 
-template <int M> constexpr int kD = 6 + Model<M>::NI;       // camera block dimension
-template <int M> constexpr int kStride = 7 + Model<M>::NI;  // stored camera row
+// Global positioning (TorchGP, global_positioning.py:45-206): the "camera" is its position c (3 values), no rotation
+// or intrinsics; kernels that depend on the camera parametrization specialise on this id.
+constexpr int kGP = 100;
+template <> struct Model<kGP> { static constexpr int NI = 0, NF = 0; };
+
+template <int M> constexpr int kD = M == kGP ? 3 : 6 + Model<M>::NI;       // camera block dimension
+template <int M> constexpr int kStride = M == kGP ? 3 : 7 + Model<M>::NI;  // stored camera row
 
 // atan(r)/r and d/dr2 (series near 0 for the derivative; value as the reference computes it).
 __device__ __forceinline__ void fisheye_g(double r2, double& g, double& dg) {

@@ -26,9 +26,11 @@
 #include <vector>
 
 #include "../../include/insfm_ba.h"
+#include "../../include/insfm_gp.h"
 #include "ba_device.h"
 #include "ba_common.h"
 #include "ba_twolevel.h"
+#include "ba_gp.h"
 
 using namespace insfm;
 
@@ -930,6 +932,13 @@ struct insfm_ba {
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
     bool tl_sync = false;  // INSFM_TL_SYNC=1: factorize on the main stream (debug)
     int coarse_used = 0;
+    // global positioning (kind 1, insfm_gp_*): per local observation ray / scale-free flag / source index, camera
+    // factors, the linearization records and the scale-eliminated camera blocks of the current trial
+    int kind = 0;
+    double *trans = nullptr, *fcam = nullptr, *gobs = nullptr, *Up = nullptr, *gpc = nullptr;
+    int *sfree = nullptr, *osrc = nullptr;
+    double *scl_cur = nullptr, *scl_new = nullptr, *ds = nullptr;
+    std::vector<int> osrc_host;
 };
 
 namespace {
@@ -989,6 +998,7 @@ int with_model(int m, F&& f) {
 template <typename F>
 int with_D(int D, F&& f) {
     switch (D) {
+        case 3: return f(std::integral_constant<int, 3>{});  // global positioning
         case 7: return f(std::integral_constant<int, 7>{});
         case 8: return f(std::integral_constant<int, 8>{});
         case 9: return f(std::integral_constant<int, 9>{});
@@ -1124,6 +1134,15 @@ int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
 // ---- phases --------------------------------------------------------------------------------------------------
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     h->tl_fresh = true;
+    if (h->kind == 1) {
+        if (h->Nl > 0)
+            k_gp_lin<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, h->sfree,
+                                                                       cams, pts_local, h->scl_cur, h->d.huber_delta, h->gobs);
+        k_gp_lin_cams<<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc);
+        int rc = launch_err(h, "k_gp_lin");
+        if (rc) return rc;
+        return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
+    }
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
@@ -1143,6 +1162,10 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
 // `build_stream`, which must already be ordered after the basis).
 int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
     const int C = h->C;
+    if (h->kind == 1) {
+        k_tl_basis<kGP><<<cdiv(C * 4, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl);
+        return launch_err(h, "k_tl_basis");
+    }
     return with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int MC = kD<M> + 1;
@@ -1215,7 +1238,22 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
     HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
-    if (h->Pl > 0)
+    const bool gpk = h->kind == 1;
+    // global positioning: the scale-eliminated blocks are already damped, so k_schur takes U'/g'_c as they are
+    const double* Uin = gpk ? h->Up : h->U;
+    const double* gcin = gpk ? h->gpc : h->gc;
+    const double sf = gpk ? 1.0 : f;
+    const double smin = gpk ? -1.0e308 : h->d.clamp_min, smax = gpk ? 1.0e308 : h->d.clamp_max;
+    const int sdiag = gpk ? 1 : (h->d.rank == 0);
+    if (gpk) {
+        if (h->Pl > 0)
+            k_gp_prep_points<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->gobs, f, h->d.clamp_min,
+                                                                               h->d.clamp_max, h->W, h->V, h->gp, h->Vinv,
+                                                                               h->y, h->flags);
+        k_gp_prep_cams<<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
+                                                                     h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->Up,
+                                                                     h->gpc);
+    } else if (h->Pl > 0)
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
                                                                        h->Vinv, h->y, h->flags);
     int iters = 0;
@@ -1227,13 +1265,11 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             if (h->d.deterministic)
                 k_schur<DV, 1><<<h->nwork, 64, h->schur_lds, h->stream>>>(
                     h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y,
-                    h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+                    h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
             else
                 k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
                     h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y,
-                    h->U, h->gc, f, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+                    h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
             return launch_err(h, "k_schur");
         });
         if (rc) return rc;
@@ -1303,6 +1339,16 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         dcp = h->dc;
     }
     rec(h, 3);
+    if (gpk) {
+        if (h->Pl > 0)
+            k_gp_backsub<<<h->n_gp, kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->gobs, h->W, dcp, h->Vinv, h->gp,
+                                                              pts_local, h->scl_cur, f, h->d.clamp_min, h->d.clamp_max, h->dp,
+                                                              h->pts_new, h->scl_new, h->ds, h->part_gp);
+        k_gp_update_cams<<<cdiv(3 * h->C, kThreads), kThreads, 0, h->stream>>>(3 * h->C, cams, dcp, h->cams_new);
+        int rc = launch_err(h, "k_gp_backsub/update");
+        if (rc) return rc;
+        return iters;
+    }
     int rc = with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (h->Pl > 0)
@@ -1322,7 +1368,21 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
 }
 
 // cost at (cams, pts_local) -> h->result[0..1]; with gain partials when `gains` (after a solve).
-int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gains) {
+int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gains, const double* scl = nullptr) {
+    if (h->kind == 1) {
+        if (h->Nl > 0)
+            k_gp_cost<<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, cams, pts_local, scl,
+                                                             h->d.huber_delta, h->part_cost);
+        k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
+                                               h->n_gp, nullptr, 0, h->flags, h->result);
+        int rc = launch_err(h, "k_gp_cost/k_final");
+        if (rc) return rc;
+        rc = allreduce(h, h->result, 5);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return 0;
+    }
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         if (h->Nl > 0)
@@ -1337,6 +1397,84 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+// One LM step on the parameters loaded into cams_cur / pts_cur (/ scl_cur): bae.optim.LM.step semantics (SURVEY.md
+// 3.3): cumulative damping, TrustRegion radius update, up to max_rejects rejected trials.
+int lm_step(insfm_ba* h, insfm_ba_stats* st) {
+    h->timing = st != nullptr && h->want_timing;
+    for (auto& v : h->tms) v = 0.0;
+    h->cg_launches = 0;
+    int rc;
+    if (!h->have_loss) {
+        if ((rc = run_cost(h, h->cams_cur, h->pts_cur, false, h->scl_cur))) return rc;
+        h->loss = h->host_res[0];
+        h->have_loss = true;
+    }
+    const double last = h->loss;
+    rec(h, 0);
+    if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
+    rec(h, 1);
+    double f = 1.0;
+    int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
+    for (;;) {
+        f *= (1.0 + h->damping);
+        ++trials;
+        const int it = run_solve(h, f, h->cams_cur, h->pts_cur);
+        if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
+        if (it < 0) return it;
+        rec(h, 4);
+        if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new))) return rc;  // synchronizes
+        rec(h, 5);
+        if (h->timing) {
+            (void)hipEventSynchronize(h->ev[5]);
+            if (trials == 1) acc_time(h, 0, 1, 0);
+            if (h->d.optimize_poses) {
+                acc_time(h, 6, 7, 1);
+                acc_time(h, 1, 3, 2);
+            }
+            acc_time(h, 3, 4, 3);
+            acc_time(h, 4, 5, 4);
+            rec(h, 1);  // the next trial starts here
+        }
+        if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
+        pcg_last = it;
+        pcg_total += it;
+        const double loss_new = h->host_res[0];
+        const double denom = h->host_res[2] + h->host_res[3];
+        const double quality = (last - loss_new) / denom;
+        double radius = 1.0 / h->damping;
+        if (quality > h->d.tr_high) { radius = h->d.tr_up * radius; h->down = h->d.tr_down; }
+        else if (quality > h->d.tr_low) { h->down = h->d.tr_down; }
+        else { radius = radius * h->down; h->down = h->down * h->d.tr_factor; }
+        radius = std::min(std::max(radius, h->d.tr_min), h->d.tr_max);
+        h->damping = 1.0 / radius;
+        if (last < loss_new && rejects < h->d.max_rejects) {
+            ++rejects;
+            h->loss = last;
+            continue;
+        }
+        std::swap(h->cams_cur, h->cams_new);
+        std::swap(h->pts_cur, h->pts_new);
+        std::swap(h->scl_cur, h->scl_new);
+        h->loss = loss_new;
+        break;
+    }
+    if (st) {
+        st->loss = h->loss;
+        st->loss_before = last;
+        st->damping = h->damping;
+        st->trials = trials;
+        st->rejects = rejects;
+        st->pcg_iters_last = pcg_last;
+        st->pcg_iters_total = pcg_total;
+        st->solver_failed = failed;
+        for (int k = 0; k < 8; ++k) st->time_ms[k] = h->tms[k];
+        st->cg_launches = h->cg_launches;
+        st->coarse_used = h->coarse_used;
+    }
+    h->timing = false;
     return 0;
 }
 
@@ -1387,26 +1525,41 @@ void insfm_ba_destroy(insfm_ba* h) {
 
 int64_t insfm_ba_nnzb(const insfm_ba* h) { return h ? h->nnzb : -1; }
 
-int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32_t* cam_idx, const int32_t* pt_idx,
-                    const double* pp, void* stream, insfm_ba** out) {
+}  // extern "C"
+
+namespace {
+
+// Shared creation of a BA (kind 0: obs = uv [N,2], cpar = pp [C,2]) or global-positioning (kind 1: obs = rays [N,3],
+// cpar = camera factors [C], sfree = scale-free flags [N] or NULL) handle.
+int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const int32_t* cam_idx, const int32_t* pt_idx,
+                const double* cpar, const int32_t* sfree_in, void* stream, insfm_ba** out) {
     if (!desc || !out) return INSFM_BA_EINVAL;
     *out = nullptr;
     insfm_ba* h = new insfm_ba();
     h->d = *desc;
+    h->kind = kind;
     h->stream = reinterpret_cast<hipStream_t>(stream);
     auto fail = [&](int rc, const std::string& msg) {
         if (!msg.empty()) h->err = msg;
         *out = h;  // handle returned so the caller can read the error; caller destroys it
         return rc;
     };
-    h->model = desc->cam_model;
-    h->ni = model_ni(h->model);
-    if (h->ni < 0) return fail(INSFM_BA_EINVAL, "unsupported camera model " + std::to_string(h->model));
-    h->D = 6 + h->ni;
-    h->stride = 7 + h->ni;
+    if (kind == 1) {
+        h->model = kGP;
+        h->ni = 0;
+        h->D = 3;
+        h->stride = 3;
+        h->d.optimize_poses = 1;
+    } else {
+        h->model = desc->cam_model;
+        h->ni = model_ni(h->model);
+        if (h->ni < 0) return fail(INSFM_BA_EINVAL, "unsupported camera model " + std::to_string(h->model));
+        h->D = 6 + h->ni;
+        h->stride = 7 + h->ni;
+    }
     h->C = desc->n_cams; h->P = desc->n_points; h->N = desc->n_obs;
     if (h->C <= 0 || h->P <= 0 || h->N < 0) return fail(INSFM_BA_EINVAL, "empty problem");
-    if (!obs_uv || !cam_idx || !pt_idx || !pp) return fail(INSFM_BA_EINVAL, "null input pointer");
+    if (!obs || !cam_idx || !pt_idx || !cpar) return fail(INSFM_BA_EINVAL, "null input pointer");
     if (desc->world_size < 1 || desc->rank < 0 || desc->rank >= desc->world_size) return fail(INSFM_BA_EINVAL, "bad rank");
     if (desc->world_size > 1 && !desc->allreduce) return fail(INSFM_BA_EINVAL, "world_size > 1 needs allreduce");
     if (h->C > 30000) return fail(INSFM_BA_EINVAL, "n_cams > 30000 not supported (LDS slot table)");
@@ -1546,13 +1699,34 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
 
     int rc;
-    std::vector<double> uvl((size_t)2 * Nl);
-    for (int o = 0; o < Nl; ++o) {
-        uvl[2 * (size_t)o] = obs_uv[2 * (size_t)lsrc[o]];
-        uvl[2 * (size_t)o + 1] = obs_uv[2 * (size_t)lsrc[o] + 1];
+    if (kind == 1) {
+        std::vector<double> tl((size_t)3 * Nl);
+        std::vector<int> sl(Nl);
+        for (int o = 0; o < Nl; ++o) {
+            for (int k = 0; k < 3; ++k) tl[3 * (size_t)o + k] = obs[3 * (size_t)lsrc[o] + k];
+            sl[o] = sfree_in ? (sfree_in[lsrc[o]] != 0) : 1;
+        }
+        if ((rc = upload(h, &h->trans, tl.data(), tl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->sfree, sl.data(), sl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->fcam, cpar, (size_t)C))) return fail(rc, "");
+        if ((rc = upload(h, &h->osrc, lsrc.data(), lsrc.size()))) return fail(rc, "");
+        h->osrc_host = lsrc;
+        auto dd1 = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
+        if ((rc = dd1(&h->gobs, (size_t)Nl * kGO))) return fail(rc, "");
+        if ((rc = dd1(&h->Up, (size_t)C * 9))) return fail(rc, "");
+        if ((rc = dd1(&h->gpc, (size_t)C * 3))) return fail(rc, "");
+        if ((rc = dd1(&h->scl_cur, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dd1(&h->scl_new, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dd1(&h->ds, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    } else {
+        std::vector<double> uvl((size_t)2 * Nl);
+        for (int o = 0; o < Nl; ++o) {
+            uvl[2 * (size_t)o] = obs[2 * (size_t)lsrc[o]];
+            uvl[2 * (size_t)o + 1] = obs[2 * (size_t)lsrc[o] + 1];
+        }
+        if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->pp, cpar, (size_t)2 * C))) return fail(rc, "");
     }
-    if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->pp, pp, (size_t)2 * C))) return fail(rc, "");
     if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->ptl, lptl.data(), lptl.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
@@ -1642,7 +1816,7 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
         return 0;
     });
     if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
-    if (desc->precond == 1 && desc->optimize_poses) {
+    if (desc->precond == 1 && h->d.optimize_poses) {
         // ---- two-level preconditioner: clusters, source lists of E, buffers ----
         const int MC = D + 1;
         CovisGraph g = covis_graph(C, gcptr, gcobs, gptr, cam_idx, pt_idx);
@@ -1793,6 +1967,15 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
     return INSFM_BA_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32_t* cam_idx, const int32_t* pt_idx,
+                    const double* pp, void* stream, insfm_ba** out) {
+    return create_impl(desc, 0, obs_uv, cam_idx, pt_idx, pp, nullptr, stream, out);
+}
+
 int insfm_ba_set_timing(insfm_ba* h, int32_t on) {
     if (!h) return INSFM_BA_EINVAL;
     h->want_timing = on != 0;
@@ -1823,7 +2006,7 @@ int insfm_ba_reset(insfm_ba* h) {
 }
 
 int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* loss, double* rmse) {
-    if (!h || !cams || !pts) return INSFM_BA_EINVAL;
+    if (!h || !cams || !pts || h->kind != 0) return INSFM_BA_EINVAL;
     HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
     int rc = run_cost(h, cams, pts + 3 * (size_t)h->p0, false);
     if (rc) return rc;
@@ -1833,91 +2016,21 @@ int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* lo
 }
 
 int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_stats* st) {
-    if (!h || !cams_user || !pts_user) return INSFM_BA_EINVAL;
-    const int C = h->C, ST = h->stride;
-    const size_t cam_bytes = sizeof(double) * (size_t)C * ST;
+    if (!h || !cams_user || !pts_user || h->kind != 0) return INSFM_BA_EINVAL;
+    const size_t cam_bytes = sizeof(double) * (size_t)h->C * h->stride;
     const size_t pt_bytes = sizeof(double) * (size_t)h->Pl * 3;
-    h->timing = st != nullptr && h->want_timing;
-    for (auto& v : h->tms) v = 0.0;
-    h->cg_launches = 0;
     HIPCHK(hipMemcpyAsync(h->cams_cur, cams_user, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
     if (pt_bytes) HIPCHK(hipMemcpyAsync(h->pts_cur, pts_user + 3 * (size_t)h->p0, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
-    int rc;
-    if (!h->have_loss) {
-        if ((rc = run_cost(h, h->cams_cur, h->pts_cur, false))) return rc;
-        h->loss = h->host_res[0];
-        h->have_loss = true;
-    }
-    const double last = h->loss;
-    rec(h, 0);
-    if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
-    rec(h, 1);
-    double f = 1.0;
-    int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
-    for (;;) {
-        f *= (1.0 + h->damping);
-        ++trials;
-        const int it = run_solve(h, f, h->cams_cur, h->pts_cur);
-        if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
-        if (it < 0) return it;
-        rec(h, 4);
-        if ((rc = run_cost(h, h->cams_new, h->pts_new, true))) return rc;  // synchronizes
-        rec(h, 5);
-        if (h->timing) {
-            (void)hipEventSynchronize(h->ev[5]);
-            if (trials == 1) acc_time(h, 0, 1, 0);
-            if (h->d.optimize_poses) {
-                acc_time(h, 6, 7, 1);
-                acc_time(h, 1, 3, 2);
-            }
-            acc_time(h, 3, 4, 3);
-            acc_time(h, 4, 5, 4);
-            rec(h, 1);  // the next trial starts here
-        }
-        if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
-        pcg_last = it;
-        pcg_total += it;
-        const double loss_new = h->host_res[0];
-        const double denom = h->host_res[2] + h->host_res[3];
-        const double quality = (last - loss_new) / denom;
-        double radius = 1.0 / h->damping;
-        if (quality > h->d.tr_high) { radius = h->d.tr_up * radius; h->down = h->d.tr_down; }
-        else if (quality > h->d.tr_low) { h->down = h->d.tr_down; }
-        else { radius = radius * h->down; h->down = h->down * h->d.tr_factor; }
-        radius = std::min(std::max(radius, h->d.tr_min), h->d.tr_max);
-        h->damping = 1.0 / radius;
-        if (last < loss_new && rejects < h->d.max_rejects) {
-            ++rejects;
-            h->loss = last;
-            continue;
-        }
-        std::swap(h->cams_cur, h->cams_new);
-        std::swap(h->pts_cur, h->pts_new);
-        h->loss = loss_new;
-        break;
-    }
+    int rc = lm_step(h, st);
+    if (rc) return rc;
     HIPCHK(hipMemcpyAsync(cams_user, h->cams_cur, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
     if (pt_bytes) HIPCHK(hipMemcpyAsync(pts_user + 3 * (size_t)h->p0, h->pts_cur, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
-    if (st) {
-        st->loss = h->loss;
-        st->loss_before = last;
-        st->damping = h->damping;
-        st->trials = trials;
-        st->rejects = rejects;
-        st->pcg_iters_last = pcg_last;
-        st->pcg_iters_total = pcg_total;
-        st->solver_failed = failed;
-        for (int k = 0; k < 8; ++k) st->time_ms[k] = h->tms[k];
-        st->cg_launches = h->cg_launches;
-        st->coarse_used = h->coarse_used;
-    }
-    h->timing = false;
     return INSFM_BA_OK;
 }
 
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts) {
-    if (!h || !cams || !pts) return INSFM_BA_EINVAL;
+    if (!h || !cams || !pts || h->kind != 0) return INSFM_BA_EINVAL;
     HIPCHK(hipMemcpyAsync(h->cams_cur, cams, sizeof(double) * (size_t)h->C * h->stride, hipMemcpyDeviceToDevice, h->stream));
     if (h->Pl)
         HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * (size_t)h->Pl * 3, hipMemcpyDeviceToDevice,
@@ -1963,7 +2076,8 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             else
                 k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
                     h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y, h->U, h->gc, 1.0, h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->S, h->b);
+                    h->Vinv, h->y, h->kind ? h->Up : h->U, h->kind ? h->gpc : h->gc, 1.0, h->kind ? -1e308 : h->d.clamp_min,
+                    h->kind ? 1e308 : h->d.clamp_max, h->kind ? 1 : h->d.rank == 0, h->S, h->b);
         }
         return launch_err(h, "debug_time_kernel");
     });
@@ -2018,4 +2132,76 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     return (int64_t)n;
 }
 
+// ---- global positioning (include/insfm_gp.h) -------------------------------------------------------------------
+void insfm_gp_default_desc(insfm_ba_desc* d) {
+    insfm_ba_default_desc(d);
+    d->cam_model = -1;
+    d->huber_delta = 0.1;  // GLOBAL_POSITIONER_OPTIONS['thres_loss_function'] (config/colmap.py:41-46)
+    d->tr_radius = 1e3;    // TrustRegion(radius=1e3, max=1e8, up=2.0, down=0.5**4) (global_positioning.py:158)
+    d->tr_max = 1e8;
+}
+
+int insfm_gp_create(const insfm_ba_desc* desc, const double* trans, const int32_t* cam_idx, const int32_t* pt_idx,
+                    const double* cam_factor, const int32_t* scale_free, void* stream, insfm_ba** out) {
+    return create_impl(desc, 1, trans, cam_idx, pt_idx, cam_factor, scale_free, stream, out);
+}
+
+static int gp_load(insfm_ba* h, const double* pos, const double* pts, const double* scales, double* scl_dst) {
+    HIPCHK(hipMemcpyAsync(h->cams_cur, pos, sizeof(double) * 3 * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
+    if (h->Pl)
+        HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * 3 * (size_t)h->Pl, hipMemcpyDeviceToDevice,
+                              h->stream));
+    if (h->Nl) k_gp_gather<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->osrc, scales, scl_dst);
+    return launch_err(h, "k_gp_gather");
+}
+
+int insfm_gp_step(insfm_ba* h, double* pos, double* pts, double* scales, insfm_ba_stats* st) {
+    if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
+    int rc = gp_load(h, pos, pts, scales, h->scl_cur);
+    if (rc) return rc;
+    if ((rc = lm_step(h, st))) return rc;
+    HIPCHK(hipMemcpyAsync(pos, h->cams_cur, sizeof(double) * 3 * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
+    if (h->Pl)
+        HIPCHK(hipMemcpyAsync(pts + 3 * (size_t)h->p0, h->pts_cur, sizeof(double) * 3 * (size_t)h->Pl, hipMemcpyDeviceToDevice,
+                              h->stream));
+    if (h->Nl) k_gp_scatter<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->osrc, h->scl_cur, scales);
+    if ((rc = launch_err(h, "k_gp_scatter"))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return INSFM_BA_OK;
+}
+
+int insfm_gp_cost(insfm_ba* h, const double* pos, const double* pts, const double* scales, double* loss, double* rmse) {
+    if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
+    HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
+    // scratch copies (the LM's current state is untouched: cams_new / pts_new / scl_new are trial buffers)
+    HIPCHK(hipMemcpyAsync(h->cams_new, pos, sizeof(double) * 3 * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
+    if (h->Nl) k_gp_gather<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->osrc, scales, h->scl_new);
+    int rc = launch_err(h, "k_gp_gather");
+    if (rc) return rc;
+    if ((rc = run_cost(h, h->cams_new, pts + 3 * (size_t)h->p0, false, h->scl_new))) return rc;
+    if (loss) *loss = h->host_res[0];
+    if (rmse) *rmse = h->N > 0 ? std::sqrt(h->host_res[1] / h->N) : 0.0;
+    return INSFM_BA_OK;
+}
+
+int insfm_gp_debug_linearize(insfm_ba* h, const double* pos, const double* pts, const double* scales) {
+    if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
+    int rc = gp_load(h, pos, pts, scales, h->scl_cur);
+    if (rc) return rc;
+    if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return 0;
+}
+
+int64_t insfm_gp_debug_get_ds(insfm_ba* h, double* host_out) {
+    if (!h || !host_out || h->kind != 1) return INSFM_BA_EINVAL;
+    std::vector<double> loc(h->Nl);
+    if (h->Nl) HIPCHK(hipMemcpyAsync(loc.data(), h->ds, sizeof(double) * h->Nl, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    std::memset(host_out, 0, sizeof(double) * (size_t)h->N);
+    for (int o = 0; o < h->Nl; ++o) host_out[h->osrc_host[o]] = loc[o];
+    return h->N;
+}
+
 }  // extern "C"
+

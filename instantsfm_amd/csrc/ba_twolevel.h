@@ -66,6 +66,10 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
     for (int a = 0; a < D; ++a) col[a] = 0.0;
     if (tl.alone[i]) {
         if (k < D) col[k] = 1.0;
+    } else if constexpr (M == kGP) {  // global positioning: translation (I) and scaling about the origin (c_i)
+        const double* cp = cams + (size_t)i * ST;
+        if (k < 3) col[k] = 1.0;
+        else { col[0] = cp[0]; col[1] = cp[1]; col[2] = cp[2]; }
     } else {
         const double* cp = cams + (size_t)i * ST;
         const double t0 = cp[0], t1 = cp[1], t2 = cp[2];

@@ -181,3 +181,84 @@ class BundleAdjuster:
         _capi.check(self._h, n)
         assert n == out.size, (n, out.shape)
         return out
+
+
+# TorchGP.Optimize's LM (global_positioning.py:158-161): TrustRegion(radius=1e3, max=1e8, up=2, down=1/16), PCG(1e-5),
+# Huber(GLOBAL_POSITIONER_OPTIONS['thres_loss_function'] = 0.1), reject=30.
+GP_DEFAULTS = dict(LM_DEFAULTS, tr_radius=1e3, tr_max=1e8)
+
+
+class GlobalPositioner(BundleAdjuster):
+    """One global-positioning LM problem (include/insfm_gp.h): camera positions [C,3], points [P,3] and one scale per
+    observation [N] -- the replacement for the LM TorchGP builds around PairwiseNonBatched (global_positioning.py:51-71,
+    :155-161).  ``scale_free`` [N] (or None = all free) marks the observations whose scale is optimized; the others
+    (valid depth) keep theirs (scales.optimize_indices, :57-59)."""
+
+    def __init__(self, trans, cam_idx, pt_idx, cam_factor, scale_free, n_cams, n_points, device="cuda:0",
+                 huber_delta=0.1, deterministic=False, world_size=1, rank=0, shard=None, process_group=None, **lm):
+        self.device = _require_gpu(device)
+        L = _capi.load()
+        opts = dict(GP_DEFAULTS, **lm)
+        trans = np.ascontiguousarray(trans, dtype=np.float64).reshape(-1, 3)
+        cam_idx = np.ascontiguousarray(cam_idx, dtype=np.int32).reshape(-1)
+        pt_idx = np.ascontiguousarray(pt_idx, dtype=np.int32).reshape(-1)
+        cam_factor = np.ascontiguousarray(cam_factor, dtype=np.float64).reshape(-1)
+        sf = None if scale_free is None else np.ascontiguousarray(scale_free, dtype=np.int32).reshape(-1)
+        d = _capi.gp_default_desc()
+        d.n_cams, d.n_points, d.n_obs = int(n_cams), int(n_points), int(trans.shape[0])
+        d.deterministic = int(bool(deterministic))
+        d.huber_delta = float(huber_delta)
+        for k, v in opts.items():
+            setattr(d, k, type(getattr(d, k))(v))
+        d.world_size, d.rank = int(world_size), int(rank)
+        d.shard_point_begin, d.shard_point_end = (0, -1) if shard is None else (int(shard[0]), int(shard[1]))
+        self._xbuf = None
+        self._cb = None
+        self._errors = []
+        if world_size > 1:
+            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors))
+            d.allreduce = self._cb
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        h = ctypes.c_void_p()
+        dp, ip = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
+        rc = L.insfm_gp_create(ctypes.byref(d), trans.ctypes.data_as(dp), cam_idx.ctypes.data_as(ip),
+                               pt_idx.ctypes.data_as(ip), cam_factor.ctypes.data_as(dp),
+                               None if sf is None else sf.ctypes.data_as(ip), ctypes.c_void_p(stream), ctypes.byref(h))
+        if rc != 0:
+            msg = L.insfm_ba_last_error(h).decode() if h.value else ""
+            if h.value:
+                L.insfm_ba_destroy(h)
+            raise _capi.BAError(rc, msg)
+        self._h = h
+        self.desc = d
+        self.n_cams, self.n_points, self.n_obs = d.n_cams, d.n_points, d.n_obs
+        self.D = 3
+        if world_size > 1:
+            n = L.insfm_ba_exchange_count(h)
+            self._xbuf = torch.zeros(int(n), dtype=torch.float64, device=self.device)
+            _capi.check(h, L.insfm_ba_set_exchange(h, ctypes.c_void_p(self._xbuf.data_ptr()), n))
+
+    def _args(self, positions, points, scales):
+        return (self._ptr(positions, (self.n_cams, 3)), self._ptr(points, (self.n_points, 3)),
+                self._ptr(scales, (self.n_obs,)))
+
+    def step(self, positions, points, scales):
+        """One LM step; updates ``positions`` [C,3], ``points`` [P,3], ``scales`` [N] in place.  Returns (loss, stats)."""
+        st = _capi.Stats()
+        _capi.check(self._h, _capi.load().insfm_gp_step(self._h, *self._args(positions, points, scales), ctypes.byref(st)))
+        return st.loss, st.as_dict()
+
+    def cost(self, positions, points, scales):
+        loss, rmse = ctypes.c_double(), ctypes.c_double()
+        _capi.check(self._h, _capi.load().insfm_gp_cost(self._h, *self._args(positions, points, scales), ctypes.byref(loss),
+                                                        ctypes.byref(rmse)))
+        return loss.value, rmse.value
+
+    def debug_linearize(self, positions, points, scales):
+        _capi.check(self._h, _capi.load().insfm_gp_debug_linearize(self._h, *self._args(positions, points, scales)))
+
+    def debug_ds(self):
+        out = np.zeros(self.n_obs, dtype=np.float64)
+        _capi.check(self._h, _capi.load().insfm_gp_debug_get_ds(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+        return out

@@ -1,0 +1,168 @@
+"""TorchGP -- drop-in for ``instantsfm/processors/global_positioning.py`` (reference :17-206).
+
+Same constructor, ``InitializeRandomPositions``, ``ConvertResults`` and ``Optimize(cameras, images, tracks, depths,
+GLOBAL_POSITIONER_OPTIONS, depth_only=False)``: same track / image filters (they mutate ``tracks`` and
+``images[*].is_registered`` like the reference), same packing order, stop rule and write-back.  The LM underneath is
+the MI355X HIP library (``engine.GlobalPositioner``, include/insfm_gp.h) instead of bae/pypose; the packing loop
+(reference :114-152, Python over tracks x observations) is vectorized.
+"""
+import numpy as np
+import torch
+
+from ..engine import GlobalPositioner
+
+
+class PackedGP:
+    """What TorchGP.Optimize hands the LM (reference :101-161)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
+    """Vectorized restatement of global_positioning.py:85-152.  Mutates ``tracks`` (drops short tracks) and
+    ``images[*].is_registered`` (images left without tracks) exactly like the reference."""
+    for track_id in list(tracks.keys()):                                                        # :86-89
+        if tracks[track_id].observations.shape[0] < options['min_num_view_per_track']:
+            del tracks[track_id]
+    image_used = np.zeros(len(images), dtype=bool)                                              # :91-99
+    for track in tracks.values():
+        image_used[np.unique(np.asarray(track.observations)[:, 0])] = True
+        if all(image_used):
+            break
+    for image_id, image in enumerate(images):
+        if not image_used[image_id]:
+            image.is_registered = False
+
+    registered = np.array([img.is_registered for img in images], dtype=bool)                    # :101-107
+    image_idx2id = np.nonzero(registered)[0]
+    image_id2idx = -np.ones(len(images), dtype=np.int64)
+    image_id2idx[image_idx2id] = np.arange(image_idx2id.size)
+    camera_translations = np.stack([np.asarray(images[i].world2cam, dtype=np.float64)[:3, 3]    # :108-109
+                                    for i in image_idx2id])
+    track_list = list(tracks.values())
+    points_3d = np.stack([np.asarray(t.xyz, dtype=np.float64) for t in track_list])             # :110-111
+
+    obs = [np.asarray(t.observations, dtype=np.int64).reshape(-1, 2) for t in track_list]       # :120-138
+    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+    obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
+    tid = np.repeat(np.arange(len(track_list)), counts)
+    img_id, feat_id = obs[:, 0], obs[:, 1]
+    keep = registered[img_id]
+    img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
+    if depths is not None:
+        dep = np.array([float(images[i].depths[f]) for i, f in zip(img_id.tolist(), feat_id.tolist())], dtype=np.float64)
+        if depth_only:                                                                          # :129-130
+            m = dep != 0
+            img_id, feat_id, tid, dep = img_id[m], feat_id[m], tid[m], dep[m]
+        available = dep != 0                                                                    # :131-134
+        scales = 1.0 / np.where(available, dep, 1.0)
+    else:
+        available = np.zeros(img_id.size, dtype=bool)
+        scales = np.ones(img_id.size)                                                           # :146-147
+    rot = np.stack([np.asarray(images[i].world2cam, dtype=np.float64)[:3, :3] for i in range(len(images))])
+    fu_list = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) if len(im.features_undist) else
+               np.zeros((0, 3)) for im in images]
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu_list])])
+    fu_all = np.concatenate(fu_list) if fu_list else np.zeros((0, 3))
+    fu = fu_all[foff[img_id] + feat_id]
+    translations = np.einsum('nki,nk->ni', rot[img_id], fu)                                     # :135  R^T f
+    is_calibrated = np.array([bool(cameras[images[i].cam_id].has_prior_focal_length) for i in image_idx2id])
+    # depth_only: the scales are inputs, none optimized (PairwiseNonBatchedDepthOnly, :73-83); otherwise the
+    # observations with a valid depth keep theirs (scales.optimize_indices, :57-59, :150-152)
+    scale_free = np.zeros(img_id.size, np.int32) if depth_only else (~available).astype(np.int32)
+    return PackedGP(translations=np.ascontiguousarray(translations), camera_indices=image_id2idx[img_id],
+                    point_indices=tid.astype(np.int64), is_calibrated=is_calibrated,
+                    camera_translations=np.ascontiguousarray(camera_translations),
+                    points_3d=np.ascontiguousarray(points_3d), scales=np.ascontiguousarray(scales),
+                    scale_free=scale_free, image_idx2id=image_idx2id, track_list=track_list)
+
+
+class TorchGP:
+    """global_positioning.py:17-206 with the HIP engine underneath."""
+
+    def __init__(self, visualizer=None, device='cuda:0'):
+        self.device = device
+        self.visualizer = visualizer
+        self.loss_history = []
+        self.last_stats = None
+
+    def InitializeRandomPositions(self, cameras, images, tracks, depths=None):
+        """global_positioning.py:23-39 (same draws from numpy's global RNG, in the same order)."""
+        scene_scale = 100
+        if depths is not None:
+            valid_depths = depths[depths > 0]
+            if len(valid_depths):
+                scene_scale = np.mean(valid_depths) * 4.0
+        for image in images:
+            image.world2cam[:3, 3] = scene_scale * np.random.uniform(-1, 1, 3)
+        for track in tracks.values():
+            track.xyz = scene_scale * np.random.uniform(-1, 1, 3)
+            track.is_initialized = True
+        if self.visualizer:
+            self.visualizer.add_step(cameras, images, tracks)
+
+    def ConvertResults(self, images):
+        """global_positioning.py:41-43: position c -> translation t = -R c (every image, like the reference)."""
+        for image in images:
+            image.world2cam[:3, 3] = -(image.world2cam[:3, :3] @ image.world2cam[:3, 3])
+
+    def Optimize(self, cameras, images, tracks, depths, GLOBAL_POSITIONER_OPTIONS, depth_only=False, progress=True):
+        opts = GLOBAL_POSITIONER_OPTIONS
+        if depth_only and depths is None:                                                       # :46-48
+            print("Warning: No depth maps provided, skip depth-only optimization.")
+            return
+        pk = pack_gp(cameras, images, tracks, depths, opts, depth_only)
+        C, P = pk.camera_translations.shape[0], pk.points_3d.shape[0]
+        eng = GlobalPositioner(pk.translations, pk.camera_indices, pk.point_indices,
+                               np.where(pk.is_calibrated, 1.0, 0.5), pk.scale_free, C, P, device=self.device,
+                               huber_delta=opts['thres_loss_function'], deterministic=opts.get('deterministic', False),
+                               **{k: opts[k] for k in ('pcg_max_iter', 'pcg_tol', 'precond') if k in opts})
+        dev = torch.device(self.device)
+        pos_t = torch.from_numpy(pk.camera_translations).to(dev).contiguous()
+        pts_t = torch.from_numpy(pk.points_3d).to(dev).contiguous()
+        scl_t = torch.from_numpy(pk.scales).to(dev).contiguous()
+        window_size = 4                                                                         # :172-186
+        loss_history = []
+        it = range(opts['max_num_iterations'])
+        bar = None
+        if progress:
+            try:
+                import tqdm
+                bar = tqdm.trange(opts['max_num_iterations'])
+                it = bar
+            except ImportError:
+                pass
+        for _ in it:
+            loss, stats = eng.step(pos_t, pts_t, scl_t)
+            self.last_stats = stats
+            loss_history.append(loss)
+            if len(loss_history) >= 2 * window_size:
+                avg_recent = np.mean(loss_history[-window_size:])
+                avg_previous = np.mean(loss_history[-2 * window_size:-window_size])
+                improvement = (avg_previous - avg_recent) / avg_previous
+                if abs(improvement) < opts['function_tolerance']:
+                    break
+            if bar is not None:
+                bar.set_postfix({"loss": loss})
+            if self.visualizer:
+                self._write_back(images, pk, pos_t, pts_t)
+                self.ConvertResults(images)
+                self.visualizer.add_step(cameras, images, tracks, "global_positioning")
+        if bar is not None:
+            bar.close()
+        self.loss_history = loss_history
+        self.final_loss, self.final_rmse = eng.cost(pos_t, pts_t, scl_t)
+        self.scales = scl_t.cpu().numpy()
+        self._write_back(images, pk, pos_t, pts_t)                                              # :199-206
+        self.ConvertResults(images)
+        eng.close()
+
+    @staticmethod
+    def _write_back(images, pk, pos_t, pts_t):
+        pts = pts_t.detach().cpu().numpy()
+        pos = pos_t.detach().cpu().numpy()
+        for k, track in enumerate(pk.track_list):
+            track.xyz = pts[k]
+        for idx, image_id in enumerate(pk.image_idx2id.tolist()):
+            images[image_id].world2cam[:3, 3] = pos[idx]

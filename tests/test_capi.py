@@ -1,4 +1,4 @@
-"""C-ABI library: loads without a GPU, exports every symbol include/insfm_ba.h declares, rejects bad inputs before
+"""C-ABI library: loads without a GPU, exports every symbol include/*.h declares, rejects bad inputs before
 touching the device, and the product path refuses to run without a GPU (no CPU fallback)."""
 import ctypes
 import os
@@ -13,14 +13,19 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_functions():
-    txt = open(os.path.join(REPO, "include", "insfm_ba.h")).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(insfm_ba_[a-z_]+)\s*\(", txt)) - {"insfm_ba_allreduce_fn"})
+    names = set()
+    for h in sorted(os.listdir(os.path.join(REPO, "include"))):
+        if h.endswith(".h"):
+            txt = open(os.path.join(REPO, "include", h)).read()
+            txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+            names |= set(re.findall(r"\b(insfm_(?:ba|gp)_[a-z_]+)\s*\(", txt))
+    return sorted(names - {"insfm_ba_allreduce_fn"})
 
 
 def test_header_declares_expected_api():
     fns = header_functions()
-    for name in ("insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_destroy", "insfm_ba_last_error"):
+    for name in ("insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_destroy", "insfm_ba_last_error",
+                 "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost"):
         assert name in fns
 
 
@@ -75,10 +80,44 @@ def test_create_rejects_bad_inputs_without_gpu(case):
     assert msg
 
 
+def test_gp_default_desc_is_torchgp():
+    d = _capi.gp_default_desc()
+    assert d.huber_delta == 0.1 and d.tr_radius == 1e3 and d.tr_max == 1e8 and d.tr_down == 1 / 16
+    assert d.max_rejects == 30 and abs(d.pcg_tol - 1e-5) < 1e-20
+
+
+@pytest.mark.parametrize("case", ["not_track_major", "cam_oob", "null_factor"])
+def test_gp_create_rejects_bad_inputs_without_gpu(case):
+    L = _capi.load()
+    d = _capi.gp_default_desc()
+    d.n_cams, d.n_points, d.n_obs = 2, 2, 4
+    t = np.zeros((4, 3))
+    cam = np.array([0, 1, 0, 1], np.int32)
+    pt = np.array([0, 0, 1, 1], np.int32)
+    fc = np.ones(2)
+    if case == "not_track_major":
+        pt = np.array([1, 0, 1, 0], np.int32)
+    elif case == "cam_oob":
+        cam = np.array([0, 2, 0, 1], np.int32)
+    h = ctypes.c_void_p()
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int32)
+    rc = L.insfm_gp_create(ctypes.byref(d), t.ctypes.data_as(dp), cam.ctypes.data_as(ip), pt.ctypes.data_as(ip),
+                           None if case == "null_factor" else fc.ctypes.data_as(dp), None, None, ctypes.byref(h))
+    msg = L.insfm_ba_last_error(h).decode() if h.value else ""
+    if h.value:
+        L.insfm_ba_destroy(h)
+    assert rc == _capi.INSFM_BA_EINVAL, (rc, msg)
+    assert msg
+
+
 def test_no_cpu_fallback():
     from instantsfm_amd.engine import BundleAdjuster
     with pytest.raises(RuntimeError):
         BundleAdjuster(2, np.zeros((4, 2)), [0, 1, 0, 1], [0, 0, 1, 1], np.zeros((2, 2)), 2, 2, device="cpu")
+    from instantsfm_amd.engine import GlobalPositioner
+    with pytest.raises(RuntimeError):
+        GlobalPositioner(np.zeros((4, 3)), [0, 1, 0, 1], [0, 0, 1, 1], np.ones(2), None, 2, 2, device="cpu")
 
 
 def test_product_path_does_not_import_oracle():

@@ -95,3 +95,19 @@ def test_gp_fixed_scales_stay_fixed():
     assert fixed.any() and (~fixed).any()
     np.testing.assert_array_equal(scales[fixed], p.scales_init[fixed])
     assert np.abs(scales[~fixed] - 1.0).max() > 1e-3
+
+
+def test_gp_cost_matches_reference_pairwise_cost(golden_dir):
+    """The oracle's residual is the reference's pairwise_cost (golden vectors from the reference itself)."""
+    import os
+    g = np.load(os.path.join(golden_dir, "gp_cost_golden.npz"))
+    ref = g["out"]
+    C, P = g["cams"].shape[0], g["pts"].shape[0]
+    fcam = np.where(g["calibrated"], 1.0, 0.5)
+    for delta in (0.1, 1e6):  # Huber active / inactive (then loss = sum ||r||^2)
+        gp = O.OracleGP(g["trans"], g["cam_idx"], g["pt_idx"], fcam, np.ones(len(ref), np.int32), C, P, huber_delta=delta)
+        loss, rmse = gp.cost(g["cams"], g["pts"], g["scales"])
+        s = (ref ** 2).sum(1)
+        exp = np.where(np.sqrt(s) < delta, s, 2 * delta * np.sqrt(s) - delta * delta).sum()
+        assert loss == pytest.approx(exp, rel=1e-13)
+        assert rmse == pytest.approx(np.sqrt(s.mean()), rel=1e-13)

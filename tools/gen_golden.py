@@ -10,6 +10,9 @@ records:
 * ``projection_golden.npz`` -- ``reproject_funcs[m]`` (cost_function.py:32-208) for the 9 implemented
   models, 256 random observations each (seed 0).  The only restated piece inside is
   ``bae.utils.ba.rotate_quat`` (R(q) p + t, pypose [t, q_xyzw] layout).
+* ``gp_packing_<name>.npz`` -- what ``TorchGP.Optimize`` (global_positioning.py:85-170) hands to the LM: rays,
+  indices, calibration flags, initial positions / points / scales, the fixed-scale set, the LM options, and the
+  scene mutations (dropped tracks, unregistered images), together with the scene that produced them.
 * ``packing_<name>.npz`` -- what ``TorchBA.Solve`` (bundle_adjustment.py:66-126) hands to the LM:
   ``points_2d``, ``camera_indices``, ``point_indices``, ``camera_pps`` and the model's ``pose`` /
   ``points_3d`` parameters, together with the scene that produced them.  The LM shim raises after
@@ -274,16 +277,153 @@ def gen_packing(out_dir, LM):
     print("packing_edge_points_only.npz", res["out_points_2d"].shape)
 
 
+def _gp_scene_arrays(cameras, images, tracks):
+    keys = list(tracks.keys())
+    obs = [np.asarray(tracks[k].observations, dtype=np.int64).reshape(-1, 2) for k in keys]
+    fu = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) for im in images]
+    dep = [np.asarray(im.depths, dtype=np.float64).reshape(-1) for im in images]
+    return dict(
+        cam_prior_focal=np.array([c.has_prior_focal_length for c in cameras]),
+        img_cam_id=np.array([im.cam_id for im in images]),
+        img_registered=np.array([im.is_registered for im in images]),
+        img_world2cam=np.stack([np.asarray(im.world2cam, dtype=np.float64) for im in images]),
+        img_feat_ptr=np.concatenate([[0], np.cumsum([len(f) for f in fu])]),
+        img_feats_undist=np.concatenate(fu),
+        img_depths=np.concatenate(dep),
+        track_keys=np.array(keys, dtype=np.int64),
+        track_xyz=np.stack([np.asarray(tracks[k].xyz, dtype=np.float64) for k in keys]),
+        track_obs_ptr=np.concatenate([[0], np.cumsum([len(o) for o in obs])]),
+        track_obs=np.concatenate(obs),
+    )
+
+
+def _run_gp(LM, cameras, images, tracks, depths, opts, depth_only):
+    from instantsfm.processors.global_positioning import TorchGP
+    try:
+        TorchGP(device="cpu").Optimize(cameras, images, tracks, depths, opts, depth_only=depth_only)
+    except _Captured:
+        pass
+    model, kwargs, inp = LM.last
+    scales = inp["scales"] if depth_only else model.scales
+    opt_idx = getattr(model.scales, "optimize_indices", None) if not depth_only else None
+    strat = kwargs["strategy"].kwargs
+    return dict(
+        out_translations=inp["translations"].numpy(),
+        out_camera_indices=inp["camera_indices"].numpy(),
+        out_point_indices=inp["point_indices"].numpy(),
+        out_is_calibrated=inp["is_calibrated"].numpy(),
+        out_positions=model.translations.detach().numpy(),
+        out_points_3d=model.points_3d.detach().numpy(),
+        out_scales=scales.detach().numpy().reshape(-1),
+        out_has_optimize_indices=np.array(opt_idx is not None),
+        out_optimize_indices=(opt_idx.numpy() if opt_idx is not None else np.zeros(0, np.int64)),
+        out_track_keys_after=np.array(list(tracks.keys()), dtype=np.int64),
+        out_img_registered_after=np.array([im.is_registered for im in images]),
+        out_tr=np.array([strat["radius"], strat["max"], strat["up"], strat["down"]]),
+        out_huber=np.array(kwargs["kernel"].args[0]),
+        out_pcg_tol=np.array(kwargs["solver"].tol),
+        out_reject=np.array(kwargs.get("reject", -1)),
+        out_depth_only=np.array(bool(depth_only)),
+    )
+
+
+def gen_gp_cost(out_dir):
+    """pairwise_cost (cost_function.py:23-29) on random inputs: 512 observations, mixed calibration flags."""
+    from instantsfm.utils.cost_function import pairwise_cost
+    rng = np.random.default_rng(11)
+    n, C, P = 512, 16, 100
+    cams = rng.normal(0, 10, (C, 3))
+    pts = rng.normal(0, 10, (P, 3))
+    ci = rng.integers(0, C, n)
+    pi = np.sort(rng.integers(0, P, n))
+    t = rng.normal(size=(n, 3))
+    t /= np.linalg.norm(t, axis=1, keepdims=True)
+    s = rng.uniform(0.02, 0.2, (n, 1))
+    calib = rng.uniform(size=C) < 0.6
+    out = pairwise_cost(torch.from_numpy(pts[pi]), torch.from_numpy(cams[ci]), torch.from_numpy(s), torch.from_numpy(t),
+                        torch.from_numpy(calib[ci]))
+    np.savez_compressed(os.path.join(out_dir, "gp_cost_golden.npz"), cams=cams, pts=pts, cam_idx=ci, pt_idx=pi, trans=t,
+                        scales=s.reshape(-1), calibrated=calib, out=out.numpy())
+    print("gp_cost_golden.npz", out.shape)
+
+
+def gen_gp_packing(out_dir, LM):
+    """TorchGP.Optimize packing: a small synthetic scene (no depths / some depths / depth-only) and edge cases."""
+    from instantsfm.scene.defs import Camera, CameraModelId, Image, Track
+    sys.path.insert(0, REPO)
+    from instantsfm_amd.synth import make_gp_problem
+    opts = dict(min_num_view_per_track=3, thres_loss_function=1e-1, max_num_iterations=100, function_tolerance=5e-4)
+    rng = np.random.default_rng(7)
+
+    def build(prob, with_depth, extra):
+        C = prob.n_cams
+        cams = [Camera(id=c, model_id=CameraModelId.SIMPLE_RADIAL, params=[1000.0, 500.0, 400.0, 0.0],
+                       has_prior_focal_length=bool(prob.fcam[c] == 1.0)) for c in range(C)]
+        Rs = []
+        imgs = []
+        order = np.argsort(prob.cam_idx, kind="stable")
+        counts = np.bincount(prob.cam_idx, minlength=C)
+        starts = np.concatenate([[0], np.cumsum(counts)])
+        feat_id = np.empty(prob.n_obs, np.int64)
+        feat_id[order] = np.arange(prob.n_obs) - np.repeat(starts[:-1], counts)
+        for c in range(C):
+            from scipy.spatial.transform import Rotation
+            R = Rotation.from_rotvec(rng.normal(0, 0.5, 3)).as_matrix()
+            Rs.append(R)
+            w2c = np.eye(4)
+            w2c[:3, :3] = R
+            w2c[:3, 3] = prob.cams_init[c]
+            rays_world = prob.trans[order[starts[c]:starts[c + 1]]]
+            fu = rays_world @ R.T  # features_undist = R t  so that  R^T fu = t
+            dep = np.where(rng.uniform(size=fu.shape[0]) < 0.5, rng.uniform(1, 20, fu.shape[0]), 0.0) if with_depth \
+                else np.zeros(fu.shape[0])
+            imgs.append(Image(id=c, cam_id=c, is_registered=True, world2cam=w2c, features=np.zeros((fu.shape[0], 2)),
+                              features_undist=fu, depths=dep))
+        ptr = np.concatenate([[0], np.cumsum(np.bincount(prob.pt_idx, minlength=prob.n_points))])
+        pairs = np.stack([prob.cam_idx.astype(np.int64), feat_id], 1)
+        trks = {}
+        for p in range(prob.n_points):
+            trks[3 * p + 1] = Track(id=3 * p + 1, xyz=prob.points_init[p].copy(), observations=pairs[ptr[p]:ptr[p + 1]].copy())
+        if extra:
+            # an extra image observed by nothing (-> unregistered), an unregistered image with observations, a
+            # 2-view track (-> dropped)
+            imgs.append(Image(id=C, cam_id=0, is_registered=True, world2cam=np.eye(4), features=np.zeros((2, 2)),
+                              features_undist=np.array([[0, 0, 1.0], [0, 1.0, 0]]), depths=np.array([3.0, 0.0])))
+            imgs[1].is_registered = False
+            trks[1000] = Track(id=1000, xyz=np.ones(3), observations=np.array([[0, 0], [2, 0]]))
+        return cams, imgs, trks
+
+    cases = [("gp_packing_plain", dict(seed=3), False, False, False),
+             ("gp_packing_depth", dict(seed=4), True, False, False),
+             ("gp_packing_depth_only", dict(seed=5), True, True, False),
+             ("gp_packing_edge", dict(seed=6), True, False, True)]
+    for name, kw, with_depth, depth_only, extra in cases:
+        prob = make_gp_problem(8, 40, track_len=4, window=3, init="perturbed", **kw)
+        cams, imgs, trks = build(prob, with_depth, extra)
+        res = _gp_scene_arrays(cams, imgs, trks)
+        depths = np.concatenate([np.asarray(im.depths) for im in imgs]) if with_depth else None
+        res["has_depths"] = np.array(depths is not None)
+        res.update(_run_gp(LM, cams, imgs, trks, depths, opts, depth_only))
+        np.savez_compressed(os.path.join(out_dir, name + ".npz"), **res)
+        print(name + ".npz", res["out_translations"].shape)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    ap.add_argument("--only", choices=("projection", "packing", "gp"), default=None)
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     with tempfile.TemporaryDirectory():
         LM = install_shims()
         sys.path.insert(0, REF)
-        gen_projection(args.out)
-        gen_packing(args.out, LM)
+        if args.only in (None, "projection"):
+            gen_projection(args.out)
+        if args.only in (None, "packing"):
+            gen_packing(args.out, LM)
+        if args.only in (None, "gp"):
+            gen_gp_cost(args.out)
+            gen_gp_packing(args.out, LM)
 
 
 if __name__ == "__main__":
