@@ -8,6 +8,8 @@ TrustRegion accept/reject) over the whole scene.  Inputs are resident in HBM bef
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL all-reduce of the camera system)
+    python bench.py --path gp ...   global positioning (TorchGP.Optimize's LM) on the same scene geometry
+
 
 Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) is the build's C/OpenMP restatement of the same LM
 (oracle/ba_oracle.c; the reference has no CPU BA) run to convergence on the same scene.
@@ -76,6 +78,120 @@ def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8):
                 final_rmse_px=rmse, steps=len(hist))
 
 
+def cpu_baseline_gp(prob, max_steps, min_seconds=10.0, max_runs=8):
+    from oracle import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    dt, steps, runs = 0.0, 0, 0
+    while runs < max_runs and (runs == 0 or dt < min_seconds):
+        t0 = time.perf_counter()
+        _, _, _, hist = O.gp_solve_to_convergence(prob, max_iters=max_steps, threads=threads)
+        dt += time.perf_counter() - t0
+        steps += len(hist)
+        runs += 1
+    return dict(value=steps / dt, unit="LM it/s", cores=threads, kind="port",
+                sample=f"oracle/ba_oracle.c ora_gp_* (C/OpenMP f64 restatement of TorchGP's LM), same scene, {runs} "
+                       f"runs of up to {max_steps} LM steps ({len(hist)} each), {steps} steps in {dt:.2f} s",
+                final_loss=hist[-1], steps=len(hist))
+
+
+def run_gp(args):
+    """Global positioning (TorchGP.Optimize, global_positioning.py:158-186): LM it/s on a synthetic scene with the
+    geometry of config 3 (1k cameras / 200k tracks / 2M rays), random initial positions as InitializeRandomPositions."""
+    import numpy as np
+    import torch
+    from instantsfm_amd.engine import GlobalPositioner
+    from instantsfm_amd.shard import shard_ranges
+    from instantsfm_amd.synth import make_gp_problem
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    prob = make_gp_problem(1000, 200000, track_len=10, seed=args.seed, init="random")
+    shards = shard_ranges(prob.pt_idx, prob.n_points, world)
+    eng = GlobalPositioner(prob.trans, prob.cam_idx, prob.pt_idx, prob.fcam, prob.sfree, prob.n_cams, prob.n_points,
+                           device=dev, deterministic=args.deterministic, world_size=world, rank=rank, shard=shards[rank],
+                           precond=args.precond)
+    init = [torch.from_numpy(a).to(dev) for a in (prob.cams_init, prob.points_init, prob.scales_init)]
+    par = [a.clone() for a in init]
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.step(*par)
+    eng.reset()
+    for a, b in zip(par, init):
+        a.copy_(b)
+    barrier()
+    t0 = time.perf_counter()
+    stats, losses = [], []
+    for _ in range(args.steps):
+        loss, st = eng.step(*par)
+        losses.append(loss)
+        stats.append(st)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    final_loss, rmse = eng.cost(*par)
+    tl = args.precond == 1
+    us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
+    us_schur = eng.debug_time_kernel(1, 5)
+    C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, 3
+    Pl = shards[rank][1] - shards[rank][0]
+    Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
+    nnzb = eng.nnzb()
+    trials = sum(s["trials"] for s in stats)
+    cg_launches = sum(s["cg_launches"] for s in stats)
+    kcg = "k_tl_spmv" if tl else "k_cg_iter"
+    kern = {kcg: (us_cg * cg_launches, cg_launches, us_cg, algorithmic_bytes(kcg, C, Pl, Nl, D, nnzb)),
+            "k_schur": (us_schur * trials, trials, us_schur, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb))}
+    name = max(kern, key=lambda k: kern[k][0])
+    _, launches, avg_us, nbytes = kern[name]
+    achieved = nbytes / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0
+    out = {
+        "metric": "LM-GP iterations/sec (global positioning, TorchGP.Optimize)",
+        "value": round(args.steps / dt, 4), "unit": "LM it/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (instantsfm_amd/synth.py make_gp_problem, random initial positions)",
+        "config": {"workload": f"global positioning: {C} cameras / {P} tracks / {N} rays (config-3 geometry), "
+                               f"LM steps of the full scene from random initial positions",
+                   "cams": C, "points": P, "obs": N, "camera_block_dim": D, "schur_blocks": nnzb,
+                   "parallelism": f"track-shard x{world}" if world > 1 else "single GPU"},
+        "final_loss": final_loss, "final_rmse": rmse, "loss_history": [round(x, 6) for x in losses],
+        "pcg_iters": [s["pcg_iters"] for s in stats], "trials": trials,
+        "kernel_us": {kcg: round(us_cg, 3), "k_schur": round(us_schur, 2)},
+        "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(nbytes),
+                     "launches_per_run": int(launches)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline_gp(prob, args.cpu_max_steps)
+        out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+        out["cpu_final_loss"] = cb["final_loss"]
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,7 +203,10 @@ def main():
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
+    ap.add_argument("--path", choices=("ba", "gp"), default="ba")
     args = ap.parse_args()
+    if args.path == "gp":
+        return run_gp(args)
 
     import numpy as np
     import torch

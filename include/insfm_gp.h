@@ -47,7 +47,8 @@ int insfm_gp_cost(insfm_ba* h, const double* positions, const double* points, co
 
 /* ---- introspection used by the parity tests ---- */
 /* Linearize at DEVICE parameters; then insfm_ba_debug_solve(h, f) solves the damped system and
- * insfm_ba_debug_get gives 0 W[N,3,3] (scale-eliminated) 1 V[P,6] (damped) 2 g'_p 5 S 6 b 7 dc[C,3] 8 dp[P,3]. */
+ * insfm_ba_debug_get gives 0 W as [N,4] records {u, beta^2} (W_o = -beta^2 (I - u u^T), scale-eliminated) 1 V[P,6]
+ * (damped) 2 g'_p 5 S 6 b 7 dc[C,3] 8 dp[P,3]. */
 int insfm_gp_debug_linearize(insfm_ba* h, const double* positions, const double* points, const double* scales);
 /* Scale steps of the last solve in the caller's observation order (HOST out, [N]); returns N. */
 int64_t insfm_gp_debug_get_ds(insfm_ba* h, double* host_out);

@@ -257,7 +257,23 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 __host__ __device__ constexpr int schur_bs(int D) { return D * D + ((D * D) % 16 == 0 ? 8 : 0); }
 __host__ __device__ constexpr int schur_ws(int D) { return D * 4 + 1; }
 
-template <int D, int WAVES>
+// Column cb of W_o: the BA stores W [o][3][D]; global positioning (GPW) stores the 32-byte record {u, beta^2} of
+// W_o = -beta^2 (I - u u^T) (u = a / sqrt(h_ss), 0 for a fixed scale; symmetric, D = 3) written by k_gp_prep_points.
+template <int D, bool GPW>
+__device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, int cb, double& w0, double& w1, double& w2) {
+    if constexpr (GPW) {
+        const double4 r = reinterpret_cast<const double4*>(W)[o];
+        const double uc = cb == 0 ? r.x : (cb == 1 ? r.y : r.z);
+        w0 = -r.w * ((cb == 0 ? 1.0 : 0.0) - r.x * uc);
+        w1 = -r.w * ((cb == 1 ? 1.0 : 0.0) - r.y * uc);
+        w2 = -r.w * ((cb == 2 ? 1.0 : 0.0) - r.z * uc);
+    } else {
+        const double* wo = W + (size_t)o * D * 3 + cb;
+        w0 = wo[0]; w1 = wo[D]; w2 = wo[2 * D];
+    }
+}
+
+template <int D, int WAVES, bool GPW = false>
 __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
@@ -314,8 +330,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
             const int p = dcur.y;
             const double* vi = Vinv + 6 * (size_t)p;
             const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
-            const double* wo = W + (size_t)o * D * 3 + cb;
-            const double w0 = wo[0], w1 = wo[D], w2 = wo[2 * D];
+            double w0, w1, w2;
+            load_wcol<D, GPW>(W, o, cb, w0, w1, w2);
             my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
             my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
             my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
@@ -351,8 +367,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                 cj[u] = -1;
                 if (k0 + u < n) {
                     const int q = qs + k0 + u;
-                    const double* wq = W + (size_t)q * D * 3 + cb;
-                    x[u][0] = wq[0]; x[u][1] = wq[D]; x[u][2] = wq[2 * D];
+                    load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
                     cj[u] = cam[q];
                 }
             }
@@ -903,6 +918,7 @@ struct insfm_ba {
     double *cams_cur = nullptr, *cams_new = nullptr, *pts_cur = nullptr, *pts_new = nullptr;
     double *part_cost = nullptr, *part_gp = nullptr, *part_gc = nullptr;
     int n_cost = 0, n_gp = 0, n_gc = 0;
+    int n_gp_grp = 0;  // global positioning: k_gp_backsub blocks (kGPG lanes per track)
     double* result = nullptr;
     int* flags = nullptr;
     double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
@@ -935,7 +951,7 @@ struct insfm_ba {
     // global positioning (kind 1, insfm_gp_*): per local observation ray / scale-free flag / source index, camera
     // factors, the linearization records and the scale-eliminated camera blocks of the current trial
     int kind = 0;
-    double *trans = nullptr, *fcam = nullptr, *gobs = nullptr, *Up = nullptr, *gpc = nullptr;
+    double *trans = nullptr, *fcam = nullptr, *gobs = nullptr, *Up = nullptr, *gpc = nullptr, *VY = nullptr;
     int *sfree = nullptr, *osrc = nullptr;
     double *scl_cur = nullptr, *scl_new = nullptr, *ds = nullptr;
     std::vector<int> osrc_host;
@@ -1233,6 +1249,35 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
     k_tl_spmv<D><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
 }
 
+// k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
+int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, double smin, double smax, int sdiag) {
+    const bool det = h->d.deterministic != 0;
+    const int nt = det ? 64 : kSchurWaves * 64;
+    if (h->kind == 1) {
+        if (det)
+            k_schur<3, 1, true><<<h->nwork, nt, h->schur_lds, h->stream>>>(
+                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
+                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+        else
+            k_schur_gp<kSchurWaves, kGPSG><<<h->nwork, nt, h->schur_lds, h->stream>>>(
+                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->cam, h->W, h->VY, Uin, gcin, h->S, h->b,
+                h->probe);
+        return launch_err(h, "k_schur");
+    }
+    return with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        if (det)
+            k_schur<DV, 1><<<h->nwork, nt, h->schur_lds, h->stream>>>(
+                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
+                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+        else
+            k_schur<DV, kSchurWaves><<<h->nwork, nt, h->schur_lds, h->stream>>>(
+                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
+                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+        return launch_err(h, "k_schur");
+    });
+}
+
 // Build S/b for factor f, solve, back-substitute and form the trial parameters.  Returns PCG iterations (>= 0),
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
@@ -1247,9 +1292,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     const int sdiag = gpk ? 1 : (h->d.rank == 0);
     if (gpk) {
         if (h->Pl > 0)
-            k_gp_prep_points<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->gobs, f, h->d.clamp_min,
+            k_gp_prep_points<kGPG><<<cdiv((long long)h->Pl * kGPG, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->gobs, f, h->d.clamp_min,
                                                                                h->d.clamp_max, h->W, h->V, h->gp, h->Vinv,
-                                                                               h->y, h->flags);
+                                                                               h->y, h->VY, h->flags);
         k_gp_prep_cams<<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
                                                                      h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->Up,
                                                                      h->gpc);
@@ -1260,18 +1305,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
         rec(h, 6);
-        int rc = with_D(D, [&](auto dc_) -> int {
-            constexpr int DV = decltype(dc_)::value;
-            if (h->d.deterministic)
-                k_schur<DV, 1><<<h->nwork, 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
-            else
-                k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
-            return launch_err(h, "k_schur");
-        });
+        int rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
         if (rc) return rc;
         rec(h, 7);
         rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
@@ -1341,7 +1375,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     rec(h, 3);
     if (gpk) {
         if (h->Pl > 0)
-            k_gp_backsub<<<h->n_gp, kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->gobs, h->W, dcp, h->Vinv, h->gp,
+            k_gp_backsub<kGPG><<<h->n_gp_grp, kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->gobs, dcp, h->Vinv, h->gp,
                                                               pts_local, h->scl_cur, f, h->d.clamp_min, h->d.clamp_max, h->dp,
                                                               h->pts_new, h->scl_new, h->ds, h->part_gp);
         k_gp_update_cams<<<cdiv(3 * h->C, kThreads), kThreads, 0, h->stream>>>(3 * h->C, cams, dcp, h->cams_new);
@@ -1714,6 +1748,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         auto dd1 = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
         if ((rc = dd1(&h->gobs, (size_t)Nl * kGO))) return fail(rc, "");
         if ((rc = dd1(&h->Up, (size_t)C * 9))) return fail(rc, "");
+        if ((rc = dd1(&h->VY, (size_t)std::max(Pl, 1) * kVY))) return fail(rc, "");
         if ((rc = dd1(&h->gpc, (size_t)C * 3))) return fail(rc, "");
         if ((rc = dd1(&h->scl_cur, (size_t)std::max(Nl, 1)))) return fail(rc, "");
         if ((rc = dd1(&h->scl_new, (size_t)std::max(Nl, 1)))) return fail(rc, "");
@@ -1786,6 +1821,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = dd(&h->pts_new, (size_t)std::max(Pl, 1) * 3))) return fail(rc, "");
     h->n_cost = std::max(1, cdiv(Nl, kThreads));
     h->n_gp = std::max(1, cdiv(Pl, kThreads));
+    h->n_gp_grp = std::max(1, cdiv((long long)Pl * kGPG, kThreads));
+    if (kind == 1) h->n_gp = h->n_gp_grp;  // the gain partials of k_gp_backsub
     h->n_gc = std::max(1, cdiv(C, kThreads));
     if ((rc = dd(&h->part_cost, 2 * (size_t)h->n_cost))) return fail(rc, "");
     if ((rc = dd(&h->part_gp, (size_t)h->n_gp))) return fail(rc, "");
@@ -1813,6 +1850,14 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)h->schur_lds);
+        if constexpr (DV == 3) {
+            (void)hipFuncSetAttribute((const void*)k_schur<3, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->schur_lds);
+            (void)hipFuncSetAttribute((const void*)k_schur<3, kSchurWaves, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->schur_lds);
+            (void)hipFuncSetAttribute((const void*)k_schur_gp<kSchurWaves, kGPSG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->schur_lds);
+        }
         return 0;
     });
     if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
@@ -2073,11 +2118,15 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                 h->Lf, h->cg, 0);
-            else
-                k_schur<DV, kSchurWaves><<<h->nwork, kSchurWaves * 64, h->schur_lds, h->stream>>>(
-                    h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                    h->Vinv, h->y, h->kind ? h->Up : h->U, h->kind ? h->gpc : h->gc, 1.0, h->kind ? -1e308 : h->d.clamp_min,
-                    h->kind ? 1e308 : h->d.clamp_max, h->kind ? 1 : h->d.rank == 0, h->S, h->b);
+            else {
+                const int det = h->d.deterministic;
+                h->d.deterministic = 0;
+                const int rc2 = launch_schur(h, h->kind ? h->Up : h->U, h->kind ? h->gpc : h->gc, 1.0,
+                                             h->kind ? -1e308 : h->d.clamp_min, h->kind ? 1e308 : h->d.clamp_max,
+                                             h->kind ? 1 : h->d.rank == 0);
+                h->d.deterministic = det;
+                if (rc2) return rc2;
+            }
         }
         return launch_err(h, "debug_time_kernel");
     });

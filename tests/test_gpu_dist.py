@@ -22,7 +22,7 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"]])
+@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"], ["--gp", "--steps", "6"]])
 def test_two_ranks_match_single_gpu(extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "tools", "dist_check.py"), "--backend", "gloo",
@@ -36,3 +36,5 @@ def test_two_ranks_match_single_gpu(extra):
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
     assert out["cams_equal_across_ranks"], out
     assert abs(out["rmse"] - out["ref_rmse"]) < 1e-6, out
+    if "scales_rel" in out:
+        assert out["scales_rel"] < 1e-7, out

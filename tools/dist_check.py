@@ -20,9 +20,56 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from instantsfm_amd.engine import BundleAdjuster  # noqa: E402
+from instantsfm_amd.engine import BundleAdjuster, GlobalPositioner  # noqa: E402
 from instantsfm_amd.shard import shard_ranges  # noqa: E402
-from instantsfm_amd.synth import make_config, make_problem  # noqa: E402
+from instantsfm_amd.synth import make_config, make_gp_problem, make_problem  # noqa: E402
+
+
+def allsum(t, backend):
+    if backend == "gloo" and t.is_cuda:
+        host = t.cpu()
+        dist.all_reduce(host)
+        return host
+    dist.all_reduce(t)
+    return t.cpu()
+
+
+def rel(a, b):
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def run_gp(args, rank, world, dev):
+    """Global positioning: the same check for insfm_gp (points and per-observation scales are rank-local)."""
+    prob = make_gp_problem(24, 900, seed=9, init="random", depth_frac=0.2)
+    shards = shard_ranges(prob.pt_idx, prob.n_points, world)
+    mk = lambda **kw: GlobalPositioner(prob.trans, prob.cam_idx, prob.pt_idx, prob.fcam, prob.sfree, prob.n_cams,  # noqa: E731
+                                       prob.n_points, device=dev, deterministic=True, **kw)
+    eng = mk(world_size=world, rank=rank, shard=shards[rank])
+    par = [torch.from_numpy(a.copy()).to(dev) for a in (prob.cams_init, prob.points_init, prob.scales_init)]
+    losses = [eng.step(*par)[0] for _ in range(args.steps)]
+    rmse = eng.cost(*par)[1]  # collective (the cost partials are all-reduced): every rank calls it
+    p0, p1 = shards[rank]
+    pm = torch.zeros_like(par[1])
+    pm[p0:p1] = 1.0
+    om = torch.from_numpy(((prob.pt_idx >= p0) & (prob.pt_idx < p1)).astype(np.float64)).to(dev)
+    pts = allsum((par[1] * pm).contiguous(), args.backend)
+    scl = allsum((par[2] * om).contiguous(), args.backend)
+    cams_all = [torch.zeros_like(par[0]).cpu() for _ in range(world)]
+    if args.backend == "gloo":
+        dist.all_gather(cams_all, par[0].cpu())
+    if rank == 0:
+        ref = mk()
+        rpar = [torch.from_numpy(a.copy()).to(dev) for a in (prob.cams_init, prob.points_init, prob.scales_init)]
+        ref_losses = [ref.step(*rpar)[0] for _ in range(args.steps)]
+        out = dict(world=world, backend=args.backend, path="gp",
+                   loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
+                   cams_rel=rel(par[0].cpu().numpy(), rpar[0].cpu().numpy()),
+                   points_rel=rel(pts.numpy(), rpar[1].cpu().numpy()), scales_rel=rel(scl.numpy(), rpar[2].cpu().numpy()),
+                   rmse=rmse, ref_rmse=ref.cost(*rpar)[1],
+                   cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all))
+        print(json.dumps(out), flush=True)
+    dist.barrier()
+    eng.close()
 
 
 def main():
@@ -32,12 +79,17 @@ def main():
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0")
+    ap.add_argument("--gp", action="store_true", help="global positioning (insfm_gp) instead of BA")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
     dist.init_process_group(args.backend)
+    if args.gp:
+        run_gp(args, rank, world, dev)
+        dist.destroy_process_group()
+        return
     prob = make_problem(24, 900, seed=9) if args.small else make_config(args.config)
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
@@ -70,9 +122,6 @@ def main():
         ref_losses = [ref.step(rc, rp)[0] for _ in range(args.steps)]
         _, ref_rmse = ref.cost(rc, rp)
         rcn, rpn = rc.cpu().numpy(), rp.cpu().numpy()
-
-        def rel(a, b):
-            return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
         out = dict(world=world, backend=args.backend, shards=shards,
                    loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
                    cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
