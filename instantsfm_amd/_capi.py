@@ -1,4 +1,5 @@
-"""ctypes binding of the C ABI in include/insfm_ba.h and include/insfm_gp.h (libinsfm_ba.so, built in-tree for gfx950).
+"""ctypes binding of the C ABI in include/insfm_ba.h, insfm_gp.h and insfm_passes.h (libinsfm_ba.so, built in-tree for
+gfx950).
 
 There is no CPU fallback: if the HIP library is missing or no GPU is visible, every entry point raises.
 """
@@ -57,7 +58,8 @@ SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_b
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
            "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters",
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
-           "insfm_gp_debug_get_ds")
+           "insfm_gp_debug_get_ds",
+           "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle")
 
 _lib = None
 
@@ -123,6 +125,13 @@ def load(path=LIB_PATH):
     L.insfm_gp_debug_linearize.restype = ctypes.c_int
     L.insfm_gp_debug_get_ds.argtypes = [vp, dp]
     L.insfm_gp_debug_get_ds.restype = ctypes.c_int64
+    i64, f64, i32 = ctypes.c_int64, ctypes.c_double, ctypes.c_int32
+    L.insfm_undistort.argtypes = [i64, vp, i32, vp, vp, vp, vp, vp]
+    L.insfm_filter_reproj_normalized.argtypes = [i64, vp, vp, vp, vp, vp, vp, f64, vp, vp, vp]
+    L.insfm_filter_angle.argtypes = [i64, vp, vp, vp, vp, vp, vp, f64, vp, vp]
+    L.insfm_filter_tri_angle.argtypes = [i64, vp, vp, vp, vp, f64, vp, vp]
+    for fn in ("insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle"):
+        getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L
 

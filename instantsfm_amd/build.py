@@ -6,8 +6,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SRC = os.path.join(HERE, "csrc", "ba_kernels.hip")
-DEPS = [SRC, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), *sorted(glob.glob(os.path.join(REPO, "include", "*.h")))]
+SRCS = [os.path.join(HERE, "csrc", "ba_kernels.hip"), os.path.join(HERE, "csrc", "passes.hip")]
+DEPS = [*SRCS, *sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), *sorted(glob.glob(os.path.join(REPO, "include", "*.h")))]
 OUT = os.path.join(HERE, "_lib", "libinsfm_ba.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -25,7 +25,7 @@ def build(force=False, verbose=True):
     if not force and not needs_build():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-o", OUT + ".tmp", SRC]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *FLAGS, "-o", OUT + ".tmp", *SRCS]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

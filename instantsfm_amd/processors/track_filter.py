@@ -1,0 +1,96 @@
+"""Track filters -- drop-in for ``instantsfm/processors/track_filter.py`` (reference :1-137): the per-observation
+and per-track geometry on the GPU (csrc/passes.hip), the scene bookkeeping (gathering, per-track compaction, the
+counters and messages the reference prints) on the host, vectorized.
+
+Same signatures, same in-place effects on ``tracks`` and the same return values, including
+FilterTracksByReprojectionNormalized's counter, which the reference computes on the slice of the *next* track
+(track_filter.py:59-63: ``count`` is advanced before the test).
+"""
+import numpy as np
+
+from .. import passes
+
+EPSILON = 1e-10
+
+
+def _gather(images, tracks):
+    """Observations of all tracks in dict order -> (obs [X,2], per-track counts, track rows, global feature row of each
+    observation into the concatenated features_undist, the rays themselves)."""
+    obs = [np.asarray(t.observations).reshape(-1, 2).astype(np.int64, copy=False) for t in tracks.values()]
+    if not obs:
+        raise ValueError("need at least one array to concatenate")  # what the reference's np.concatenate raises
+    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+    allobs = np.concatenate(obs)
+    fu = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) if len(im.features_undist) else np.zeros((0, 3))
+          for im in images]
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu])]).astype(np.int64)
+    rays = np.concatenate(fu) if fu else np.zeros((0, 3))
+    ray_row = foff[allobs[:, 0]] + allobs[:, 1]
+    trow = np.repeat(np.arange(len(obs), dtype=np.int64), counts)
+    return obs, allobs, counts, trow, ray_row, rays
+
+
+def _world2cams(images):
+    return np.array([np.asarray(im.world2cam, dtype=np.float64) for im in images]).reshape(-1, 16)
+
+
+def _xyz(tracks):
+    return np.array([np.asarray(t.xyz, dtype=np.float64) for t in tracks.values()]).reshape(-1, 3)
+
+
+def quirk_counter(valid, counts):
+    """track_filter.py:57-63: after ``count += len_j`` the test reads valid[count : count + len_j]."""
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    inv = np.concatenate([[0], np.cumsum(~valid)])
+    n = valid.shape[0]
+    a = np.minimum(starts[1:], n)
+    b = np.minimum(starts[1:] + counts, n)
+    return int(np.sum(inv[b] - inv[a] > 0))
+
+
+def FilterTracksByReprojectionNormalized(cameras, images, tracks, max_reprojection_error, device="cuda:0"):
+    """track_filter.py:26-66."""
+    obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
+    valid = passes.filter_reproj_normalized(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays,
+                                            max_reprojection_error, device)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    for j, track in enumerate(tracks.values()):
+        track.observations = track.observations[valid[starts[j]:starts[j + 1]]]
+    counter = quirk_counter(valid, counts)
+    print(f'Filtered {counter} / {len(tracks)} tracks by reprojection error')
+    return counter
+
+
+def FilterTracksByAngle(cameras, images, tracks, max_angle_error, device="cuda:0"):
+    """track_filter.py:5-24."""
+    thres = np.cos(np.deg2rad(max_angle_error))
+    obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
+    valid = passes.filter_angle(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays, thres, device)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    counter = 0
+    for j, track in enumerate(tracks.values()):
+        v = valid[starts[j]:starts[j + 1]]
+        if not v.all():
+            counter += 1
+            track.observations = track.observations[np.flatnonzero(v)]
+    print(f'Filtered {counter} / {len(tracks)} tracks by angle error')
+    return tracks
+
+
+def FilterTracksTriangulationAngle(cameras, images, tracks, min_angle, device="cuda:0"):
+    """track_filter.py:116-137: drop tracks whose viewing directions are all within ``min_angle`` of each other."""
+    thres = np.cos(np.deg2rad(min_angle))
+    centers = np.array([np.asarray(im.center(), dtype=np.float64) for im in images]).reshape(-1, 3)
+    keys = list(tracks.keys())
+    obs = [np.asarray(tracks[k].observations).reshape(-1, 2) for k in keys]
+    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+    ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    img = np.concatenate([o[:, 0] for o in obs]).astype(np.int32) if obs else np.zeros(0, np.int32)
+    remove = passes.filter_tri_angle(ptr, img, centers, _xyz(tracks), thres, device) if keys else np.zeros(0, bool)
+    counter = 0
+    for k, r in zip(keys, remove.tolist()):
+        if r:
+            del tracks[k]
+            counter += 1
+    print(f'Filtered {counter} / {counter + len(tracks)} tracks by too small triangulation angle')
+    return counter

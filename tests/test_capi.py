@@ -18,7 +18,7 @@ def header_functions():
         if h.endswith(".h"):
             txt = open(os.path.join(REPO, "include", h)).read()
             txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-            names |= set(re.findall(r"\b(insfm_(?:ba|gp)_[a-z_]+)\s*\(", txt))
+            names |= set(re.findall(r"\b(insfm_[a-z_]+)\s*\(", txt))
     return sorted(names - {"insfm_ba_allreduce_fn"})
 
 

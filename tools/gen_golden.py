@@ -408,10 +408,127 @@ def gen_gp_packing(out_dir, LM):
         print(name + ".npz", res["out_translations"].shape)
 
 
+def gen_passes(out_dir):
+    """Between-round passes: the reference's own track filters and NormalizeReconstruction on a
+    perturbed config-1 scene, img2cam for the models that do not call cv2, cam2img (the forward model) for all."""
+    import copy
+    from scipy.spatial.transform import Rotation
+    from instantsfm.scene.defs import Camera, CameraModelId, Image, Track
+    from instantsfm.processors import track_filter as TF
+    from instantsfm.processors.reconstruction_normalizer import NormalizeReconstruction
+    sys.path.insert(0, REPO)
+    from instantsfm_amd.synth import make_config, quat_to_matrix
+    rng = np.random.default_rng(21)
+    prob = make_config(1, seed=3)
+    C, P = prob.n_cams, prob.n_points
+    order = np.argsort(prob.cam_idx, kind="stable")
+    counts = np.bincount(prob.cam_idx, minlength=C)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    feat_id = np.empty(prob.n_obs, np.int64)
+    feat_id[order] = np.arange(prob.n_obs) - np.repeat(starts[:-1], counts)
+    imgs = []
+    w2cs = []
+    for c in range(C):
+        w2c = np.eye(4)
+        w2c[:3, :3] = quat_to_matrix(prob.cams_gt[c, 3:7])
+        w2c[:3, 3] = prob.cams_gt[c, :3]
+        w2cs.append(w2c)
+    # rays: ground-truth camera-frame directions, small noise, 5% outliers, a few rays pointing backwards
+    fu_all = np.zeros((prob.n_obs, 3))
+    for o in range(prob.n_obs):
+        W = w2cs[prob.cam_idx[o]]
+        pc = W[:3, :3] @ prob.points_gt[prob.pt_idx[o]] + W[:3, 3]
+        fu_all[o] = pc / np.linalg.norm(pc)
+    fu_all += rng.normal(0, 2e-3, fu_all.shape) * (rng.uniform(size=(prob.n_obs, 1)) < 0.95)
+    fu_all += rng.normal(0, 5e-2, fu_all.shape) * (rng.uniform(size=(prob.n_obs, 1)) >= 0.95)
+    fu_all /= np.linalg.norm(fu_all, axis=1, keepdims=True)
+    depth_all = np.where(rng.uniform(size=prob.n_obs) < 0.7, rng.uniform(5, 60, prob.n_obs), 0.0)
+    for c in range(C):
+        sl = order[starts[c]:starts[c + 1]]
+        W = w2cs[c].copy()
+        W[:3, :3] = W[:3, :3] @ Rotation.from_rotvec(rng.normal(0, 2e-3, 3)).as_matrix()
+        imgs.append(Image(id=c, cam_id=c, is_registered=True, world2cam=W, features=prob.uv[sl].copy(),
+                          features_undist=fu_all[sl].copy(), depths=depth_all[sl].copy()))
+    ptr = np.concatenate([[0], np.cumsum(np.bincount(prob.pt_idx, minlength=P))])
+    pairs = np.stack([prob.cam_idx.astype(np.int64), feat_id], 1)
+    tracks = {}
+    for p in range(P):
+        xyz = prob.points_gt[p] + rng.normal(0, 0.02, 3)
+        ob = pairs[ptr[p]:ptr[p + 1]].copy()
+        if p % 97 == 5:
+            ob = ob[:1]                                # single-view track
+        if p % 89 == 7:
+            ob = np.concatenate([ob, ob[:1]])          # duplicate observation of one image
+        if p % 83 == 11:
+            xyz = -3.0 * prob.cams_gt[prob.cam_idx[ptr[p]], :3]  # far away / behind some cameras
+        tracks[5 * p + 2] = Track(id=5 * p + 2, xyz=xyz, observations=ob)
+    tracks[10 ** 6] = Track(id=10 ** 6, xyz=np.zeros(3), observations=np.zeros((0, 2), np.int64))  # empty track
+    res = dict(
+        w2c=np.stack([im.world2cam for im in imgs]), feat_ptr=starts, feats_undist=np.concatenate([im.features_undist for im in imgs]),
+        depths=np.concatenate([im.depths for im in imgs]),
+        track_keys=np.array(list(tracks.keys())), track_xyz=np.stack([t.xyz for t in tracks.values()]),
+        track_ptr=np.concatenate([[0], np.cumsum([len(t.observations) for t in tracks.values()])]),
+        track_obs=np.concatenate([t.observations for t in tracks.values()]).astype(np.int64))
+
+    def run(fn, *a):
+        ims, trs = copy.deepcopy(imgs), copy.deepcopy(tracks)
+        out = fn(ims, trs, *a)
+        return ims, trs, out
+
+    def tracks_out(trs, prefix):
+        return {prefix + "keys": np.array(list(trs.keys())),
+                prefix + "ptr": np.concatenate([[0], np.cumsum([len(t.observations) for t in trs.values()])]),
+                prefix + "obs": (np.concatenate([np.asarray(t.observations).reshape(-1, 2) for t in trs.values()])
+                                 if trs else np.zeros((0, 2))).astype(np.int64)}
+    # FilterTracksByReprojectionNormalized needs at least one observation per concatenation -> drop the empty track
+    for thr in (1e-2, 3e-2):
+        ims, trs = copy.deepcopy(imgs), copy.deepcopy({k: v for k, v in tracks.items() if len(v.observations)})
+        cnt = TF.FilterTracksByReprojectionNormalized(None, ims, trs, thr)
+        res.update(tracks_out(trs, f"reproj_{thr:g}_"))
+        res[f"reproj_{thr:g}_counter"] = np.array(cnt)
+    ims, trs = copy.deepcopy(imgs), copy.deepcopy({k: v for k, v in tracks.items() if len(v.observations)})
+    TF.FilterTracksByAngle(None, ims, trs, 1.0)
+    res.update(tracks_out(trs, "angle_"))
+    ims, trs = copy.deepcopy(imgs), copy.deepcopy(tracks)
+    cnt = TF.FilterTracksTriangulationAngle(None, ims, trs, 1.5)
+    res.update(tracks_out(trs, "tri_"))
+    res["tri_counter"] = np.array(cnt)
+    for name, dep in (("norm_", None), ("normdepth_", np.ones(3))):
+        ims, trs = copy.deepcopy(imgs), copy.deepcopy(tracks)
+        NormalizeReconstruction(ims, trs, dep)
+        res[name + "w2c"] = np.stack([im.world2cam for im in ims])
+        res[name + "xyz"] = np.stack([t.xyz for t in trs.values()])
+    np.savez_compressed(os.path.join(out_dir, "passes_golden.npz"), **res)
+    print("passes_golden.npz", len(res), "arrays")
+
+    # camera models: img2cam where it is numpy-only (0, 1, 7), cam2img (forward) for every model
+    cam_res = {}
+    base = {0: [900.0, 500.0, 400.0], 1: [900.0, 950.0, 500.0, 400.0], 2: [900.0, 500.0, 400.0, -0.05],
+            3: [900.0, 500.0, 400.0, -0.05, 0.01], 4: [900.0, 950.0, 500.0, 400.0, -0.05, 0.01, 1e-3, -2e-3],
+            5: [900.0, 950.0, 500.0, 400.0, -0.02, 0.004, -1e-3, 5e-4],
+            6: [900.0, 950.0, 500.0, 400.0, -0.05, 0.01, 1e-3, -2e-3, 3e-3, 0.02, -0.004, 6e-4],
+            7: [900.0, 950.0, 500.0, 400.0, 0.9], 8: [900.0, 500.0, 400.0, -0.03], 9: [900.0, 500.0, 400.0, -0.03, 0.006],
+            10: [900.0, 950.0, 500.0, 400.0, -0.02, 0.004, 1e-3, -2e-3, 1e-3, 5e-4, 2e-4, -3e-4]}
+    for m, prm in base.items():
+        cam = Camera(id=0, model_id=CameraModelId(m), params=list(prm))
+        uvw = np.stack([rng.uniform(-0.6, 0.6, 300), rng.uniform(-0.45, 0.45, 300), np.ones(300)], 1)
+        cam_res[f"m{m}_params"] = np.array(prm)
+        cam_res[f"m{m}_uv"] = uvw[:, :2].copy()
+        cam_res[f"m{m}_cam2img"] = cam.cam2img(uvw.copy())
+        if m in (0, 1, 7):
+            xy = rng.uniform([0, 0], [1000, 800], (300, 2))
+            cam_res[f"m{m}_xy"] = xy
+            cam_res[f"m{m}_img2cam"] = cam.img2cam(xy.copy())
+            cam_res[f"m{m}_xy32"] = xy.astype(np.float32)
+            cam_res[f"m{m}_img2cam32"] = cam.img2cam(xy.astype(np.float32))
+    np.savez_compressed(os.path.join(out_dir, "camera_models_golden.npz"), **cam_res)
+    print("camera_models_golden.npz", len(cam_res), "arrays")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
-    ap.add_argument("--only", choices=("projection", "packing", "gp"), default=None)
+    ap.add_argument("--only", choices=("projection", "packing", "gp", "passes"), default=None)
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     with tempfile.TemporaryDirectory():
@@ -424,6 +541,8 @@ def main():
         if args.only in (None, "gp"):
             gen_gp_cost(args.out)
             gen_gp_packing(args.out, LM)
+        if args.only in (None, "passes"):
+            gen_passes(args.out)
 
 
 if __name__ == "__main__":
