@@ -7,7 +7,11 @@
  *       -> insfm_undistort(): every feature of every image -> unit ray [x, y, 1] / ||.||;
  *   - FilterTracksByReprojectionNormalized (processors/track_filter.py:26-66) -> insfm_filter_reproj_normalized();
  *   - FilterTracksByAngle (track_filter.py:5-24)                            -> insfm_filter_angle();
- *   - FilterTracksTriangulationAngle (track_filter.py:116-137)             -> insfm_filter_tri_angle().
+ *   - FilterTracksTriangulationAngle (track_filter.py:116-137)             -> insfm_filter_tri_angle();
+ * and, for RetriangulateTracks (processors/track_retriangulation.py:215-259):
+ *   - FilterTracksByReprojection (track_filter.py:68-113, pixel space via Camera.cam2img, defs.py:371-412)
+ *                                                                          -> insfm_filter_reproj_pixel();
+ *   - complete_tracks' candidate reprojection (track_retriangulation.py:43-92) -> insfm_reproj_candidates().
  * The kernels compute per feature / observation / track; the scene bookkeeping (gathering the arrays from the scene
  * objects, the per-track compaction, the counters) stays in the host processors (instantsfm_amd/processors/).
  *
@@ -48,6 +52,26 @@ int insfm_filter_angle(int64_t n_obs, const int32_t* obs_img, const int32_t* obs
  * duplicate images do not change the outcome, so no np.unique is needed).  centers [M,3]. */
 int insfm_filter_tri_angle(int64_t n_tracks, const int64_t* track_ptr, const int32_t* obs_img, const double* centers,
                            const double* track_xyz, double cos_thres, uint8_t* remove, void* stream);
+
+/* Per observation x: p = world2cam[img] [xyz[track], 1]; the pixel projection of p through Camera.cam2img of camera
+ * img_cam[img] (model cam_model[c], params cam_params[c,12] = the reference's Camera.params, zero padded);
+ * valid[x] = p.z > 1e-10 && ||proj - feats[obs_feat[x]]|| < max_err (track_filter.py:68-113).  feats [F,2] is float32
+ * when feats_f32 != 0 (the database's keypoint type), else float64.  err (nullable) receives the error. */
+int insfm_filter_reproj_pixel(int64_t n_obs, const int32_t* obs_img, const int32_t* obs_track, const int64_t* obs_feat,
+                              const void* feats, int32_t feats_f32, const int32_t* img_cam, const int32_t* cam_model,
+                              const double* cam_params, const double* world2cam, const double* track_xyz, double max_err,
+                              uint8_t* valid, double* err, void* stream);
+
+/* complete_tracks (track_retriangulation.py:58-90): candidate x observes feats[cand_feat[x]] in image cand_img[x] of
+ * track point track_xyz[cand_track[x]].  image_rows [M, 7+n_intr] are the reference's per-image rows
+ * [t, q_xyzw (scipy as_quat of world2cam), camera params without the principal point], image_pps [M,2] the
+ * principal points; the projection is reproject_funcs[cam_model] (cost_function.py:32-208).
+ * valid[x] = rotate_quat(X).z > 1e-7 && ||proj - uv|| <= max_err.  FOV (7) and THIN_PRISM_FISHEYE (10) return
+ * INSFM_BA_EINVAL (their reproject functions raise NotImplementedError). */
+int insfm_reproj_candidates(int64_t n, int32_t cam_model, const int32_t* cand_img, const int32_t* cand_track,
+                            const int64_t* cand_feat, const void* feats, int32_t feats_f32, const double* image_rows,
+                            const double* image_pps, const double* track_xyz, double max_err, uint8_t* valid, double* err,
+                            void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,6 +12,8 @@
 
 #pragma clang fp contract(off)
 
+#include "ba_device.h"  // eval_obs<M>: the reproject_funcs restatement shared with the BA kernels
+
 namespace {
 
 constexpr int kT = 256;
@@ -216,6 +218,154 @@ __global__ __launch_bounds__(kT) void k_filter_tri_angle(int64_t nt, const int64
     remove[t] = all ? 1 : 0;
 }
 
+// Camera.cam2img (scene/defs.py:371-412) of one camera-frame point, with Camera.Distortion (defs.py:257-313) and
+// fisheye_from_normal (defs.py:246-250) in numpy's operation order; p is the reference's Camera.params vector.
+// Integer powers follow numpy: r2**2 is a square (r2 * r2), r2**3 goes through pow().
+__device__ void cam2img(int model, const double* p, double X, double Y, double Z, double& xo, double& yo) {
+    const bool single = model == 0 || model == 2 || model == 3 || model == 8 || model == 9;
+    const double fx = p[0], fy = single ? p[0] : p[1];
+    const double cx = single ? p[1] : p[2], cy = single ? p[2] : p[3];
+    const double f = (fx + fy) / 2;  // np.mean(focal_length)
+    const double zz = Z + 1e-10;
+    double u = X / zz, v = Y / zz;
+    const bool fisheye = model == 5 || model == 8 || model == 9 || model == 10;
+    if (fisheye) {  // uv * arctan(r) / r, r = max(||uv||, 1e-8)
+        double r = sqrt(u * u + v * v);
+        r = r < 1e-8 ? 1e-8 : r;
+        const double th = atan(r);
+        u = u * th / r;
+        v = v * th / r;
+    }
+    const double r2 = u * u + v * v;
+    bool use_ff = false;
+    switch (model) {
+        case 0: break;
+        case 1: use_ff = true; break;
+        case 2: case 8: {
+            const double du = u * p[3] * r2, dv = v * p[3] * r2;
+            u += du; v += dv;
+        } break;
+        case 3: case 9: {
+            const double du = u * p[3] * r2 + u * p[4] * (r2 * r2), dv = v * p[3] * r2 + v * p[4] * (r2 * r2);
+            u += du; v += dv;
+        } break;
+        case 4: case 6: case 10: {
+            use_ff = true;
+            double radial;
+            if (model == 4) radial = p[4] * r2 + p[5] * (r2 * r2);
+            else if (model == 6)
+                radial = (1 + p[4] * r2 + p[5] * (r2 * r2) + p[8] * pow(r2, 3.0)) /
+                         (1 + p[9] * r2 + p[10] * (r2 * r2) + p[11] * pow(r2, 3.0)) - 1;
+            else radial = p[4] * r2 + p[5] * (r2 * r2) + p[8] * pow(r2, 3.0);
+            const double p0 = p[6], p1 = p[7], uv_ = u * v;
+            double dx = u * radial + 2 * p0 * uv_, dy = v * radial + 2 * p1 * uv_;
+            dx += p1 * (r2 + 2 * (u * u));
+            dy += p0 * (r2 + 2 * (v * v));
+            if (model == 10) { dx += p[10] * r2; dy += p[11] * r2; }
+            u += dx; v += dy;
+        } break;
+        case 5: {
+            use_ff = true;
+            const double radial = p[4] * r2 + p[5] * (r2 * r2) + p[6] * pow(r2, 3.0);
+            const double du = u * radial, dv = v * radial;
+            u += du; v += dv;
+        } break;
+        case 7: {  // FOV: uv = Distortion(uv), then the mean focal
+            const double omega = p[4], omega2 = omega * omega, eps = 1e-4;
+            double factor;
+            if (omega2 < eps) factor = (omega2 * r2) / 3 - omega2 / 12 + 1;
+            else if (r2 < eps) {
+                const double th = tan(omega / 2);
+                factor = (-2 * th * (4 * r2 * (th * th) - 3)) / (3 * omega);
+            } else {
+                const double radius = sqrt(r2);
+                factor = atan(radius * 2 * tan(omega / 2)) / (radius * omega);
+            }
+            u = u * factor; v = v * factor;
+        } break;
+        default: break;
+    }
+    xo = use_ff ? u * fx + cx : u * f + cx;
+    yo = use_ff ? v * fy + cy : v * f + cy;
+}
+
+// FilterTracksByReprojection (track_filter.py:68-113): p = world2cam[img] [xyz, 1] (einsum order as k_filter_reproj),
+// pixel reprojection through the image's camera, error against the raw feature (float32 or float64).
+__global__ __launch_bounds__(kT) void k_filter_reproj_pixel(int64_t n, const int32_t* __restrict__ obs_img,
+                                                            const int32_t* __restrict__ obs_track,
+                                                            const int64_t* __restrict__ obs_feat, const void* __restrict__ feats,
+                                                            int f32, const int32_t* __restrict__ img_cam,
+                                                            const int32_t* __restrict__ cam_model,
+                                                            const double* __restrict__ cam_params, const double* __restrict__ w2c,
+                                                            const double* __restrict__ xyz, double max_err,
+                                                            uint8_t* __restrict__ valid, double* __restrict__ err_out) {
+    const int64_t x = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= n) return;
+    const int im = obs_img[x];
+    const double* W = w2c + 16 * (size_t)im;
+    const double* X = xyz + 3 * (size_t)obs_track[x];
+    const double X0 = X[0], X1 = X[1], X2 = X[2];
+    const double p0 = W[0] * X0 + W[1] * X1 + W[2] * X2 + W[3];
+    const double p1 = W[4] * X0 + W[5] * X1 + W[6] * X2 + W[7];
+    const double p2 = W[8] * X0 + W[9] * X1 + W[10] * X2 + W[11];
+    const int c = img_cam[im];
+    double px, py;
+    cam2img(cam_model[c], cam_params + 12 * (size_t)c, p0, p1, p2, px, py);
+    double fu, fv;
+    if (f32) {
+        const float2 q = reinterpret_cast<const float2*>(feats)[obs_feat[x]];
+        fu = q.x; fv = q.y;
+    } else {
+        const double2 q = reinterpret_cast<const double2*>(feats)[obs_feat[x]];
+        fu = q.x; fv = q.y;
+    }
+    const double d0 = px - fu, d1 = py - fv;
+    const double e = sqrt(d0 * d0 + d1 * d1);
+    valid[x] = (p2 > kEps) && (e < max_err);
+    if (err_out) err_out[x] = e;
+}
+
+// complete_tracks' candidate test (track_retriangulation.py:58-90): reproject_funcs[M] (eval_obs, the BA kernels'
+// projection) with the image's row [t, q_xyzw, intrinsics without pp] and pp; valid = z > 1e-7 && ||err|| <= thr.
+template <int M>
+__global__ __launch_bounds__(kT) void k_reproj_candidates(int64_t n, const int32_t* __restrict__ cand_img,
+                                                          const int32_t* __restrict__ cand_track,
+                                                          const int64_t* __restrict__ cand_feat,
+                                                          const void* __restrict__ feats, int f32,
+                                                          const double* __restrict__ rows, const double* __restrict__ pps,
+                                                          const double* __restrict__ xyz, double thr,
+                                                          uint8_t* __restrict__ valid, double* __restrict__ err_out) {
+    constexpr int S = insfm::kStride<M>;
+    const int64_t x = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (x >= n) return;
+    const int im = cand_img[x];
+    double cam[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) cam[j] = rows[(size_t)im * S + j];
+    const double Xp[3] = {xyz[3 * (size_t)cand_track[x]], xyz[3 * (size_t)cand_track[x] + 1],
+                          xyz[3 * (size_t)cand_track[x] + 2]};
+    const double pp[2] = {pps[2 * (size_t)im], pps[2 * (size_t)im + 1]};
+    double uv[2];
+    if (f32) {
+        const float2 q = reinterpret_cast<const float2*>(feats)[cand_feat[x]];
+        uv[0] = q.x; uv[1] = q.y;
+    } else {
+        const double2 q = reinterpret_cast<const double2*>(feats)[cand_feat[x]];
+        uv[0] = q.x; uv[1] = q.y;
+    }
+    double r[2];
+    insfm::eval_obs<M, false>(cam, Xp, pp, uv, r, nullptr, nullptr);
+    // rotate_quat z (the same expression eval_obs evaluates)
+    const double qx = cam[3], qy = cam[4], qw = cam[6];
+    const double c1z = qx * Xp[1] - qy * Xp[0];
+    const double c1x = qy * Xp[2] - cam[5] * Xp[1], c1y = cam[5] * Xp[0] - qx * Xp[2];
+    const double c2z = qx * c1y - qy * c1x;
+    const double pz = Xp[2] + 2.0 * (qw * c1z + c2z) + cam[2];
+    const double e = sqrt(r[0] * r[0] + r[1] * r[1]);
+    valid[x] = (e <= thr) && (pz > 1e-7);
+    if (err_out) err_out[x] = e;
+}
+
 inline unsigned grid(int64_t n) { return (unsigned)((n + kT - 1) / kT); }
 
 int finish() {
@@ -266,6 +416,43 @@ int insfm_filter_tri_angle(int64_t n_tracks, const int64_t* track_ptr, const int
     k_filter_tri_angle<<<grid(n_tracks), kT, 0, reinterpret_cast<hipStream_t>(stream)>>>(n_tracks, track_ptr, obs_img,
                                                                                         centers, track_xyz, cos_thres, remove);
     return finish();
+}
+
+int insfm_filter_reproj_pixel(int64_t n_obs, const int32_t* obs_img, const int32_t* obs_track, const int64_t* obs_feat,
+                              const void* feats, int32_t feats_f32, const int32_t* img_cam, const int32_t* cam_model,
+                              const double* cam_params, const double* world2cam, const double* track_xyz, double max_err,
+                              uint8_t* valid, double* err, void* stream) {
+    if (n_obs < 0 || (n_obs > 0 && (!obs_img || !obs_track || !obs_feat || !feats || !img_cam || !cam_model || !cam_params ||
+                                    !world2cam || !track_xyz || !valid)))
+        return INSFM_BA_EINVAL;
+    if (n_obs == 0) return INSFM_BA_OK;
+    k_filter_reproj_pixel<<<grid(n_obs), kT, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        n_obs, obs_img, obs_track, obs_feat, feats, feats_f32, img_cam, cam_model, cam_params, world2cam, track_xyz, max_err,
+        valid, err);
+    return finish();
+}
+
+int insfm_reproj_candidates(int64_t n, int32_t cam_model, const int32_t* cand_img, const int32_t* cand_track,
+                            const int64_t* cand_feat, const void* feats, int32_t feats_f32, const double* image_rows,
+                            const double* image_pps, const double* track_xyz, double max_err, uint8_t* valid, double* err,
+                            void* stream) {
+    if (n < 0 || (n > 0 && (!cand_img || !cand_track || !cand_feat || !feats || !image_rows || !image_pps || !track_xyz ||
+                            !valid)))
+        return INSFM_BA_EINVAL;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+#define INSFM_CAND(M)                                                                                                      \
+    case M:                                                                                                                \
+        if (n > 0)                                                                                                         \
+            k_reproj_candidates<M><<<grid(n), kT, 0, s>>>(n, cand_img, cand_track, cand_feat, feats, feats_f32, image_rows, \
+                                                          image_pps, track_xyz, max_err, valid, err);                      \
+        break;
+    switch (cam_model) {
+        INSFM_CAND(0) INSFM_CAND(1) INSFM_CAND(2) INSFM_CAND(3) INSFM_CAND(4) INSFM_CAND(5) INSFM_CAND(6) INSFM_CAND(8)
+        INSFM_CAND(9)
+        default: return INSFM_BA_EINVAL;  // FOV / THIN_PRISM_FISHEYE: reproject_funcs raises (cost_function.py:125,179)
+    }
+#undef INSFM_CAND
+    return n > 0 ? finish() : INSFM_BA_OK;
 }
 
 }  // extern "C"

@@ -95,3 +95,53 @@ def filter_tri_angle(track_ptr, obs_img, centers, track_xyz, cos_thres, device="
         _check(L.insfm_filter_tri_angle(nt, *[_p(t) for t in a], float(cos_thres), _p(remove), _stream(dev)),
                "insfm_filter_tri_angle")
     return remove.cpu().numpy().astype(bool)
+
+
+def _feats(feats, dev):
+    """Concatenated features [F,2]: float32 stays float32 (the database's keypoint type), anything else float64."""
+    a = np.asarray(feats)
+    f32 = a.dtype == np.float32
+    a = a.astype(np.float32 if f32 else np.float64, copy=False).reshape(-1, 2)
+    if a.shape[0] == 0:
+        a = np.zeros((1, 2), a.dtype)
+    return _dev(a, dev), int(f32)
+
+
+def filter_reproj_pixel(obs_img, obs_track, obs_feat, feats, img_cam, cam_model, cam_params, world2cam, track_xyz,
+                        max_err, device="cuda:0", with_err=False):
+    """FilterTracksByReprojection's per-observation test (track_filter.py:68-113) on the GPU."""
+    dev = _require_gpu(device)
+    L = _capi.load()
+    n = int(np.asarray(obs_img).shape[0])
+    valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    err = torch.empty(n, dtype=torch.float64, device=dev) if with_err else None
+    if n:
+        params = np.zeros((len(cam_model), 12))
+        for i, p in enumerate(cam_params):
+            p = np.asarray(p, dtype=np.float64).reshape(-1)
+            params[i, :p.size] = p
+        ft, f32 = _feats(feats, dev)
+        a = [_dev(obs_img, dev, np.int32), _dev(obs_track, dev, np.int32), _dev(obs_feat, dev, np.int64)]
+        b = [_dev(img_cam, dev, np.int32), _dev(cam_model, dev, np.int32), _dev(params, dev),
+             _dev(np.asarray(world2cam, dtype=np.float64).reshape(-1, 16), dev), _dev(track_xyz, dev, np.float64)]
+        _check(L.insfm_filter_reproj_pixel(n, *[_p(t) for t in a], _p(ft), f32, *[_p(t) for t in b], float(max_err),
+                                           _p(valid), _p(err), _stream(dev)), "insfm_filter_reproj_pixel")
+    v = valid.cpu().numpy().astype(bool)
+    return (v, err.cpu().numpy()) if with_err else v
+
+
+def reproj_candidates(cam_model, cand_img, cand_track, cand_feat, feats, image_rows, image_pps, track_xyz, max_err,
+                      device="cuda:0", with_err=False):
+    """complete_tracks' candidate test (track_retriangulation.py:58-90) on the GPU."""
+    dev = _require_gpu(device)
+    L = _capi.load()
+    n = int(np.asarray(cand_img).shape[0])
+    valid = torch.zeros(n, dtype=torch.uint8, device=dev)
+    err = torch.empty(n, dtype=torch.float64, device=dev) if with_err else None
+    ft, f32 = _feats(feats, dev)
+    a = [_dev(cand_img, dev, np.int32), _dev(cand_track, dev, np.int32), _dev(cand_feat, dev, np.int64)]
+    b = [_dev(image_rows, dev, np.float64), _dev(image_pps, dev, np.float64), _dev(track_xyz, dev, np.float64)]
+    _check(L.insfm_reproj_candidates(n, int(cam_model), *[_p(t) for t in a], _p(ft), f32, *[_p(t) for t in b],
+                                     float(max_err), _p(valid), _p(err), _stream(dev)), "insfm_reproj_candidates")
+    v = valid.cpu().numpy().astype(bool)
+    return (v, err.cpu().numpy()) if with_err else v

@@ -1,4 +1,4 @@
-"""Track filters -- drop-in for ``instantsfm/processors/track_filter.py`` (reference :1-137): the per-observation
+"""Track filters -- drop-in for ``instantsfm/processors/track_filter.py`` (reference :1-137, all four filters): the per-observation
 and per-track geometry on the GPU (csrc/passes.hip), the scene bookkeeping (gathering, per-track compaction, the
 counters and messages the reference prints) on the host, vectorized.
 
@@ -13,20 +13,25 @@ from .. import passes
 EPSILON = 1e-10
 
 
-def _gather(images, tracks):
-    """Observations of all tracks in dict order -> (obs [X,2], per-track counts, track rows, global feature row of each
-    observation into the concatenated features_undist, the rays themselves)."""
+def _gather_obs(tracks):
     obs = [np.asarray(t.observations).reshape(-1, 2).astype(np.int64, copy=False) for t in tracks.values()]
     if not obs:
         raise ValueError("need at least one array to concatenate")  # what the reference's np.concatenate raises
     counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
     allobs = np.concatenate(obs)
+    trow = np.repeat(np.arange(len(obs), dtype=np.int64), counts)
+    return obs, allobs, counts, trow, None, None
+
+
+def _gather(images, tracks):
+    """Observations of all tracks in dict order -> (obs [X,2], per-track counts, track rows, global feature row of each
+    observation into the concatenated features_undist, the rays themselves)."""
+    obs, allobs, counts, trow, _, _ = _gather_obs(tracks)
     fu = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) if len(im.features_undist) else np.zeros((0, 3))
           for im in images]
     foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu])]).astype(np.int64)
     rays = np.concatenate(fu) if fu else np.zeros((0, 3))
     ray_row = foff[allobs[:, 0]] + allobs[:, 1]
-    trow = np.repeat(np.arange(len(obs), dtype=np.int64), counts)
     return obs, allobs, counts, trow, ray_row, rays
 
 
@@ -53,6 +58,33 @@ def FilterTracksByReprojectionNormalized(cameras, images, tracks, max_reprojecti
     obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
     valid = passes.filter_reproj_normalized(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays,
                                             max_reprojection_error, device)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    for j, track in enumerate(tracks.values()):
+        track.observations = track.observations[valid[starts[j]:starts[j + 1]]]
+    counter = quirk_counter(valid, counts)
+    print(f'Filtered {counter} / {len(tracks)} tracks by reprojection error')
+    return counter
+
+
+def _features(images):
+    """Concatenated raw features of all images [F,2] and each image's first row.  float32 when every image's
+    features are float32 (the database's keypoint type), else float64 (the reference's ``np.array(features)`` then
+    promotes against the float64 projection either way, so the values are exact)."""
+    fs = [np.asarray(im.features).reshape(-1, 2) for im in images]
+    f32 = all(f.dtype == np.float32 for f in fs if f.size)
+    fs = [f.astype(np.float32 if f32 else np.float64, copy=False) for f in fs]
+    off = np.concatenate([[0], np.cumsum([f.shape[0] for f in fs])]).astype(np.int64)
+    return (np.concatenate(fs) if fs else np.zeros((0, 2))), off
+
+
+def FilterTracksByReprojection(cameras, images, tracks, max_reprojection_error, device="cuda:0"):
+    """track_filter.py:68-113: pixel reprojection error through each image's Camera.cam2img."""
+    obs, allobs, counts, trow, _, _ = _gather_obs(tracks)
+    feats, foff = _features(images)
+    img_cam = np.array([im.cam_id for im in images], dtype=np.int32)
+    valid = passes.filter_reproj_pixel(allobs[:, 0], trow, foff[allobs[:, 0]] + allobs[:, 1], feats, img_cam,
+                                       [cam.model_id.value for cam in cameras], [cam.params for cam in cameras],
+                                       _world2cams(images), _xyz(tracks), max_reprojection_error, device)
     starts = np.concatenate([[0], np.cumsum(counts)])
     for j, track in enumerate(tracks.values()):
         track.observations = track.observations[valid[starts[j]:starts[j + 1]]]

@@ -318,3 +318,38 @@ def make_gp_problem(n_cams, n_points, track_len=10, seed=0, window=30, ray_sigma
         points_init = points + rng.normal(0, init_sigma, (P, 3))
     return GPProblem(np.ascontiguousarray(rays), cam_idx, pt_idx, fcam, sfree, centers, points,
                      np.ascontiguousarray(cams_init), np.ascontiguousarray(points_init), np.ascontiguousarray(scales_init))
+
+
+# ------------------------------------------------------------------------------------------------------------
+# retriangulation scenes (RetriangulateTracks, track_retriangulation.py:215-259)
+# ------------------------------------------------------------------------------------------------------------
+def make_retri_scene(model=2, n_cams=20, n_points=600, seed=0, point_sigma=0.01, drop_frac=0.25, wrong_frac=0.03,
+                     far_frac=0.02, missing_frac=0.05, features_dtype=np.float32):
+    """(cameras, images, tracks, tracks_orig) for complete_tracks / RetriangulateTracks.
+
+    Ground-truth poses; float32 features (the database's keypoint type).  ``tracks_orig`` holds every track's full
+    observation list (as TrackEngine.EstablishFullTracks returns: id -> int array [k, 2]) plus a few wrong
+    observations (another track's feature in a random image); ``tracks`` keeps a random subset of each track's
+    observations (the completion re-adds the rest), perturbed points, some points moved far away (no candidate
+    passes), and lacks a few ids of ``tracks_orig`` altogether.  Track ids are non-contiguous."""
+    prob = make_problem(n_cams, n_points, seed=seed, model=model)
+    cameras, images, tracks0 = to_scene(prob, use_init=False, image_features_dtype=features_dtype)
+    rng = np.random.default_rng(seed + 1000)
+    nfeat = np.array([len(im.features) for im in images])
+    tracks, tracks_orig = {}, {}
+    for p, t in tracks0.items():
+        tid = 7 * p + 3
+        full = t.observations.astype(np.int64)
+        if rng.uniform() < wrong_frac:
+            img = int(rng.integers(0, n_cams))
+            full = np.concatenate([full, [[img, int(rng.integers(0, nfeat[img]))]]])
+        tracks_orig[tid] = full
+        if rng.uniform() < missing_frac:
+            continue
+        keep = rng.uniform(size=t.observations.shape[0]) >= drop_frac
+        keep[:2] = True
+        xyz = t.xyz + rng.normal(0, point_sigma, 3)
+        if rng.uniform() < far_frac:
+            xyz = xyz + rng.normal(0, 3.0, 3)
+        tracks[tid] = Track(id=tid, xyz=xyz, observations=t.observations[keep].copy(), is_initialized=True)
+    return cameras, images, tracks, tracks_orig

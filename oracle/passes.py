@@ -181,3 +181,147 @@ def filter_tri_angle(images, tracks, min_angle):
         if np.all(pts @ pts.T > thres):
             out.append(key)
     return out
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Retriangulation passes: Camera.cam2img, FilterTracksByReprojection, complete_tracks.
+
+def cam2img(model, params, uvw):
+    """Camera.cam2img (scene/defs.py:371-412) with Camera.Distortion (defs.py:257-313) and fisheye_from_normal
+    (defs.py:246-250), numpy float64, the reference's operation order.  Pinned by camera_models_golden.npz."""
+    params = np.asarray(params, dtype=np.float64)
+    fx, fy, cx, cy = focal_pp(model, params)
+    pp = np.array([cx, cy])
+    ff = np.array([fx, fy])
+    f = np.mean(ff)
+    uv = uvw[..., :2] / (np.expand_dims(uvw[..., 2], axis=-1) + 1e-10)
+
+    def fisheye_from_normal(uv):
+        r = np.linalg.norm(uv, axis=-1, keepdims=True)
+        r = np.clip(r, 1e-8, None)
+        return uv * np.arctan(r) / r
+
+    def r2_of(uv):
+        return np.sum(uv ** 2, axis=-1, keepdims=True)
+
+    def tangential(uv, p, r2):
+        uv_ = np.expand_dims(uv[..., 0] * uv[..., 1], axis=-1)
+        return 2 * p * uv_, p[::-1] * (r2 + 2 * uv ** 2)
+
+    if model == 0:
+        return uv * f + pp
+    if model == 1:
+        return uv * ff + pp
+    if model in (2, 8):
+        if model == 8:
+            uv = fisheye_from_normal(uv)
+        r2 = r2_of(uv)
+        uv += uv * params[3] * r2
+        return uv * f + pp
+    if model in (3, 9):
+        if model == 9:
+            uv = fisheye_from_normal(uv)
+        r2 = r2_of(uv)
+        uv += uv * params[3] * r2 + uv * params[4] * r2 ** 2
+        return uv * f + pp
+    if model == 4:
+        r2 = r2_of(uv)
+        p = params[6:8]
+        a, b = tangential(uv, p, r2)
+        d = uv * (params[4] * r2 + params[5] * r2 ** 2) + a
+        d += b
+        uv += d
+        return uv * ff + pp
+    if model == 5:
+        uv = fisheye_from_normal(uv)
+        r2 = r2_of(uv)
+        uv += uv * (params[4] * r2 + params[5] * r2 ** 2 + params[6] * r2 ** 3)
+        return uv * ff + pp
+    if model == 6:
+        r2 = r2_of(uv)
+        k = params[[4, 5, 8, 9, 10, 11]]
+        radial = (1 + k[0] * r2 + k[1] * r2 ** 2 + k[2] * r2 ** 3) / (1 + k[3] * r2 + k[4] * r2 ** 2 + k[5] * r2 ** 3) - 1
+        a, b = tangential(uv, params[6:8], r2)
+        d = uv * radial + a
+        d += b
+        uv += d
+        return uv * ff + pp
+    if model == 7:
+        omega = params[4]
+        r2 = r2_of(uv)
+        omega2 = omega ** 2
+        eps = 1e-4
+        if omega2 < eps:
+            factor = (omega2 * r2) / 3 - omega2 / 12 + 1
+        else:
+            factor = np.zeros_like(r2)
+            m = r2 < eps
+            th = np.tan(omega / 2)
+            factor[m] = (-2 * th * (4 * r2[m] * th ** 2 - 3)) / (3 * omega)
+            radius = np.sqrt(r2[~m])
+            factor[~m] = np.arctan(radius * 2 * np.tan(omega / 2)) / (radius * omega)
+        return uv * factor * f + pp
+    if model == 10:
+        uv = fisheye_from_normal(uv)
+        r2 = r2_of(uv)
+        k = params[[4, 5, 8, 9]]
+        a, b = tangential(uv, params[6:8], r2)
+        d = uv * (k[0] * r2 + k[1] * r2 ** 2 + k[2] * r2 ** 3) + a
+        d += b
+        d += params[10:12] * r2
+        uv += d
+        return uv * ff + pp
+    raise NotImplementedError
+
+
+def filter_reproj_pixel(cameras, images, tracks, max_reprojection_error):
+    """FilterTracksByReprojection (track_filter.py:68-113): valid mask over the concatenated observations, per-track
+    counts, the reference's counter (same next-track-slice quirk as the normalized filter) and the errors."""
+    img, feat, trow, counts = gather_obs(tracks, images)
+    w2c = np.array([im.world2cam for im in images])[img]
+    cam_of = np.array([im.cam_id for im in images])[img]
+    xyz = np.hstack([np.array([t.xyz for t in tracks.values()]), np.ones((len(tracks), 1))])[trow]
+    feats = np.array([images[i].features[f] for i, f in zip(img.tolist(), feat.tolist())]).reshape(-1, 2)
+    pc = np.einsum('ijk,ik->ij', w2c, xyz)[:, :3]
+    valid = pc[:, 2] > EPSILON
+    pr = np.zeros((len(feats), 2))
+    for i, cam in enumerate(cameras):
+        m = cam_of == i
+        pr[m] = cam2img(cam.model_id.value, cam.params, pc[m])
+    err = np.linalg.norm(pr - feats, axis=1)
+    valid = valid & (err < max_reprojection_error)
+    return valid, counts, quirk_counter(valid, counts), err
+
+
+def complete_candidates(cameras, images, tracks, tracks_orig, max_reproj_error):
+    """complete_tracks' candidate test (track_retriangulation.py:43-92): for every observation of every track of
+    ``tracks_orig`` whose id is in ``tracks``, reproject the current track point through ``reproject_funcs`` with the
+    image's pose (scipy quaternion of world2cam) and camera; keep z > 1e-7 and ||err|| <= threshold.
+    Returns (obs_info [n,2], track row [n], passing mask [n], errors [n])."""
+    from scipy.spatial.transform import Rotation
+    from . import projection_ref as PR
+    model = cameras[0].model_id.value
+    if model in (7, 10):
+        raise NotImplementedError
+    id2idx = {k: i for i, k in enumerate(tracks.keys())}
+    obs, rows = [], []
+    for k, o in tracks_orig.items():
+        if k in id2idx:
+            o = np.asarray(o).reshape(-1, 2)
+            obs.append(o)
+            rows.append(np.full(o.shape[0], id2idx[k]))
+    obs = np.concatenate(obs).astype(np.int64)
+    rows = np.concatenate(rows)
+    uv = np.array([images[i].features[f] for i, f in obs.tolist()], dtype=np.float64)
+    pp_idx = {0: [1, 2], 1: [2, 3], 2: [1, 2], 3: [1, 2], 8: [1, 2], 9: [1, 2]}.get(model, [2, 3])
+    cams = []
+    for im in images:
+        prm = np.asarray(cameras[im.cam_id].params, dtype=np.float64)
+        cams.append(np.concatenate([im.world2cam[:3, 3], Rotation.from_matrix(im.world2cam[:3, :3]).as_quat(), prm]))
+    cams = np.array(cams)
+    keep = [j for j in range(cams.shape[1]) if j - 7 not in pp_idx]
+    rowcam = cams[obs[:, 0]]
+    X = np.array([np.asarray(t.xyz, dtype=np.float64) for t in tracks.values()])[rows]
+    z = PR.rotate_quat(X, rowcam[:, :7])[:, 2]
+    err = np.linalg.norm(PR.reproject(model, X, rowcam[:, keep], rowcam[:, [7 + j for j in pp_idx]]) - uv, axis=-1)
+    return obs, rows, (err <= max_reproj_error) & (z > 1e-7), err

@@ -525,10 +525,68 @@ def gen_passes(out_dir):
     print("camera_models_golden.npz", len(cam_res), "arrays")
 
 
+def _retri_arrays(cameras, images, tracks, tracks_orig):
+    """Flat arrays of a retriangulation scene (rebuilt into scene objects by the tests)."""
+    feats = [np.asarray(im.features).reshape(-1, 2) for im in images]
+    return dict(
+        cam_model=np.array([c.model_id.value for c in cameras]), cam_params=np.stack([np.asarray(c.params) for c in cameras]),
+        img_cam=np.array([im.cam_id for im in images]), w2c=np.stack([im.world2cam for im in images]),
+        feat_ptr=np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])]), feats=np.concatenate(feats),
+        track_keys=np.array(list(tracks.keys())), track_xyz=np.stack([t.xyz for t in tracks.values()]),
+        track_ptr=np.concatenate([[0], np.cumsum([len(t.observations) for t in tracks.values()])]),
+        track_obs=np.concatenate([t.observations for t in tracks.values()]).astype(np.int64),
+        orig_keys=np.array(list(tracks_orig.keys())),
+        orig_ptr=np.concatenate([[0], np.cumsum([len(o) for o in tracks_orig.values()])]),
+        orig_obs=np.concatenate(list(tracks_orig.values())).astype(np.int64))
+
+
+def _to_ref_scene(cameras, images, tracks):
+    from instantsfm.scene.defs import Camera, CameraModelId, Image, Track
+    cams = [Camera(id=c.id, model_id=CameraModelId(c.model_id.value), width=c.width, height=c.height,
+                   params=np.asarray(c.params, dtype=np.float64)) for c in cameras]
+    ims = [Image(id=im.id, cam_id=im.cam_id, is_registered=im.is_registered, world2cam=im.world2cam.copy(),
+                 features=np.asarray(im.features).copy()) for im in images]
+    trs = {k: Track(id=t.id, xyz=t.xyz.copy(), observations=t.observations.copy()) for k, t in tracks.items()}
+    return cams, ims, trs
+
+
+def gen_retri(out_dir):
+    """RetriangulateTracks' passes: the reference's complete_tracks and FilterTracksByReprojection
+    on seeded scenes (SIMPLE_RADIAL; OPENCV; RADIAL_FISHEYE).  The points-only BA between them is TorchBA's LM
+    (parity-tested on its own)."""
+    import copy
+    sys.path.insert(0, REPO)
+    from instantsfm.processors.track_retriangulation import complete_tracks
+    from instantsfm.processors.track_filter import FilterTracksByReprojection
+    from instantsfm_amd.synth import make_retri_scene
+    opts = dict(complete_max_reproj_error=3.0)
+
+    def tracks_out(trs, prefix):
+        return {prefix + "keys": np.array(list(trs.keys())),
+                prefix + "ptr": np.concatenate([[0], np.cumsum([len(t.observations) for t in trs.values()])]),
+                prefix + "obs": np.concatenate([np.asarray(t.observations).reshape(-1, 2) for t in trs.values()]).astype(np.int64),
+                prefix + "dtype": np.array(str(np.asarray(next(iter(trs.values())).observations).dtype))}
+
+    for name, model, seed in (("retri_simple_radial", 2, 0), ("retri_opencv", 4, 1), ("retri_radial_fisheye", 9, 2)):
+        cameras, images, tracks, tracks_orig = make_retri_scene(model=model, seed=seed)
+        res = _retri_arrays(cameras, images, tracks, tracks_orig)
+        cams, ims, trs = _to_ref_scene(cameras, images, tracks)
+        n = complete_tracks(cams, ims, trs, copy.deepcopy(tracks_orig), opts)
+        res.update(tracks_out(trs, "complete_"))
+        res["complete_num"] = np.array(n)
+        for thr in (3.0, 0.8):
+            cams, ims, trs = _to_ref_scene(cameras, images, tracks)
+            cnt = FilterTracksByReprojection(cams, ims, trs, thr)
+            res.update(tracks_out(trs, f"filter_{thr:g}_"))
+            res[f"filter_{thr:g}_counter"] = np.array(cnt)
+        np.savez_compressed(os.path.join(out_dir, name + ".npz"), **res)
+        print(name + ".npz", "completed", n)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
-    ap.add_argument("--only", choices=("projection", "packing", "gp", "passes"), default=None)
+    ap.add_argument("--only", choices=("projection", "packing", "gp", "passes", "retri"), default=None)
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     with tempfile.TemporaryDirectory():
@@ -543,6 +601,8 @@ def main():
             gen_gp_packing(args.out, LM)
         if args.only in (None, "passes"):
             gen_passes(args.out)
+        if args.only in (None, "retri"):
+            gen_retri(args.out)
 
 
 if __name__ == "__main__":
