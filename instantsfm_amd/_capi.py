@@ -52,7 +52,7 @@ class Stats(ctypes.Structure):
                     coarse_used=self.coarse_used)
 
 
-# exported symbols (every one declared in include/insfm_ba.h, include/insfm_gp.h and include/insfm_passes.h)
+# exported symbols (every one declared in include/*.h)
 SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
@@ -60,7 +60,8 @@ SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_b
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
            "insfm_gp_debug_get_ds",
            "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
-           "insfm_filter_reproj_pixel", "insfm_reproj_candidates")
+           "insfm_filter_reproj_pixel", "insfm_reproj_candidates",
+           "insfm_tracks_establish")
 
 _lib = None
 
@@ -133,8 +134,11 @@ def load(path=LIB_PATH):
     L.insfm_filter_tri_angle.argtypes = [i64, vp, vp, vp, vp, f64, vp, vp]
     L.insfm_filter_reproj_pixel.argtypes = [i64, vp, vp, vp, vp, i32, vp, vp, vp, vp, vp, f64, vp, vp, vp]
     L.insfm_reproj_candidates.argtypes = [i64, i32, vp, vp, vp, vp, i32, vp, vp, vp, f64, vp, vp, vp]
-    for fn in ("insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
-               "insfm_filter_reproj_pixel", "insfm_reproj_candidates"):
+    L.insfm_tracks_establish.argtypes = [i64, vp, vp, i32, i64, vp, vp, f64, vp, vp, vp, vp, vp,
+                                         ctypes.POINTER(ctypes.c_int64), vp]
+    for fn in ("insfm_tracks_establish", "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
+               "insfm_filter_reproj_pixel", "insfm_reproj_candidates",
+           "insfm_tracks_establish"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

@@ -7,6 +7,8 @@ Restates the subset of ``instantsfm/scene/defs.py`` that ``TorchBA.Solve`` reads
 * ``get_camera_model_info`` -- defs.py:115-140 (focal / pp / k index maps)
 * ``Camera``              -- defs.py:142-237 (``model_id``, ``params``, ``set_params``)
 * ``Track``               -- defs.py:414-423 (``xyz``, ``observations`` [k,2] = (image_id, feature_id))
+* ``ConfigurationType``, ``ImagePair``, pair-id helpers, ``ViewGraph`` (pairs only) -- defs.py:41-97, 425-430: what
+  the COLMAP database reader produces and the track engine consumes
 
 The reference module imports cv2 for undistortion helpers that are off the BA path; this
 restatement has no cv2 dependency.
@@ -38,6 +40,73 @@ class Image:
 
     def center(self):
         return self.world2cam[:3, :3].T @ -self.world2cam[:3, 3]
+
+
+class ConfigurationType(Enum):
+    """defs.py:41-50 (COLMAP's TwoViewGeometry::ConfigurationType values)."""
+    UNDEFINED = 0
+    DEGENERATE = 1
+    CALIBRATED = 2
+    UNCALIBRATED = 3
+    PLANAR = 4
+    PANORAMIC = 5
+    PLANAR_OR_PANORAMIC = 6
+    WATERMARK = 7
+    MULTIPLE = 8
+
+
+class ImagePair:
+    """defs.py:52-86 (the fields; relative-pose helpers are off the path)."""
+
+    def __init__(self, image_id1: int = -1, image_id2: int = -1, is_valid: bool = True, weight: float = 0.0,
+                 E=None, F=None, H=None, rotation=None, translation=None, inliers=None,
+                 config: ConfigurationType = ConfigurationType.UNDEFINED):
+        self.image_id1 = image_id1
+        self.image_id2 = image_id2
+        self.is_valid = is_valid
+        self.weight = weight
+        self.E = E if E is not None else np.eye(3)
+        self.F = F if F is not None else np.eye(3)
+        self.H = H if H is not None else np.eye(3)
+        self.rotation = rotation if rotation is not None else np.array([1, 0, 0, 0])
+        self.translation = translation if translation is not None else np.zeros(3)
+        self.inliers = inliers if inliers is not None else []
+        self.config = config
+
+
+C_MAX_INT = 2 ** 31 - 1  # defs.py:88
+
+
+def PairId2Ids(pair_id):
+    """defs.py:89-90."""
+    return (pair_id % C_MAX_INT, pair_id // C_MAX_INT)
+
+
+def PairId2IdsInversed(pair_id):
+    """defs.py:92-93 (COLMAP's pair_id = id1 * (2^31 - 1) + id2)."""
+    return (pair_id // C_MAX_INT, pair_id % C_MAX_INT)
+
+
+def Ids2PairId(id1, id2):
+    """defs.py:95-96."""
+    return (id1 * C_MAX_INT + id2 if id1 < id2 else id2 * C_MAX_INT + id1)
+
+
+class ViewGraph:
+    """defs.py:425-430 plus establish_adjacency_list (:431-441)."""
+
+    def __init__(self):
+        self.image_pairs = {}  # pair_id -> ImagePair
+        self.num_images = 0
+        self.num_pairs = 0
+
+    def establish_adjacency_list(self):
+        self.adjacency_list = {}
+        for pair in self.image_pairs.values():
+            if not pair.is_valid:
+                continue
+            self.adjacency_list.setdefault(pair.image_id1, set()).add(pair.image_id2)
+            self.adjacency_list.setdefault(pair.image_id2, set()).add(pair.image_id1)
 
 
 class CameraModelId(Enum):

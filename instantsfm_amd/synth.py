@@ -353,3 +353,110 @@ def make_retri_scene(model=2, n_cams=20, n_points=600, seed=0, point_sigma=0.01,
             xyz = xyz + rng.normal(0, 3.0, 3)
         tracks[tid] = Track(id=tid, xyz=xyz, observations=t.observations[keep].copy(), is_initialized=True)
     return cameras, images, tracks, tracks_orig
+
+
+# ------------------------------------------------------------------------------------------------------------
+# COLMAP database scenes (ReadColmapDatabase + TrackEngine)
+# ------------------------------------------------------------------------------------------------------------
+def write_match_database(path, n_images=24, n_points=1500, track_len=6, window=5, seed=0, distractors=40,
+                         wrong_frac=0.03, dup_frac=0.03, bad_index_frac=0.002, kp_cols=6, feature_name="superpoint",
+                         min_common=12):
+    """Write a seeded COLMAP database.db (utils/database.py schema) of a ring of images looking at a point cloud.
+
+    Images get DB ids 1..n with one gap and share cameras (one per 3 images, SIMPLE_RADIAL, a third with a focal
+    prior); keypoints are the float32 projections of the points each image sees plus random distractors, shuffled
+    (``kp_cols`` columns like SIFT's affine shape; one image has no keypoints row).  Every image pair with at least
+    ``min_common`` common points gets a matches row (random order, ``wrong_frac`` random wrong matches, ``dup_frac``
+    near-duplicate features -- a second keypoint within 2 px matched to the same partner -- and a few out-of-range
+    indices) and a two_view_geometries row whose config is mostly valid (2, 3, 4) and sometimes invalid (0, 1, 7, 8);
+    one pair has NULL match data, one has matches but no geometry, some are stored with the larger image id first.
+    Returns the number of match rows written."""
+    from .utils.database import COLMAPDatabase
+    rng = np.random.default_rng(seed)
+    prob = make_problem(n_images, n_points, track_len=track_len, seed=seed, window=window)
+    C, P = prob.n_cams, prob.n_points
+    db = COLMAPDatabase.connect(path)
+    db.create_tables()
+    cam_ids = []
+    for c in range(0, C, 3):
+        f = float(prob.cams_gt[c, 7])
+        cam_ids.append(db.add_camera(2, 2000, 1500, [f, 1000.0, 750.0, float(prob.cams_gt[c, 8])],
+                                     prior_focal_length=(c // 3) % 3 == 0))
+    img_ids = [i + 1 + (1 if i >= n_images // 2 else 0) for i in range(C)]  # one gap in the ids
+    for i in range(C):
+        db.add_image(f"img_{i:04d}.jpg", cam_ids[i // 3], image_id=img_ids[i])
+    # features: projections (float32) + distractors, shuffled; near-duplicates of some observations
+    feat_of = {}
+    feats_per_img = []
+    no_kp = C // 3
+    for c in range(C):
+        sel = np.flatnonzero(prob.cam_idx == c)
+        pts = prob.pt_idx[sel]
+        xy = prob.uv[sel]
+        dup = rng.uniform(size=sel.size) < dup_frac
+        extra = rng.uniform([0, 0], [2000, 1500], (distractors, 2))
+        near = xy[dup] + rng.uniform(-1.4, 1.4, (int(dup.sum()), 2))
+        allxy = np.concatenate([xy, near, extra])
+        order = rng.permutation(allxy.shape[0])
+        inv = np.empty_like(order)
+        inv[order] = np.arange(order.size)
+        for k, p in enumerate(pts):
+            feat_of[(c, int(p))] = [int(inv[k])]
+        for j, k in enumerate(np.flatnonzero(dup)):
+            feat_of[(c, int(pts[k]))].append(int(inv[sel.size + j]))
+        kp = np.zeros((allxy.shape[0], kp_cols), np.float32)
+        kp[:, :2] = allxy[order]
+        if kp_cols > 2:
+            kp[:, 2:] = rng.normal(size=(allxy.shape[0], kp_cols - 2))
+        feats_per_img.append(kp.shape[0])
+        if c != no_kp:
+            db.add_keypoints(img_ids[c], kp)
+    seen = [set(prob.pt_idx[prob.cam_idx == c].tolist()) for c in range(C)]
+    n_rows = 0
+    pairs = [(i, j) for i in range(C) for j in range(i + 1, C) if len(seen[i] & seen[j]) >= min_common]
+    null_pair = pairs[len(pairs) // 2]
+    nogeo_pair = pairs[len(pairs) // 3]
+    for i, j in pairs:
+        common = sorted(seen[i] & seen[j])
+        m = []
+        for p in common:
+            fi, fj = feat_of[(i, p)], feat_of[(j, p)]
+            m.append((fi[0], fj[0]))
+            if len(fi) > 1:
+                m.append((fi[1], fj[0]))
+            if len(fj) > 1:
+                m.append((fi[0], fj[1]))
+        n_wrong = int(np.ceil(wrong_frac * len(m))) if rng.uniform() < 0.7 else 0
+        for _ in range(n_wrong):
+            m.append((int(rng.integers(0, feats_per_img[i])), int(rng.integers(0, feats_per_img[j]))))
+        m = np.array(m, dtype=np.int64)[rng.permutation(len(m))]
+        if rng.uniform() < 0.2:
+            k = max(1, int(bad_index_frac * len(m)))
+            rows = rng.choice(len(m), k, replace=False)
+            m[rows, rng.integers(0, 2)] = feats_per_img[i] + feats_per_img[j] + 5
+        a, b = (img_ids[i], img_ids[j]) if rng.uniform() < 0.8 else (img_ids[j], img_ids[i])
+        mm = m if a == img_ids[i] else m[:, ::-1]
+        if (i, j) == null_pair:
+            db.add_null_matches(a, b)
+        else:
+            db.add_matches(a, b, mm)
+        n_rows += 1
+        if (i, j) == nogeo_pair:
+            continue
+        u = rng.uniform()
+        config = 2 if u < 0.7 else 3 if u < 0.8 else 4 if u < 0.85 else int(rng.choice([0, 1, 7, 8]))
+        F = rng.normal(size=(3, 3))
+        db.add_two_view_geometry(a, b, mm, F=F, E=rng.normal(size=(3, 3)), H=rng.normal(size=(3, 3)), config=config)
+    if feature_name:
+        db.add_feature_name(feature_name)
+    db.commit()
+    db.close()
+    return n_rows
+
+
+def assign_inliers(view_graph, seed=0, frac=0.9):
+    """Seeded inlier subsets (the relative-pose stage's output, image_pair_inliers.py) for every pair, in order."""
+    for pair_id, pair in view_graph.image_pairs.items():
+        rng = np.random.default_rng([seed, pair_id % (2 ** 63)])
+        n = len(pair.matches)
+        pair.inliers = np.flatnonzero(rng.uniform(size=n) < frac)

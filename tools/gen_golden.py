@@ -583,10 +583,80 @@ def gen_retri(out_dir):
         print(name + ".npz", "completed", n)
 
 
+TRACK_DBS = {  # write_match_database() arguments of the golden databases
+    "tracks_db0": dict(n_images=24, n_points=1500, seed=0),
+    "tracks_db1": dict(n_images=30, n_points=2500, seed=1, kp_cols=2, feature_name=None, wrong_frac=0.08,
+                       dup_frac=0.06, distractors=10),
+}
+
+
+def gen_tracks(out_dir):
+    """COLMAP database reader + TrackEngine: databases written by the build's own writer
+    (instantsfm_amd.synth.write_match_database, the reference's schema), read by the reference's ReadColmapDatabase,
+    then the reference's TrackEngine.EstablishFullTracks / FindTracksForProblem on seeded inlier subsets.
+    The reference pins numpy 1.26 (pyproject.toml:17), where ``(image_id << 32) | np.uint32`` promotes to int64; under
+    this image's numpy 2 it overflows, so the captured pairs' matches are widened to int64 first (same values)."""
+    import contextlib
+    import io
+    import re
+    sys.path.insert(0, REPO)
+    from instantsfm.controllers.data_reader import ReadColmapDatabase
+    from instantsfm.processors.track_establishment import TrackEngine
+    from instantsfm_amd.synth import write_match_database, assign_inliers
+    for name, kw in TRACK_DBS.items():
+        with tempfile.TemporaryDirectory() as d:
+            path = os.path.join(d, "database.db")
+            write_match_database(path, **kw)
+            vg, cams, imgs, fname = ReadColmapDatabase(path)
+        res = dict(db_args=np.array(repr(kw)), feature_name=np.array(fname))
+        res["img_id"] = np.array([im.id for im in imgs])
+        res["img_cam"] = np.array([im.cam_id for im in imgs])
+        res["img_name"] = np.array([im.filename for im in imgs])
+        feats = [np.asarray(im.features).reshape(-1, 2) for im in imgs]
+        res["feat_ptr"] = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])])
+        res["feats"] = np.concatenate(feats).astype(np.float32)
+        res["cam_id"] = np.array([c.id for c in cams])
+        res["cam_model"] = np.array([c.model_id.value for c in cams])
+        res["cam_wh"] = np.array([[c.width, c.height] for c in cams])
+        res["cam_params"] = np.stack([np.asarray(c.params) for c in cams])
+        res["cam_prior"] = np.array([c.has_prior_focal_length for c in cams])
+        pairs = list(vg.image_pairs.items())
+        res["pair_key"] = np.array([k for k, _ in pairs], dtype=np.int64)
+        res["pair_ids"] = np.array([[p.image_id1, p.image_id2] for _, p in pairs])
+        res["pair_config"] = np.array([p.config.value for _, p in pairs])
+        res["pair_valid"] = np.array([p.is_valid for _, p in pairs])
+        res["pair_FEH"] = np.stack([np.stack([p.F, p.E, p.H]) for _, p in pairs])
+        res["pair_mptr"] = np.concatenate([[0], np.cumsum([len(p.matches) for _, p in pairs])])
+        res["pair_matches"] = np.concatenate([np.asarray(p.matches).reshape(-1, 2) for _, p in pairs]).astype(np.int64)
+        res["pair_mdtype"] = np.array(str(pairs[0][1].matches.dtype))
+        assign_inliers(vg, seed=kw["seed"])
+        for _, p in pairs:
+            p.matches = np.asarray(p.matches).astype(np.int64)
+        opts = dict(thres_inconsistency=10.0, min_num_view_per_track=3, max_num_view_per_track=9)
+        out = io.StringIO()
+        with contextlib.redirect_stdout(out):
+            eng = TrackEngine(vg, imgs)
+            full = eng.EstablishFullTracks(opts)
+        res["discarded"] = np.array(int(re.search(r"Discarded (\d+) features", out.getvalue()).group(1)))
+        res["full_keys"] = np.array([int(k) for k in full.keys()], dtype=np.int64)
+        res["full_ptr"] = np.concatenate([[0], np.cumsum([len(v) for v in full.values()])])
+        res["full_obs"] = np.concatenate(list(full.values())).astype(np.int64)
+        res["full_dtype"] = np.array(str(next(iter(full.values())).dtype))
+        for i, im in enumerate(imgs):
+            im.is_registered = (i % 5) != 2
+        res["registered"] = np.array([im.is_registered for im in imgs])
+        prob = eng.FindTracksForProblem(full, opts)
+        res["prob_keys"] = np.array([int(k) for k in prob.keys()], dtype=np.int64)
+        res["prob_ptr"] = np.concatenate([[0], np.cumsum([len(t.observations) for t in prob.values()])])
+        res["prob_obs"] = np.concatenate([t.observations for t in prob.values()]).astype(np.int64)
+        np.savez_compressed(os.path.join(out_dir, name + ".npz"), **res)
+        print(name + ".npz", len(full), "tracks,", int(res["discarded"]), "discarded,", len(pairs), "pairs")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
-    ap.add_argument("--only", choices=("projection", "packing", "gp", "passes", "retri"), default=None)
+    ap.add_argument("--only", choices=("projection", "packing", "gp", "passes", "retri", "tracks"), default=None)
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     with tempfile.TemporaryDirectory():
@@ -603,6 +673,8 @@ def main():
             gen_passes(args.out)
         if args.only in (None, "retri"):
             gen_retri(args.out)
+        if args.only in (None, "tracks"):
+            gen_tracks(args.out)
 
 
 if __name__ == "__main__":
