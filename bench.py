@@ -192,6 +192,251 @@ def run_gp(args):
         dist.destroy_process_group()
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return ""
+
+
+def run_tracks(args):
+    """Track establishment (TrackEngine.EstablishFullTracks, track_establishment.py:14-86) on a config-5-sized match
+    graph (500 images, ~8M inlier matches, synth.make_match_graph): matches/s of the device pipeline
+    (insfm_tracks_establish) with the flattened matches already in HBM; the end-to-end EstablishFullTracks time (host
+    flattening + device + building the reference's dict) is reported beside it.  N GPUs: independent replicas."""
+    import ctypes
+    import numpy as np
+    import torch
+    from instantsfm_amd import _capi
+    from instantsfm_amd.processors.track_establishment import TrackEngine, flatten_matches
+    from instantsfm_amd.synth import make_match_graph
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    vg, images = make_match_graph(seed=args.seed)
+    ea, eb, off, xy = flatten_matches(vg, images)
+    ne, nn = int(ea.shape[0]), int(off[-1])
+    node_img = np.repeat(np.arange(len(images), dtype=np.int32), np.diff(off))
+    d = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    t_img, t_xy, t_a, t_b = d(node_img, np.int32), d(xy, np.float32), d(ea, np.int32), d(eb, np.int32)
+    outs = [torch.empty(ne, dtype=torch.int32, device=dev), torch.empty(ne, dtype=torch.uint8, device=dev),
+            torch.empty(ne, dtype=torch.int32, device=dev), torch.empty(2 * ne, dtype=torch.int32, device=dev),
+            torch.empty(2 * ne, dtype=torch.int32, device=dev)]
+    counts = (ctypes.c_int64 * 2)()
+    L = _capi.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def call():
+        rc = L.insfm_tracks_establish(nn, p(t_img), p(t_xy), 1, ne, p(t_a), p(t_b), 10.0, *[p(o) for o in outs],
+                                      counts, stream)
+        if rc != 0:
+            raise RuntimeError(f"insfm_tracks_establish: {rc}")
+
+    for _ in range(args.warmup):
+        call()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        call()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    n_tracks, n_rows = int(counts[0]), int(counts[1])
+    avg_s = dt / args.steps
+    # compulsory bytes of one call: read the two edge arrays and every node's image and (float32) coordinates once,
+    # write the per-track and per-row outputs once
+    nbytes = 8 * ne + 12 * nn + 9 * n_tracks + 8 * n_rows
+    achieved = nbytes / avg_s / 1e9
+    t0 = time.perf_counter()
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        full = TrackEngine(vg, images, device=dev).EstablishFullTracks({'thres_inconsistency': 10.0})
+    e2e = time.perf_counter() - t0
+    out = {
+        "metric": "track establishment: inlier matches/s (TrackEngine.EstablishFullTracks core)",
+        "value": round(world * ne / dt * args.steps, 1), "unit": "matches/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(avg_s * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak" if world > 1 else "strong", "vs_baseline": None, "dtype": "int32",
+        "data": "synthetic (instantsfm_amd/synth.py make_match_graph)",
+        "config": {"workload": f"config-5-sized match graph: {len(images)} images / {nn} features / {len(vg.image_pairs)} "
+                               f"pairs / {ne} inlier matches -> {n_tracks} tracks", "images": len(images),
+                   "features": nn, "pairs": len(vg.image_pairs), "matches": ne, "tracks": n_tracks,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+        "tracks_kept": len(full), "end_to_end_s": round(e2e, 3),
+        "roofline": {"kernel": "insfm_tracks_establish (whole device pipeline, 15 launches incl. 2 radix sorts)",
+                     "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_us": round(avg_s * 1e6, 1), "algorithmic_bytes_per_launch": int(nbytes),
+                     "launches_per_run": args.steps},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle import tracks as OT
+        from instantsfm_amd.scene.defs import ViewGraph
+        sub = ViewGraph()
+        n = 0
+        for k, pair in vg.image_pairs.items():
+            sub.image_pairs[k] = pair
+            n += len(pair.inliers)
+            if n >= args.cpu_edges:
+                break
+        t0 = time.perf_counter()
+        OT.establish_full_tracks(sub, images, 10.0)
+        cdt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(n / cdt, 1), "unit": "matches/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle/tracks.py (the reference's TrackEngine restated loop for loop, "
+                                         f"pure Python) on the first {len(sub.image_pairs)} pairs = {n} matches, "
+                                         f"{cdt:.2f} s; CPU: {_cpu_model()}"}
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_passes(args):
+    """Between-round and retriangulation passes on the config-3 scene (1000 images,
+    200k tracks, 2M observations), inputs resident in HBM: one "step" = the six per-item kernels once each --
+    undistortion of every feature (UndistortImages), FilterTracksByReprojectionNormalized, FilterTracksByAngle,
+    FilterTracksTriangulationAngle, FilterTracksByReprojection (pixel) and complete_tracks' candidate test.
+    value = observations / s through the whole set; per-kernel device times from HIP events on the library stream."""
+    import ctypes
+    import numpy as np
+    import torch
+    from scipy.spatial.transform import Rotation
+    from instantsfm_amd import _capi
+    from instantsfm_amd.synth import make_config, full_params, quat_to_matrix
+
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    prob = make_config(3, seed=args.seed)
+    C, P, N = prob.n_cams, prob.n_points, prob.n_obs
+    w2c = np.tile(np.eye(4), (C, 1, 1))
+    for c in range(C):
+        w2c[c, :3, :3] = quat_to_matrix(prob.cams_gt[c, 3:7])
+        w2c[c, :3, 3] = prob.cams_gt[c, :3]
+    params = np.zeros((C, 12))
+    params[:, :4] = np.stack([full_params(2, prob.cams_gt[c, 7:], prob.pp[c]) for c in range(C)])
+    feats = prob.uv.astype(np.float32)
+    pc = np.einsum('nij,nj->ni', w2c[prob.cam_idx, :3, :3], prob.points_gt[prob.pt_idx]) + w2c[prob.cam_idx, :3, 3]
+    rays = pc / np.linalg.norm(pc, axis=1, keepdims=True)
+    centers = -np.einsum('cji,cj->ci', w2c[:, :3, :3], w2c[:, :3, 3])
+    rows = np.concatenate([w2c[:, :3, 3], Rotation.from_matrix(w2c[:, :3, :3]).as_quat(), prob.cams_gt[:, 7:]], 1)
+    d = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else np.asarray(a, dt))).to(dev)  # noqa
+    t = dict(img=d(prob.cam_idx, np.int32), trk=d(prob.pt_idx, np.int32), row=d(np.arange(N), np.int64),
+             cam=d(np.zeros(C) + np.arange(C), np.int32), model=d(np.full(C, 2), np.int32), params=d(params),
+             feats=d(feats), w2c=d(w2c.reshape(C, 16)), xyz=d(prob.points_gt), rays=d(rays), centers=d(centers),
+             ptr=d(np.arange(0, N + 1, 10), np.int64), rows=d(rows), pps=d(prob.pp),
+             valid=torch.empty(N, dtype=torch.uint8, device=dev), out=torch.empty((N, 3), dtype=torch.float64, device=dev))
+    L = _capi.load()
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    p = lambda k: ctypes.c_void_p(t[k].data_ptr())  # noqa: E731
+    calls = {
+        "k_undistort": (lambda: L.insfm_undistort(N, p("feats"), 1, p("img"), p("model"), p("params"), p("out"), stream),
+                        N * (8 + 4 + 24)),
+        "k_filter_reproj": (lambda: L.insfm_filter_reproj_normalized(N, p("img"), p("trk"), p("row"), p("w2c"), p("xyz"),
+                                                                     p("rays"), 1e-2, p("valid"), None, stream),
+                            N * 65),
+        "k_filter_angle": (lambda: L.insfm_filter_angle(N, p("img"), p("trk"), p("row"), p("w2c"), p("xyz"), p("rays"),
+                                                        0.99985, p("valid"), stream), N * 65),
+        "k_filter_tri_angle": (lambda: L.insfm_filter_tri_angle(P, p("ptr"), p("img"), p("centers"), p("xyz"), 0.99966,
+                                                                p("valid"), stream), P * (8 + 24 + 1) + N * 4),
+        "k_filter_reproj_pixel": (lambda: L.insfm_filter_reproj_pixel(N, p("img"), p("trk"), p("row"), p("feats"), 1,
+                                                                      p("cam"), p("model"), p("params"), p("w2c"),
+                                                                      p("xyz"), 3.0, p("valid"), None, stream), N * 49),
+        "k_reproj_candidates": (lambda: L.insfm_reproj_candidates(N, 2, p("img"), p("trk"), p("row"), p("feats"), 1,
+                                                                  p("rows"), p("pps"), p("xyz"), 3.0, p("valid"), None,
+                                                                  stream), N * 49),
+    }
+    for fn, _ in calls.values():
+        for _ in range(max(args.warmup, 1)):
+            if fn() != 0:
+                raise RuntimeError("pass kernel failed")
+    torch.cuda.synchronize(dev)
+    kern = {}
+    for name, (fn, nbytes) in calls.items():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / args.steps
+        kern[name] = dict(avg_launch_us=round(us, 2), algorithmic_bytes_per_launch=int(nbytes),
+                          achieved_gbs=round(nbytes / (us * 1e-6) / 1e9, 1))
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for fn, _ in calls.values():
+            fn()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    name = max(kern, key=lambda k: kern[k]["avg_launch_us"])
+    kk = kern[name]
+    out = {
+        "metric": "between-round + retriangulation passes: observations/s (6 per-item kernels per step)",
+        "value": round(N * args.steps / dt, 1), "unit": "obs/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (config-3 scene, instantsfm_amd/synth.py; float32 features as a database holds them)",
+        "config": {"workload": f"config 3 scene: {C} images / {P} tracks / {N} observations, one pass of each filter",
+                   "images": C, "tracks": P, "obs": N, "parallelism": "single GPU"},
+        "kernel_us": {k: v["avg_launch_us"] for k, v in kern.items()}, "kernels": kern,
+        "roofline": {"kernel": name, "bound": "hbm", "achieved": kk["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(kk["achieved_gbs"] / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_us": kk["avg_launch_us"], "algorithmic_bytes_per_launch": kk["algorithmic_bytes_per_launch"],
+                     "launches_per_run": args.steps,
+                     "timing": "torch.cuda.Event on the current stream, which the library launches on"},
+    }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_passes(args.seed)
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_passes(seed):
+    """The oracle restatements of the six passes (oracle/passes.py; numpy where the reference is numpy, its Python
+    loops where it loops) on a 400-image / 40k-track / 400k-observation sample of the same generator."""
+    import copy
+    import numpy as np
+    from oracle import passes as OP
+    from instantsfm_amd.synth import make_problem, to_scene
+    prob = make_problem(400, 40000, seed=seed)
+    cameras, images, tracks = to_scene(prob, use_init=False, image_features_dtype=np.float32)
+    t0 = time.perf_counter()
+    for c, im in enumerate(images):
+        im.features_undist = OP.undistort_rays(2, cameras[c].params, im.features)
+    OP.filter_reproj_normalized(images, tracks, 1e-2)
+    OP.filter_angle(images, tracks, 1.0)
+    OP.filter_tri_angle(images, tracks, 1.5)
+    OP.filter_reproj_pixel(cameras, images, tracks, 3.0)
+    OP.complete_candidates(cameras, images, tracks, {k: t.observations for k, t in tracks.items()}, 3.0)
+    dt = time.perf_counter() - t0
+    return {"value": round(prob.n_obs / dt, 1), "unit": "obs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/passes.py restatements of the six passes on a 400-image / 40000-track / {prob.n_obs}-obs "
+                      f"scene of the same generator, {dt:.2f} s; CPU: {_cpu_model()}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,10 +448,15 @@ def main():
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
-    ap.add_argument("--path", choices=("ba", "gp"), default="ba")
+    ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes"), default="ba")
+    ap.add_argument("--cpu-edges", type=int, default=1_500_000, help="--path tracks: matches in the CPU sample")
     args = ap.parse_args()
     if args.path == "gp":
         return run_gp(args)
+    if args.path == "tracks":
+        return run_tracks(args)
+    if args.path == "passes":
+        return run_passes(args)
 
     import numpy as np
     import torch
