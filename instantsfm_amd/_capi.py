@@ -72,11 +72,13 @@ class BAError(RuntimeError):
         self.code = code
 
 
-def load(path=LIB_PATH):
-    """Load the HIP library (no GPU needed to load it).  Raises if it was not built."""
+def load(path=None):
+    """Load the HIP library (no GPU needed to load it).  Raises if it was not built.  ``INSFM_LIB`` names another
+    build of the same library (tools/schur_variants.sh compiles kernel variants for timing)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("INSFM_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
     L = ctypes.CDLL(path)

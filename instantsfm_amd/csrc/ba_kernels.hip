@@ -41,6 +41,9 @@ constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgr
 #define INSFM_SCHUR_WAVES 8
 #endif
 constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (non-deterministic mode)
+#ifndef SCHUR_MINW
+#define SCHUR_MINW 1  // k_schur launch bound: minimum waves per SIMD (caps VGPRs: 4 -> 128)
+#endif
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
@@ -274,7 +277,7 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
 }
 
 template <int D, int WAVES, bool GPW = false>
-__global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
+__global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
                                                       const int* __restrict__ pt_ptr, const int* __restrict__ ustart,
@@ -324,23 +327,35 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
             const int en = e + WAVES * NG;
             if (active && en < oe) dnext = sdesc[en];
         }
-        int qs = 0, qe = 0;
+        constexpr int UP = SCHUR_UP;  // partners in flight per group
+        const int qs = has ? dcur.z : 0, qe = has ? dcur.w : 0;
+        const int n = qe - qs;
+        // issue order = wait order (vmcnt retires in order): the own record first, then the first UP partner records,
+        // so the W^ staging waits only for the own record while the partner loads stay in flight
+        double w0 = 0.0, w1 = 0.0, w2 = 0.0, v00 = 0.0, v01 = 0.0, v02 = 0.0, v11 = 0.0, v12 = 0.0, v22 = 0.0;
         if (has) {
-            const int o = dcur.x;
-            const int p = dcur.y;
-            const double* vi = Vinv + 6 * (size_t)p;
-            const double v00 = vi[0], v01 = vi[1], v02 = vi[2], v11 = vi[3], v12 = vi[4], v22 = vi[5];
-            double w0, w1, w2;
-            load_wcol<D, GPW>(W, o, cb, w0, w1, w2);
+            const double* vi = Vinv + 6 * (size_t)dcur.y;
+            v00 = vi[0]; v01 = vi[1]; v02 = vi[2]; v11 = vi[3]; v12 = vi[4]; v22 = vi[5];
+            load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
+        }
+        double x[UP][3];
+        int cj[UP];
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+            cj[u] = -1;
+            if (u < n) {
+                load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
+                cj[u] = cam[qs + u];
+            }
+        }
+        if (has) {
             my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
             my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
             my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
             if (diag_chunk) {
-                const double* yp = y + 3 * (size_t)p;
+                const double* yp = y + 3 * (size_t)dcur.y;
                 breg -= w0 * yp[0] + w1 * yp[1] + w2 * yp[2];
             }
-            qs = dcur.z;
-            qe = dcur.w;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -354,21 +369,19 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur(const int4* __restrict__ w
                 wh[a2][2] = my_wh[a2 * 4 + 2];
             }
         }
-        const int n = qe - qs;
         int nmax = n;
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-        constexpr int UP = SCHUR_UP;  // partners in flight per group
         for (int k0 = 0; k0 < nmax; k0 += UP) {
-            double x[UP][3];
-            int cj[UP];
+            if (k0 > 0) {
 #pragma unroll
-            for (int u = 0; u < UP; ++u) {
-                cj[u] = -1;
-                if (k0 + u < n) {
-                    const int q = qs + k0 + u;
-                    load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
-                    cj[u] = cam[q];
+                for (int u = 0; u < UP; ++u) {
+                    cj[u] = -1;
+                    if (k0 + u < n) {
+                        const int q = qs + k0 + u;
+                        load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
+                        cj[u] = cam[q];
+                    }
                 }
             }
 #pragma unroll
