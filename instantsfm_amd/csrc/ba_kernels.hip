@@ -1342,7 +1342,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         int it = 0;
         int* st = reinterpret_cast<int*>(h->host_res + 8);
         for (;;) {
-            const int chunk = (it == 0) ? std::max(8, h->last_cg_iters + 2) : 8;
+            // the count grows by a few iterations per LM step as the damping drops: launch past the last count so most
+            // solves need one host poll (a converged iteration costs ~1 us per launch: its kernels exit at the flag)
+            const int chunk = (it == 0) ? std::max(8, h->last_cg_iters + 6) : 8;
             const int stop = std::min(it + chunk, maxit + 2);
             const int first = it;
             rec(h, 8);

@@ -499,6 +499,19 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_update(int it, int C, int max
         pr = cg.r[0][idx0];
         if (it > 0) { pu = tl.u[idx0]; pp = cg.p[idx0]; pw = cg.w[0][idx0]; ps = cg.s[0][idx0]; px = cg.x[idx0]; }
     }
+    // the first pass's L row and Z~ column depend only on the cluster's rows: in flight before the barriers too
+    double Lp[D], Zp[D];
+    if (on0) {
+        const double* L = Lf + idx0 * D;  // row a of L_row (idx0 = row * D + a)
+#pragma unroll
+        for (int k = 0; k < D; ++k) Lp[k] = (k <= a) ? L[k] : 0.0;
+    }
+    const bool zon = t < RPW * MC && t / MC < ne;
+    if (zon) {
+        const double* Z = tl.Zt + (size_t)tl.cl_cams[e0 + t / MC] * D * MC + t % MC;
+#pragma unroll
+        for (int aa = 0; aa < D; ++aa) Zp[aa] = Z[aa * MC];
+    }
     double al = 0.0, be = 0.0;
     if (it > 0) {
         const int i = it - 1;
@@ -570,22 +583,32 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_update(int it, int C, int max
         }
         __syncthreads();
         if (on) {
-            const double* L = Lf + (size_t)row * D * D + a * D;
             double lr = 0.0;
+            if (pass == 0) {
 #pragma unroll
-            for (int k = 0; k < D; ++k)
-                if (k <= a) lr += L[k] * rl[rloc * D + k];
+                for (int k = 0; k < D; ++k)
+                    if (k <= a) lr += Lp[k] * rl[rloc * D + k];
+            } else {
+                const double* L = Lf + (size_t)row * D * D + a * D;
+#pragma unroll
+                for (int k = 0; k < D; ++k)
+                    if (k <= a) lr += L[k] * rl[rloc * D + k];
+            }
             lq[rloc * D + a] = lr * lr;
         }
         __syncthreads();
         for (int e = t; e < RPW * MC; e += kCgThreads) {
             const int rr = e / MC, k = e % MC, mj = pass * RPW + rr;
             if (mj < ne) {
-                const int row2 = tl.cl_cams[e0 + mj];
-                const double* Z = tl.Zt + (size_t)row2 * D * MC + k;
                 double v = 0.0;
+                if (pass == 0 && e == t) {
 #pragma unroll
-                for (int aa = 0; aa < D; ++aa) v += Z[aa * MC] * rl[rr * D + aa];
+                    for (int aa = 0; aa < D; ++aa) v += Zp[aa] * rl[rr * D + aa];
+                } else {
+                    const double* Z = tl.Zt + (size_t)tl.cl_cams[e0 + mj] * D * MC + k;
+#pragma unroll
+                    for (int aa = 0; aa < D; ++aa) v += Z[aa * MC] * rl[rr * D + aa];
+                }
                 Rm[mj * MC + k] = v;
                 if (k == 0) {
                     double s2 = 0.0;
@@ -618,25 +641,54 @@ __global__ __launch_bounds__(kThreads) void k_tl_coarse(CgBufs cg, TlBufs tl, co
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c = blockIdx.x, m = tl.m;
     const bool use = tl.ok[0] != 0;
+    const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
+    // this thread's first row entry (r and its Z~ row) is independent of y: loaded together with E^-1 and R
+    const bool pon = t < ne * D;
+    size_t pidx = 0;
+    double rp = 0.0, Zq[MC];
+    if (pon) {
+        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;
+        rp = cg.r[0][pidx];
+        if (use) {
+#pragma unroll
+            for (int k = 0; k < MC; ++k) Zq[k] = tl.Zt[pidx * MC + k];
+        }
+    }
     if (use) {
-        for (int k = wv; k < MC; k += kWaves) {
-            const double* Er = Einv + (size_t)(c * MC + k) * m;
-            double s = 0.0;
-            for (int l = lane; l < m; l += 64) s += Er[l] * tl.Rc[l];
-            s = wave_sum(s);
-            if (lane == 0) y[k] = s;
+        // a wave's rows of E^-1 are read together (every load of the wave in flight at once), each row's dot in the
+        // same lane order as a row-at-a-time loop
+        constexpr int KPW = (MC + kWaves - 1) / kWaves, LPL = (kCoarseMax + 63) / 64;
+        double s[KPW];
+#pragma unroll
+        for (int kk = 0; kk < KPW; ++kk) s[kk] = 0.0;
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) {
+            const int l = lane + 64 * q;
+            if (l < m) {
+                const double rl = tl.Rc[l];
+#pragma unroll
+                for (int kk = 0; kk < KPW; ++kk) {
+                    const int k = wv + kk * kWaves;
+                    if (k < MC) s[kk] += Einv[(size_t)(c * MC + k) * m + l] * rl;
+                }
+            }
+        }
+#pragma unroll
+        for (int kk = 0; kk < KPW; ++kk) {
+            const int k = wv + kk * kWaves;
+            const double v = wave_sum(s[kk]);
+            if (lane == 0 && k < MC) y[k] = v;
         }
         __syncthreads();
     }
-    const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
     for (int e = t; e < ne * D; e += kThreads) {
-        const int i = tl.cl_cams[e0 + e / D], a = e % D;
-        const size_t idx = (size_t)i * D + a;
-        double v = cg.r[0][idx];
+        const bool first = e == t;
+        const size_t idx = first ? pidx : (size_t)tl.cl_cams[e0 + e / D] * D + e % D;
+        double v = first ? rp : cg.r[0][idx];
         if (use) {
             const double* Z = tl.Zt + idx * MC;
 #pragma unroll
-            for (int k = 0; k < MC; ++k) v += Z[k] * y[k];
+            for (int k = 0; k < MC; ++k) v += (first ? Zq[k] : Z[k]) * y[k];
         }
         tl.u[idx] = v;
     }
