@@ -52,21 +52,21 @@ constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (
 // reductions
 // ------------------------------------------------------------------------------------------------------------
 // Fixed-order block reduction of NV values per thread; result valid in thread 0 (and returned to all).
-template <int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= kThreads*NV doubles */) {
+template <int NV, int NT = kThreads>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= NT*NV doubles */) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) sh[k * kThreads + t] = v[k];
+    for (int k = 0; k < NV; ++k) sh[k * NT + t] = v[k];
     __syncthreads();
-    for (int s = kThreads / 2; s >= 1; s >>= 1) {
+    for (int s = NT / 2; s >= 1; s >>= 1) {
         if (t < s) {
 #pragma unroll
-            for (int k = 0; k < NV; ++k) sh[k * kThreads + t] += sh[k * kThreads + t + s];
+            for (int k = 0; k < NV; ++k) sh[k * NT + t] += sh[k * NT + t + s];
         }
         __syncthreads();
     }
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = sh[k * kThreads];
+    for (int k = 0; k < NV; ++k) v[k] = sh[k * NT];
     __syncthreads();
 }
 
@@ -93,63 +93,95 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // ------------------------------------------------------------------------------------------------------------
 // linearization
 // ------------------------------------------------------------------------------------------------------------
-// One thread per (local) track: every observation's weighted J gives W_o = J~c^T J~p (stored [o][3][D]: a group of D
-// lanes reads each column of W_o as one contiguous segment in k_schur); the track
-// reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~ in registers.
+// Every observation's weighted J gives W_o = J~c^T J~p (stored [o][3][D]: a group of D lanes reads each column of W_o
+// as one contiguous segment in k_schur); each track reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~.
+constexpr int kLinThreads = 128;  // k_lin_points workgroup (LDS: W staging + V/g terms of its observations)
+
 template <int M>
-__global__ __launch_bounds__(kThreads) void k_lin_points(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+__global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
+                                                         const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
                                                          double delta, double* __restrict__ W, double* __restrict__ V,
                                                          double* __restrict__ gp) {
-    constexpr int D = kD<M>, ST = kStride<M>;
-    const int p = blockIdx.x * kThreads + threadIdx.x;
-    if (p >= Pl) return;
-    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+    // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
+    // is longer), one thread per observation: coalesced uv / cam / point loads and 192-B W records written by
+    // consecutive lanes.  Each observation's V / g_p terms go to LDS and one thread per track adds them in observation
+    // order -- the same sequence of additions as a thread walking its track.
+    constexpr int D = kD<M>, ST = kStride<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride: no bank conflicts
+    __shared__ double ct[kLinThreads][9];
+    __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here
+    const int t = threadIdx.x;
+    const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
+    const int ob = pt_ptr[tb], oe = pt_ptr[te];
     double Vs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-    const int ob = pt_ptr[p], oe = pt_ptr[p + 1];
-    for (int o = ob; o < oe; ++o) {
-        const int c = cam[o];
-        const double2 z = reinterpret_cast<const double2*>(uv)[o];
-        const double uvo[2] = {z.x, z.y};
-        const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
-        double r[2], Jc[2][D], Jp[2][3];
-        eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
-        const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
-        r[0] *= sw; r[1] *= sw;
+    const int tr = tb + t;  // the track this thread sums (tracks of the run)
+    for (int base = ob; base < oe; base += kLinThreads) {
+        const int o = base + t;
+        if (o < oe) {
+            const int c = cam[o], p = ptl[o];
+            const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+            const double2 z = reinterpret_cast<const double2*>(uv)[o];
+            const double uvo[2] = {z.x, z.y};
+            const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+            double r[2], Jc[2][D], Jp[2][3];
+            eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
+            const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+            r[0] *= sw; r[1] *= sw;
 #pragma unroll
-        for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
+            for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
 #pragma unroll
-        for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
-        double* Wo = W + (size_t)o * D * 3;
+            for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
+            double* Wo = wst + (size_t)t * WRP;
 #pragma unroll
-        for (int a = 0; a < D; ++a)
+            for (int a = 0; a < D; ++a)
 #pragma unroll
-            for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
-        Vs[0] += Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
-        Vs[1] += Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
-        Vs[2] += Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
-        Vs[3] += Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
-        Vs[4] += Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
-        Vs[5] += Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+                for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+            ct[t][0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
+            ct[t][1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
+            ct[t][2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
+            ct[t][3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
+            ct[t][4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
+            ct[t][5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) g[k] -= Jp[0][k] * r[0] + Jp[1][k] * r[1];
+            for (int k = 0; k < 3; ++k) ct[t][6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
+        }
+        __syncthreads();
+        {   // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive doubles
+            const int n = min(kLinThreads, oe - base);
+            double* dst = W + (size_t)base * WR;
+            for (int k = t; k < n * WR; k += kLinThreads) dst[k] = wst[(k / WR) * WRP + k % WR];
+        }
+        if (tr < te) {
+            const int lo = max(pt_ptr[tr], base), hi = min(pt_ptr[tr + 1], base + kLinThreads);
+            for (int q = lo; q < hi; ++q) {
+                const double* cq = ct[q - base];
+#pragma unroll
+                for (int k = 0; k < 6; ++k) Vs[k] += cq[k];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[k] -= cq[6 + k];
+            }
+        }
+        __syncthreads();
     }
+    if (tr < te) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) V[6 * (size_t)p + k] = Vs[k];
+        for (int k = 0; k < 6; ++k) V[6 * (size_t)tr + k] = Vs[k];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) gp[3 * (size_t)p + k] = g[k];
+        for (int k = 0; k < 3; ++k) gp[3 * (size_t)tr + k] = g[k];
+    }
 }
 
 // One workgroup per camera: 256 observations at a time are evaluated (one per thread) into an LDS batch
 // [obs][J~c row0 | J~c row1 | r~0 r~1]; then thread e owns entry e of [U (DxD) | g_c (D)] and sums the batch in
-// observation order (the oracle's order).
+// observation order (the oracle's order).  The camera-major point index and uv of each observation (cm_pt, cm_uv,
+// built at create) are read coalesced; the next batch's point is fetched while the current batch is reduced and
+// the indices two batches ahead, so no batch waits on a dependent load chain.
 template <int M>
-__global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ cam_ptr, const int* __restrict__ cam_obs,
-                                                       const int* __restrict__ ptl, const double* __restrict__ uv,
-                                                       const double* __restrict__ pp, const double* __restrict__ cams,
-                                                       const double* __restrict__ pts, double delta, double* __restrict__ U,
-                                                       double* __restrict__ gc) {
+__global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ cam_ptr, const int* __restrict__ cm_pt,
+                                                       const double* __restrict__ cm_uv, const double* __restrict__ pp,
+                                                       const double* __restrict__ cams, const double* __restrict__ pts,
+                                                       double delta, double* __restrict__ U, double* __restrict__ gc) {
     constexpr int D = kD<M>, ST = kStride<M>;
     constexpr int RW = 2 * D + 2;
     constexpr int E = D * D + D;
@@ -157,6 +189,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ c
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int c = blockIdx.x, t = threadIdx.x;
     const int eb = cam_ptr[c], ee = cam_ptr[c + 1];
+    const double2* uv2 = reinterpret_cast<const double2*>(cm_uv);
     double camv[ST];
 #pragma unroll
     for (int k = 0; k < ST; ++k) camv[k] = cams[(size_t)c * ST + k];
@@ -164,14 +197,27 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ c
     double acc[EPT];
 #pragma unroll
     for (int m = 0; m < EPT; ++m) acc[m] = 0.0;
+    // pipeline registers: current batch (X, z), next batch (pn, zn), two ahead (pnn, znn)
+    double X[3] = {0.0, 0.0, 0.0};
+    double2 z = make_double2(0.0, 0.0), zn = z, znn = z;
+    int pn = 0, pnn = 0;
+    {
+        const int e0 = eb + t, e1 = e0 + kThreads;
+        if (e0 < ee) {
+            const int p0 = cm_pt[e0];
+            z = uv2[e0];
+            X[0] = pts[3 * (size_t)p0]; X[1] = pts[3 * (size_t)p0 + 1]; X[2] = pts[3 * (size_t)p0 + 2];
+        }
+        if (e1 < ee) { pn = cm_pt[e1]; zn = uv2[e1]; }
+    }
     for (int base = eb; base < ee; base += kThreads) {
         const int e = base + t;
+        const bool has = e < ee, hn = e + kThreads < ee, hnn = e + 2 * kThreads < ee;
+        double Xn[3] = {0.0, 0.0, 0.0};
+        if (hn) { Xn[0] = pts[3 * (size_t)pn]; Xn[1] = pts[3 * (size_t)pn + 1]; Xn[2] = pts[3 * (size_t)pn + 2]; }
+        if (hnn) { pnn = cm_pt[e + 2 * kThreads]; znn = uv2[e + 2 * kThreads]; }
         double* row = sh + (size_t)t * RW;
-        if (e < ee) {
-            const int o = cam_obs[e];
-            const int p = ptl[o];
-            const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
-            const double2 z = reinterpret_cast<const double2*>(uv)[o];
+        if (has) {
             const double uvo[2] = {z.x, z.y};
             double r[2], Jc[2][D], Jp[2][3];
             eval_obs<M, true>(camv, X, ppc, uvo, r, Jc, Jp);
@@ -205,6 +251,8 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ c
             }
         }
         __syncthreads();
+        X[0] = Xn[0]; X[1] = Xn[1]; X[2] = Xn[2];
+        z = zn; pn = pnn; zn = znn;
     }
 #pragma unroll
     for (int m = 0; m < EPT; ++m) {
@@ -766,22 +814,55 @@ __global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __r
 // back-substitution, parameter update, cost
 // ------------------------------------------------------------------------------------------------------------
 // dp = V^-1 (g_p - sum_o W_o^T dc_c(o)); trial points; gain part  2 t.dp - dp^T V dp  (block partial).
+// dp = V^-1 (g_p - sum_o W_o^T dc_cam(o)) per track, trial points, gain part 2 g_p.dp - dp^T V dp.  Same runs of whole
+// tracks as k_lin_points.  Per chunk of the run's observations: the W records (contiguous in HBM) are copied to LDS by
+// consecutive lanes and every thread loads its observation's camera step; thread o forms q_o = W_o^T dc (a = 0..D-1 in
+// order) from LDS, and one thread per track subtracts its q_o in observation order -- the arithmetic of a thread
+// walking its track, without a dependent global load per observation.
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_backsub(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
-                                                      const double* __restrict__ W, const double* __restrict__ dc,
-                                                      const double* __restrict__ V, const double* __restrict__ Vinv,
-                                                      const double* __restrict__ gp, const double* __restrict__ pts,
-                                                      double* __restrict__ dp, double* __restrict__ pts_new,
-                                                      double* __restrict__ part) {
-    __shared__ double red[kThreads];
-    const int p = blockIdx.x * kThreads + threadIdx.x;
+__global__ __launch_bounds__(kLinThreads) void k_backsub(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
+                                                         const int* __restrict__ cam, const double* __restrict__ W,
+                                                         const double* __restrict__ dc, const double* __restrict__ V,
+                                                         const double* __restrict__ Vinv, const double* __restrict__ gp,
+                                                         const double* __restrict__ pts, double* __restrict__ dp,
+                                                         double* __restrict__ pts_new, double* __restrict__ part) {
+    constexpr int WR = 3 * D, WRP = WR | 1;
+    __shared__ double red[kLinThreads];
+    __shared__ double wst[kLinThreads * WRP];
+    __shared__ double q[kLinThreads][3];
+    const int t = threadIdx.x;
+    const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
+    const int p = tb + t;
+    const bool own = p < te;
     double gain[1] = {0.0};
-    if (p < Pl) {
-        double t0 = gp[3 * (size_t)p], t1 = gp[3 * (size_t)p + 1], t2 = gp[3 * (size_t)p + 2];
-        if (dc) {
-            for (int o = pt_ptr[p]; o < pt_ptr[p + 1]; ++o) {
-                const double* Wo = W + (size_t)o * D * 3;
-                const double* d = dc + (size_t)cam[o] * D;
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+    if (own) { t0 = gp[3 * (size_t)p]; t1 = gp[3 * (size_t)p + 1]; t2 = gp[3 * (size_t)p + 2]; }
+    if (dc) {
+        const int ob = pt_ptr[tb], oe = pt_ptr[te];
+        const int lo = own ? pt_ptr[p] : 0, hi = own ? pt_ptr[p + 1] : 0;
+        for (int base = ob; base < oe; base += kLinThreads) {
+            const int n = min(kLinThreads, oe - base);
+            const double* src = W + (size_t)base * WR;
+            double buf[WR];  // thread t holds doubles t, t + kLinThreads, ... of the chunk: every load issued first
+#pragma unroll
+            for (int j = 0; j < WR; ++j) {
+                const int k = t + j * kLinThreads;
+                if (k < n * WR) buf[j] = src[k];
+            }
+#pragma unroll
+            for (int j = 0; j < WR; ++j) {
+                const int k = t + j * kLinThreads;
+                if (k < n * WR) wst[(k / WR) * WRP + k % WR] = buf[j];
+            }
+            double d[D];
+            if (t < n) {
+                const double* dr = dc + (size_t)cam[base + t] * D;
+#pragma unroll
+                for (int a = 0; a < D; ++a) d[a] = dr[a];
+            }
+            __syncthreads();
+            if (t < n) {
+                const double* Wo = wst + (size_t)t * WRP;
                 double s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
                 for (int a = 0; a < D; ++a) {
@@ -789,9 +870,16 @@ __global__ __launch_bounds__(kThreads) void k_backsub(int Pl, const int* __restr
                     s1 += Wo[D + a] * d[a];
                     s2 += Wo[2 * D + a] * d[a];
                 }
-                t0 -= s0; t1 -= s1; t2 -= s2;
+                q[t][0] = s0; q[t][1] = s1; q[t][2] = s2;
             }
+            __syncthreads();
+            for (int o = max(lo, base); o < min(hi, base + n); ++o) {
+                t0 -= q[o - base][0]; t1 -= q[o - base][1]; t2 -= q[o - base][2];
+            }
+            __syncthreads();
         }
+    }
+    if (own) {
         const double* vi = Vinv + 6 * (size_t)p;
         const double d0 = vi[0] * t0 + vi[1] * t1 + vi[2] * t2;
         const double d1 = vi[1] * t0 + vi[3] * t1 + vi[4] * t2;
@@ -806,7 +894,7 @@ __global__ __launch_bounds__(kThreads) void k_backsub(int Pl, const int* __restr
         const double Vd2 = v[2] * d0 + v[4] * d1 + v[5] * d2;
         gain[0] = 2.0 * (t0 * d0 + t1 * d1 + t2 * d2) - (d0 * Vd0 + d1 * Vd1 + d2 * Vd2);
     }
-    block_sum<1>(gain, red);
+    block_sum<1, kLinThreads>(gain, red);
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
 }
 
@@ -913,6 +1001,10 @@ struct insfm_ba {
     int *row_ptr = nullptr, *col = nullptr, *blk_row = nullptr, *ustart = nullptr;
     int *nbr_ptr = nullptr, *nbr_j = nullptr, *pos_up = nullptr, *pos_lo = nullptr;
     int4* sdesc = nullptr;  // k_schur: per camera-major own observation {o, p, partner begin, partner end}
+    int* cm_pt = nullptr;    // k_lin_cams: per camera-major observation, its (local) point
+    int* lin_blk = nullptr;  // k_lin_points: track runs of at most kThreads observations (or one longer track)
+    int n_lin = 0;
+    double* cm_uv = nullptr; // k_lin_cams: per camera-major observation, its uv
     double* Sn = nullptr;  // row-contiguous scaled neighbour blocks for the CG (both triangles, padded rows)
     int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
@@ -1176,10 +1268,10 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
         if (h->Pl > 0)
-            k_lin_points<M><<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->uv, h->pp, cams,
-                                                                              pts_local, h->d.huber_delta, h->W, h->V, h->gp);
+            k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
+                                                                 pts_local, h->d.huber_delta, h->W, h->V, h->gp);
         const size_t lds = sizeof(double) * kThreads * (2 * D + 2);
-        k_lin_cams<M><<<h->C, kThreads, lds, h->stream>>>(h->cam_ptr, h->cam_obs, h->ptl, h->uv, h->pp, cams, pts_local,
+        k_lin_cams<M><<<h->C, kThreads, lds, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams, pts_local,
                                                           h->d.huber_delta, h->U, h->gc);
         return launch_err(h, "linearize");
     });
@@ -1401,8 +1493,8 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     int rc = with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (h->Pl > 0)
-            k_backsub<DV><<<h->n_gp, kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->cam, h->W, dcp, h->V, h->Vinv, h->gp,
-                                                               pts_local, h->dp, h->pts_new, h->part_gp);
+            k_backsub<DV><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->W, dcp, h->V, h->Vinv,
+                                                                  h->gp, pts_local, h->dp, h->pts_new, h->part_gp);
         return launch_err(h, "k_backsub");
     });
     if (rc) return rc;
@@ -1782,6 +1874,26 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->cam_ptr, cptr.data(), cptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->cam_obs, cobs.data(), cobs.size()))) return fail(rc, "");
+    if (kind != 1) {
+        std::vector<int> lb(1, 0);
+        for (int p = 0; p < Pl; ++p)  // close the run before a track that would overflow it
+            if (p > lb.back() && (lptr[p + 1] - lptr[lb.back()] > kLinThreads || p - lb.back() >= kLinThreads))
+                lb.push_back(p);
+        if (Pl > 0) lb.push_back(Pl);
+        h->n_lin = (int)lb.size() - 1;
+        if ((rc = upload(h, &h->lin_blk, lb.data(), lb.size()))) return fail(rc, "");
+        std::vector<int> cmp(cobs.size());
+        std::vector<double> cmuv(2 * cobs.size());
+        for (size_t e = 0; e < cobs.size(); ++e) {
+            const int o = cobs[e];
+            if (o < 0 || o >= Nl) continue;
+            cmp[e] = lptl[o];
+            cmuv[2 * e] = obs[2 * (size_t)lsrc[o]];
+            cmuv[2 * e + 1] = obs[2 * (size_t)lsrc[o] + 1];
+        }
+        if ((rc = upload(h, &h->cm_pt, cmp.data(), cmp.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->cm_uv, cmuv.data(), cmuv.size()))) return fail(rc, "");
+    }
     if ((rc = upload(h, &h->row_ptr, rptr.data(), rptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->col, cols.data(), cols.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->blk_row, brow.data(), brow.size()))) return fail(rc, "");
@@ -1838,6 +1950,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->n_gp = std::max(1, cdiv(Pl, kThreads));
     h->n_gp_grp = std::max(1, cdiv((long long)Pl * kGPG, kThreads));
     if (kind == 1) h->n_gp = h->n_gp_grp;  // the gain partials of k_gp_backsub
+    else h->n_gp = std::max(1, h->n_lin);   // one per run of k_backsub
     h->n_gc = std::max(1, cdiv(C, kThreads));
     if ((rc = dd(&h->part_cost, 2 * (size_t)h->n_cost))) return fail(rc, "");
     if ((rc = dd(&h->part_gp, (size_t)h->n_gp))) return fail(rc, "");
