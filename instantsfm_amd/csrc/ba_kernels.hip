@@ -76,7 +76,8 @@ __device__ __forceinline__ void sum_partials(const double* __restrict__ part, in
     double v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = 0.0;
-    for (int i = threadIdx.x; i < n; i += kThreads)
+#pragma unroll 8
+    for (int i = threadIdx.x; i < n; i += kThreads)  // unrolled: 8 loads in flight, the adds in order
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k] += part[(size_t)i * NV + k];
     block_sum<NV>(v, sh);
@@ -540,6 +541,8 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
     constexpr int DP = D + (D & 1);
     __shared__ double T[kWaves][DD];
     __shared__ double Sb[kWaves][DD];
+    __shared__ double La[kWaves][DD];
+    __shared__ double Lb[kWaves][DD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int e = blockIdx.x * kWaves + wv;
     if (e >= nnzb) return;
@@ -549,15 +552,21 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
         for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
         return;
     }
+    // the block and both factors' inverses staged together (every load in flight at once), the result kept in LDS for
+    // the transposed copy; same products in the same order as entry-wise loops over global memory
     const double* Lii = Li + (size_t)i * DD;
     const double* Ljj = Li + (size_t)j * DD;
-    for (int k = lane; k < DD; k += 64) Sb[wv][k] = blk[k];
+    for (int k = lane; k < DD; k += 64) {
+        Sb[wv][k] = blk[k];
+        La[wv][k] = Lii[k];
+        Lb[wv][k] = Ljj[k];
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (int k = lane; k < DD; k += 64) {
         const int a = k / D, bb = k % D;
         double s = 0.0;
-        for (int m = 0; m <= a; ++m) s += Lii[a * D + m] * Sb[wv][m * D + bb];
+        for (int m = 0; m <= a; ++m) s += La[wv][a * D + m] * Sb[wv][m * D + bb];
         T[wv][k] = s;
     }
     __builtin_amdgcn_wave_barrier();
@@ -566,20 +575,20 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
     double* lo = Sn + (size_t)pos_lo[e] * D * DP;
     for (int k = lane; k < D * DP; k += 64) {
         const int a = k / DP, bb = k % DP;
-        double v = 0.0, vt = 0.0;
+        double v = 0.0;
         if (bb < D) {
-            for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Ljj[bb * D + m];
+            for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Lb[wv][bb * D + m];
             blk[a * D + bb] = v;
+            Sb[wv][a * D + bb] = v;
         }
         up[k] = v;
-        (void)vt;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // transpose: lo[a][bb] = S~_ij[bb][a]  (read back the finished block)
+    // transpose: lo[a][bb] = S~_ij[bb][a]
     for (int k = lane; k < D * DP; k += 64) {
         const int a = k / DP, bb = k % DP;
-        lo[k] = (bb < D) ? blk[bb * D + a] : 0.0;
+        lo[k] = (bb < D) ? Sb[wv][bb * D + a] : 0.0;
     }
 }
 
