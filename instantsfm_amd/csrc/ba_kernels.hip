@@ -1051,7 +1051,8 @@ struct insfm_ba {
     bool tlon = false;
     TlBufs tl{};
     std::vector<int> clab_host;
-    size_t chol_lds = 0, trinv_lds = 0, erow_lds = 0, update_lds = 0;
+    size_t chol_lds = 0, trinv_lds = 0, erow_lds = 0, pc_lds = 0;
+    int pc_rows = 0;  // k_tl_pc rows per restriction pass
     // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
     double *Ebuf[2]{}, *Dinvbuf[2]{}, *Linvbuf[2]{}, *Einvbuf[2]{};
     int* okbuf = nullptr;  // [2]
@@ -1358,9 +1359,14 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
 // correction, S~ u.
 template <int D>
 void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
-    k_tl_update<D><<<h->tl.nc, kCgThreads, h->update_lds, h->stream>>>(it, h->C, maxit, tol2, h->Lf, h->cg, h->tl);
-    k_tl_coarse<D><<<h->tl.nc, kThreads, 0, h->stream>>>(h->cg, h->tl, h->tl.Einv);
-    k_tl_spmv<D><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
+    if (it == 0) {  // setup: restriction of r0, u0 = M~^-1 r0, w0 = S~ u0 and the partials of iteration 0
+        k_tl_rrest<D><<<cdiv((long long)h->C * (D + 1), kThreads), kThreads, 0, h->stream>>>(h->C, h->cg, h->tl);
+        k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
+                                                                   h->tl.Einv);
+        k_tl_pspmv<D><<<h->C, kCgThreads, 0, h->stream>>>(-1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
+    }
+    k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
+    k_tl_pspmv<D><<<h->C, kCgThreads, 0, h->stream>>>(it, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
 }
 
 // k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
@@ -2078,6 +2084,12 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         tl.cl_ptr = ip;
         if ((rc = upload(h, &ip, clc.data(), clc.size()))) return fail(rc, "");
         tl.cl_cams = ip;
+        {
+            std::vector<int> cpos(C);
+            for (int q = 0; q < C; ++q) cpos[clc[q]] = q;
+            if ((rc = upload(h, &ip, cpos.data(), cpos.size()))) return fail(rc, "");
+            tl.cpos = ip;
+        }
         if ((rc = upload(h, &ip, alone.data(), alone.size()))) return fail(rc, "");
         tl.alone = ip;
         if ((rc = upload(h, &ip, sperm.data(), sperm.size()))) return fail(rc, "");
@@ -2097,9 +2109,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd(&tl.u, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Zt, cd * MC))) return fail(rc, "");
         if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
-        if ((rc = dd(&tl.gd, 2 * (size_t)C))) return fail(rc, "");
-        if ((rc = dd(&tl.rho[0], 2 * (size_t)nc))) return fail(rc, "");
-        tl.rho[1] = tl.rho[0] + nc;
+        if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
+        if ((rc = dd(&tl.rowR, (size_t)C * MC))) return fail(rc, "");
         if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
         for (int sl = 0; sl < 2; ++sl) {
             if ((rc = dd(&h->Ebuf[sl], (size_t)m * m))) return fail(rc, "");
@@ -2125,9 +2136,12 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         const int DPd = D + (D & 1), CH = D <= 9 ? 32 : 16;
         h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
                                         (size_t)maxseg * MC * MC);
-        const int RPWd = kCgThreads / D;
-        h->update_lds = sizeof(double) * (2 * (size_t)RPWd * D + (size_t)RPWd * D * MC + (size_t)maxmem * (MC + 1));
-        if (h->erow_lds > 160 * 1024 || h->update_lds > 160 * 1024)
+        {
+            const size_t fixed = sizeof(double) * ((size_t)MC * m + (size_t)m), budget = 144 * 1024;
+            h->pc_rows = (int)std::min<size_t>((size_t)C, (budget - fixed) / (sizeof(double) * MC));
+            h->pc_lds = fixed + sizeof(double) * (size_t)h->pc_rows * MC;
+        }
+        if (h->erow_lds > 160 * 1024 || h->pc_lds > 150 * 1024)
             return fail(INSFM_BA_EINVAL, "two-level preconditioner: scene too connected for the LDS budget (use precond 0)");
         (void)hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->chol_lds);
         (void)hipFuncSetAttribute((const void*)k_tl_trinv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->trinv_lds);
@@ -2135,8 +2149,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             constexpr int DV = decltype(dc_)::value;
             (void)hipFuncSetAttribute((const void*)k_tl_erow<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->erow_lds);
-            (void)hipFuncSetAttribute((const void*)k_tl_update<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h->update_lds);
+            (void)hipFuncSetAttribute((const void*)k_tl_pc<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->pc_lds);
             return 0;
         });
         h->tlon = true;
@@ -2246,7 +2260,8 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             if (which == 2) {
                 launch_tl_iter<DV>(h, 1, h->d.pcg_max_iter, 0.0);
             } else if (which == 3) {
-                k_tl_spmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->cg, h->tl);
+                k_tl_pspmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
+                                                                   h->tl);
             } else if (which == 4) {
                 int rc2 = run_tl_basis(h, h->cams_cur, h->stream);
                 if (!rc2) rc2 = run_tl_build(h, 0, h->stream);
@@ -2298,10 +2313,10 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 6: src = h->b; n = C * D; break;
         case 7: src = h->dc; n = C * D; break;
         case 8: src = h->dp; n = Pl * 3; break;
-        // two-level internals (debug): 9 u, 10 w, 11 Rc, 12/13 E^-1 slot 0/1, 14 row partials [r.u | w.u], 15 r
+        // two-level internals (debug): 9 u, 10 w, 11 rowR, 12/13 E^-1 slot 0/1, 14 row partials [r.u | w.u], 15 r
         case 9: src = h->tl.u; n = h->tlon ? C * D : 0; break;
         case 10: src = h->cg.w[0]; n = C * D; break;
-        case 11: src = h->tl.Rc; n = h->tlon ? (size_t)h->tl.m : 0; break;
+        case 11: src = h->tl.rowR; n = h->tlon ? C * (D + 1) : 0; break;  // restriction row partials
         case 12: src = h->Einvbuf[0]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 13: src = h->Einvbuf[1]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 14: src = h->tl.gd; n = h->tlon ? 2 * C : 0; break;

@@ -15,10 +15,10 @@
 //   k_tl_dinv    : inverses of the factor's diagonal blocks
 //   k_tl_trinv   : L^-1 by column blocks (block forward substitution, diag-block inverses as GEMMs)
 //   k_tl_gram    : E^-1 = L^-T L^-1 (dense tiles)
-// Per CG iteration (preconditioned Chronopoulos-Gear, same stopping rule as block-Jacobi):
-//   k_tl_update  : per cluster: recurrence scalars from the partials, p/s/x/r update, R_c = sum Z~_i^T r_i, ||L r||^2
-//   k_tl_coarse  : per cluster: y = E^-1 R (its MC rows), u_i = r_i + Z~_i y_c
-//   k_tl_spmv    : w = S~ u (row-contiguous Sn stream), partial dots r.u and w.u per row
+// Per CG iteration (pipelined PCG, same stopping rule as block-Jacobi; see the section below):
+//   k_tl_pc      : per cluster: recurrence scalars from the row partials, restriction, y = E^-1 R (its MC rows),
+//                  m_i = w_i + Z~_i y_c
+//   k_tl_pspmv   : n = S~ m (row-contiguous Sn stream), the row's vector updates, its partials for the next iteration
 #pragma once
 #include "ba_common.h"
 #include "ba_device.h"
@@ -32,9 +32,9 @@ constexpr int kPS = kNB + 1;     // padded LDS row stride (odd: conflict-free co
 struct TlBufs {
     double* u;           // [C*D]  preconditioned residual
     double* Zt;          // [C][D][MC]
-    double* Rc;          // [m]   restriction Z~^T r per cluster (k_tl_update)
-    double* gd;          // [2C]  r_i.u_i | w_i.u_i  (row partials of k_tl_spmv)
-    double* rho[2];      // [nc]  ||L r||^2 per cluster of r_k, stored at parity k & 1
+    double* Rc;          // [m]   (debug) restriction
+    double* gd;          // [3C]  row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2  (k_tl_pspmv)
+    double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
     double* Oseg;        // [nseg][MC][MC] per (row, neighbour cluster) sums of Z~_i^T S~_ij Z~_j
     double* E;           // [m][m] coarse matrix, Cholesky factor (lower) in place
     double* Dinv;        // [nB][kNB][kNB] inverses of the diagonal blocks of the factor
@@ -43,6 +43,7 @@ struct TlBufs {
     int* ok;             // coarse correction usable (E positive definite)
     const int* cl_ptr;   // [nc+1]
     const int* cl_cams;  // cluster members, ascending camera id
+    const int* cpos;     // [C] position of camera i in cl_cams
     const int* alone;    // [C] camera is alone in its cluster -> basis [I_D | 0]
     const int* sperm;    // [n_nbr] neighbour slots of each row ordered by (cluster of the neighbour, slot)
     const int4* seg;     // [nseg] (cluster, sorted begin, sorted end, own-cluster flag) per (row, neighbour cluster)
@@ -467,249 +468,243 @@ __global__ __launch_bounds__(256) void k_tl_gram(int m, const double* __restrict
     }
 }
 
-// ---- per iteration ------------------------------------------------------------------------------------------
-// One workgroup per cluster c.  it >= 1: recurrence step i = it - 1 -- every workgroup sums the row partials of
-// k_tl_spmv (it-1) and the cluster partials of rho_i in the same fixed order, tests rho_i <= tol^2 ||b||^2 and forms
-// alpha_i, beta_i (workgroup 0 records them); then for the cluster's rows p = u + beta p, s = w + beta s,
-// x += alpha p, r -= alpha s.  Every it: R_c = sum_i Z~_i^T r_i and rho_c = sum_i ||L_i r_i||^2 over its rows.
-// The row data are loaded before the scalar reduction (they do not depend on alpha / beta).
+// ---- per iteration: pipelined PCG (oracle/ba_oracle.c ora_pcg, two-level path) -----------------------------------
+// Ghysels & Vanroose's pipelined recurrence: per iteration i, with r, u = M~^-1 r, w = S~ u and the row partials of
+// gamma = (r, u), delta = (w, u), rho = ||L r||^2 and of the restriction Z~^T w already in memory:
+//   k_tl_pc    (one workgroup per cluster): the scalars (every workgroup sums the partials in the same fixed order;
+//              convergence / breakdown test; alpha_i, beta_i recorded by workgroup 0), the full restriction R, the
+//              cluster's coarse rows y_c = (E^-1 R)_c and m = w + Z~ y_c for its rows;
+//   k_tl_pspmv (one workgroup per camera row): n = S~ m, then z = n + beta z, q = m + beta q, s = w + beta s,
+//              p = u + beta p, x += alpha p, r -= alpha s, u -= alpha q, w -= alpha z for the row, and the row's
+//              partials for iteration i + 1.
+// Two launches per iteration instead of three.  Setup (it = -1): k_tl_rrest (Z~^T r0 per row), k_tl_pc (u0 = r0 + Z~ y),
+// k_tl_pspmv (w0 = S~ u0 and the partials of iteration 0).  Buffers: q = cg.r[1], z = cg.w[1], m = cg.s[1].
+
+// rowR[i][k] = sum_a Z~_i[a][k] r_i[a]  (a ascending)
 template <int D>
-__global__ __launch_bounds__(kCgThreads) void k_tl_update(int it, int C, int maxit, double tol2_rel,
-                                                          const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
-    constexpr int MC = D + 1, RPW = kCgThreads / D;
+__global__ __launch_bounds__(kThreads) void k_tl_rrest(int C, CgBufs cg, TlBufs tl) {
+    constexpr int MC = D + 1;
+    const int g = blockIdx.x * kThreads + threadIdx.x;
+    if (g >= C * MC) return;
+    const int i = g / MC, k = g % MC;
+    const double* Z = tl.Zt + (size_t)i * D * MC + k;
+    const double* r = cg.r[0] + (size_t)i * D;
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < D; ++a) s += Z[a * MC] * r[a];
+    tl.rowR[(size_t)tl.cpos[i] * MC + k] = s;
+}
+
+// Copy n doubles global -> LDS: U loads per thread in flight before their LDS stores (a plain strided loop waits for
+// every load before its store).
+template <int NT, int U>
+__device__ __forceinline__ void stage_lds(double* dst, const double* __restrict__ src, int n) {
+    const int t = threadIdx.x;
+    for (int b = 0; b < n; b += NT * U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = b + t + u * NT;
+            if (q < n) v[u] = src[q];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = b + t + u * NT;
+            if (q < n) dst[q] = v[u];
+        }
+    }
+}
+
+// prows: restriction row partials staged in LDS per pass (rows in cluster order; the host sizes it to the LDS budget)
+template <int D>
+__global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, double tol2_rel, int prows, CgBufs cg,
+                                                      TlBufs tl, const double* __restrict__ Einv) {
+    constexpr int MC = D + 1;
     extern __shared__ double lds[];
-    double* rl = lds;                 // [RPW][D]  r of the pass's rows
-    double* lq = rl + RPW * D;        // [RPW][D]  (L r)_a^2
-    double* Rm = lq + RPW * D;        // [maxmem][MC]
-    double* sq = Rm + tl.maxmem * MC; // [maxmem]
+    double* LR = lds;                         // [prows * MC] restriction row partials of a pass
+    double* EL = LR + (size_t)prows * MC;     // [MC][m] this cluster's rows of E^-1
+    double* Rs = EL + (size_t)MC * tl.m;      // [m] full restriction
+    __shared__ double y[MC];
     __shared__ double red[3][kCgWaves];
     __shared__ double sc[3];
     if (cg.status[0] != 0) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int c = blockIdx.x;
+    const int c = blockIdx.x, m = tl.m;
+    const bool setup = it < 0, use = tl.ok[0] != 0;
     const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
-    const int rloc = t / D, a = t % D;
-    if (it == 0 && c == 0 && t == 0) cg.status[2] = tl.ok[0];   // reported as insfm_ba_stats.coarse_used
-    // first pass row data (prefetch)
-    double pu = 0.0, pp = 0.0, pw = 0.0, ps = 0.0, px = 0.0, pr = 0.0;
-    size_t idx0 = 0;
-    const bool on0 = rloc < RPW && rloc < ne;
-    if (on0) {
-        idx0 = (size_t)tl.cl_cams[e0 + rloc] * D + a;
-        pr = cg.r[0][idx0];
-        if (it > 0) { pu = tl.u[idx0]; pp = cg.p[idx0]; pw = cg.w[0][idx0]; ps = cg.s[0][idx0]; px = cg.x[idx0]; }
-    }
-    // the first pass's L row and Z~ column depend only on the cluster's rows: in flight before the barriers too
-    double Lp[D], Zp[D];
-    if (on0) {
-        const double* L = Lf + idx0 * D;  // row a of L_row (idx0 = row * D + a)
+    if (setup && c == 0 && t == 0) cg.status[2] = tl.ok[0];  // reported as insfm_ba_stats.coarse_used
+    // every global load that does not depend on a reduction is issued before the first wait: the cluster's first row
+    // entry (a two-load chain: issued first), the scalar partials, the recurrence history, the restriction entry's
+    // member range, this cluster's E^-1 rows and the first pass of the restriction partials
+    const double* src = setup ? cg.r[0] : cg.w[0];
+    const bool pon = t < ne * D;
+    size_t pidx = 0;
+    double vp = 0.0, Zq[MC];
+    if (pon) {
+        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;
+        vp = src[pidx];
+        if (use) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) Lp[k] = (k <= a) ? L[k] : 0.0;
+            for (int k = 0; k < MC; ++k) Zq[k] = tl.Zt[pidx * MC + k];
+        }
     }
-    const bool zon = t < RPW * MC && t / MC < ne;
-    if (zon) {
-        const double* Z = tl.Zt + (size_t)tl.cl_cams[e0 + t / MC] * D * MC + t % MC;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (!setup)
+        for (int k = t; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
+    double h_alpha = 1.0, h_gam = 1.0, h_bb = 0.0;
+    if (!setup && t == 0) {
+        if (it >= 1) { h_alpha = cg.hist[2 * (it - 1)]; h_gam = cg.hist[2 * (it - 1) + 1]; h_bb = cg.hist[2 * (maxit + 1)]; }
+    }
+    int rb0 = 0, rb1 = 0;
+    if (use && t < m) { rb0 = tl.cl_ptr[t / MC]; rb1 = tl.cl_ptr[t / MC + 1]; }
+    const int np = (C + prows - 1) / prows;
+    if (use) {
+        constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads;
+        double ev[UE];
 #pragma unroll
-        for (int aa = 0; aa < D; ++aa) Zp[aa] = Z[aa * MC];
+        for (int u = 0; u < UE; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < MC * m) ev[u] = Einv[(size_t)c * MC * m + q];
+        }
+        stage_lds<kCgThreads, 16>(LR, tl.rowR, min(C, prows) * MC);
+#pragma unroll
+        for (int u = 0; u < UE; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < MC * m) EL[q] = ev[u];
+        }
     }
-    double al = 0.0, be = 0.0;
-    if (it > 0) {
-        const int i = it - 1;
-        const double* G0 = tl.gd;
-        const double* G1 = tl.gd + C;
-        const double* RH = tl.rho[i & 1];
-        double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-        for (int k = t; k < C; k += kCgThreads) { g0 += G0[k]; g1 += G1[k]; }
-        for (int k = t; k < tl.nc; k += kCgThreads) g2 += RH[k];
+    if (!setup) {
+        const int i = it;
         g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
         if (lane == 0) { red[0][wv] = g0; red[1][wv] = g1; red[2][wv] = g2; }
         __syncthreads();
         if (t == 0) {
             double gam = 0.0, del = 0.0, rho = 0.0;
             for (int w = 0; w < kCgWaves; ++w) { gam += red[0][w]; del += red[1][w]; rho += red[2][w]; }
-            const double h_alpha = (i >= 1) ? cg.hist[2 * (i - 1)] : 1.0;
-            const double h_gam = (i >= 1) ? cg.hist[2 * (i - 1) + 1] : 1.0;
-            const double bb = (i == 0) ? rho : cg.hist[2 * (maxit + 1)];
-            double flag = 0.0, alv = 0.0, bev = 0.0;
+            const double bb = (i == 0) ? rho : h_bb;
+            double flag = 0.0;
             const bool lead = blockIdx.x == 0;
             if (rho <= tol2_rel * bb || i >= maxit) {
                 flag = 1.0;
                 if (lead) { cg.status[1] = i; __threadfence(); cg.status[0] = 1; }
             } else {
-                bev = (i == 0) ? 0.0 : gam / h_gam;
+                const double bev = (i == 0) ? 0.0 : gam / h_gam;
                 const double den = (i == 0) ? del : del - bev * gam / h_alpha;
                 if (!(den > 0.0)) {
                     flag = 2.0;
                     if (lead) { cg.status[1] = i; __threadfence(); cg.status[0] = 2; }
-                } else {
-                    alv = gam / den;
-                    if (lead) {
-                        cg.hist[2 * i] = alv;
-                        cg.hist[2 * i + 1] = gam;
-                        if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
-                    }
+                } else if (lead) {
+                    cg.hist[2 * i] = gam / den;
+                    cg.hist[2 * i + 1] = gam;
+                    if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
                 }
             }
-            sc[0] = alv; sc[1] = bev; sc[2] = flag;
+            sc[0] = flag;
         }
         __syncthreads();
-        if (sc[2] != 0.0) return;
-        al = sc[0];
-        be = sc[1];
-    }
-    for (int pass = 0; pass * RPW < ne; ++pass) {
-        const int mi = pass * RPW + rloc;
-        const bool on = rloc < RPW && mi < ne;
-        const int row = on ? tl.cl_cams[e0 + mi] : 0;
-        if (on) {
-            const size_t idx = (size_t)row * D + a;
-            double u_, p_, w_, s_, x_, r_;
-            if (pass == 0) { u_ = pu; p_ = pp; w_ = pw; s_ = ps; x_ = px; r_ = pr; }
-            else {
-                r_ = cg.r[0][idx];
-                if (it > 0) { u_ = tl.u[idx]; p_ = cg.p[idx]; w_ = cg.w[0][idx]; s_ = cg.s[0][idx]; x_ = cg.x[idx]; }
-                else { u_ = p_ = w_ = s_ = x_ = 0.0; }
-            }
-            if (it > 0) {
-                const double pn = u_ + be * p_;
-                const double sn = w_ + be * s_;
-                cg.p[idx] = pn;
-                cg.s[0][idx] = sn;
-                cg.x[idx] = x_ + al * pn;
-                r_ = r_ - al * sn;
-                cg.r[0][idx] = r_;
-            }
-            rl[rloc * D + a] = r_;
-        }
-        __syncthreads();
-        if (on) {
-            double lr = 0.0;
-            if (pass == 0) {
-#pragma unroll
-                for (int k = 0; k < D; ++k)
-                    if (k <= a) lr += Lp[k] * rl[rloc * D + k];
-            } else {
-                const double* L = Lf + (size_t)row * D * D + a * D;
-#pragma unroll
-                for (int k = 0; k < D; ++k)
-                    if (k <= a) lr += L[k] * rl[rloc * D + k];
-            }
-            lq[rloc * D + a] = lr * lr;
-        }
-        __syncthreads();
-        for (int e = t; e < RPW * MC; e += kCgThreads) {
-            const int rr = e / MC, k = e % MC, mj = pass * RPW + rr;
-            if (mj < ne) {
-                double v = 0.0;
-                if (pass == 0 && e == t) {
-#pragma unroll
-                    for (int aa = 0; aa < D; ++aa) v += Zp[aa] * rl[rr * D + aa];
-                } else {
-                    const double* Z = tl.Zt + (size_t)tl.cl_cams[e0 + mj] * D * MC + k;
-#pragma unroll
-                    for (int aa = 0; aa < D; ++aa) v += Z[aa * MC] * rl[rr * D + aa];
-                }
-                Rm[mj * MC + k] = v;
-                if (k == 0) {
-                    double s2 = 0.0;
-#pragma unroll
-                    for (int aa = 0; aa < D; ++aa) s2 += lq[rr * D + aa];
-                    sq[mj] = s2;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (t < MC) {
-        double v = 0.0;
-        for (int mi = 0; mi < ne; ++mi) v += Rm[mi * MC + t];
-        tl.Rc[c * MC + t] = v;
-    } else if (t == MC) {
-        double v = 0.0;
-        for (int mi = 0; mi < ne; ++mi) v += sq[mi];
-        tl.rho[it & 1][c] = v;
-    }
-}
-
-// One workgroup per cluster c: y_c = (E^-1 R) rows of c, u_i = r_i + Z~_i y_c for its rows (u = r without a usable
-// coarse matrix).
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_tl_coarse(CgBufs cg, TlBufs tl, const double* __restrict__ Einv) {
-    constexpr int MC = D + 1;
-    __shared__ double y[MC];
-    if (cg.status[0] != 0) return;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int c = blockIdx.x, m = tl.m;
-    const bool use = tl.ok[0] != 0;
-    const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
-    // this thread's first row entry (r and its Z~ row) is independent of y: loaded together with E^-1 and R
-    const bool pon = t < ne * D;
-    size_t pidx = 0;
-    double rp = 0.0, Zq[MC];
-    if (pon) {
-        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;
-        rp = cg.r[0][pidx];
-        if (use) {
-#pragma unroll
-            for (int k = 0; k < MC; ++k) Zq[k] = tl.Zt[pidx * MC + k];
-        }
+        if (sc[0] != 0.0) return;
     }
     if (use) {
-        // a wave's rows of E^-1 are read together (every load of the wave in flight at once), each row's dot in the
-        // same lane order as a row-at-a-time loop
-        constexpr int KPW = (MC + kWaves - 1) / kWaves, LPL = (kCoarseMax + 63) / 64;
-        double s[KPW];
+        // full restriction: entry (c', k) sums the row partials of cluster c' in ascending camera order (from LDS)
+        for (int pass = 0; pass < np; ++pass) {
+            const int r0 = pass * prows, r1 = min(C, r0 + prows);
+            if (pass > 0) {
+                __syncthreads();
+                stage_lds<kCgThreads, 16>(LR, tl.rowR + (size_t)r0 * MC, (r1 - r0) * MC);
+            }
+            __syncthreads();
+            for (int e = t; e < m; e += kCgThreads) {
+                const int k = e % MC;
+                const int b0 = max(e == t ? rb0 : tl.cl_ptr[e / MC], r0), b1 = min(e == t ? rb1 : tl.cl_ptr[e / MC + 1], r1);
+                double v = pass == 0 ? 0.0 : Rs[e];
+#pragma unroll 8
+                for (int mi = b0; mi < b1; ++mi) v += LR[(mi - r0) * MC + k];
+                Rs[e] = v;
+            }
+        }
+        __syncthreads();
+        constexpr int KPW = (MC + kCgWaves - 1) / kCgWaves, LPL = (kCoarseMax + 63) / 64;
+        double sy[KPW];
 #pragma unroll
-        for (int kk = 0; kk < KPW; ++kk) s[kk] = 0.0;
+        for (int kk = 0; kk < KPW; ++kk) sy[kk] = 0.0;
 #pragma unroll
         for (int q = 0; q < LPL; ++q) {
             const int l = lane + 64 * q;
             if (l < m) {
-                const double rl = tl.Rc[l];
+                const double rl = Rs[l];
 #pragma unroll
                 for (int kk = 0; kk < KPW; ++kk) {
-                    const int k = wv + kk * kWaves;
-                    if (k < MC) s[kk] += Einv[(size_t)(c * MC + k) * m + l] * rl;
+                    const int k = wv + kk * kCgWaves;
+                    if (k < MC) sy[kk] += EL[(size_t)k * m + l] * rl;
                 }
             }
         }
 #pragma unroll
         for (int kk = 0; kk < KPW; ++kk) {
-            const int k = wv + kk * kWaves;
-            const double v = wave_sum(s[kk]);
+            const int k = wv + kk * kCgWaves;
+            const double v = wave_sum(sy[kk]);
             if (lane == 0 && k < MC) y[k] = v;
         }
         __syncthreads();
     }
-    for (int e = t; e < ne * D; e += kThreads) {
+    double* dst = setup ? tl.u : cg.s[1];
+    for (int e = t; e < ne * D; e += kCgThreads) {
         const bool first = e == t;
         const size_t idx = first ? pidx : (size_t)tl.cl_cams[e0 + e / D] * D + e % D;
-        double v = first ? rp : cg.r[0][idx];
+        double v = first ? vp : src[idx];
         if (use) {
             const double* Z = tl.Zt + idx * MC;
+            double sz = 0.0;
 #pragma unroll
-            for (int k = 0; k < MC; ++k) v += (first ? Zq[k] : Z[k]) * y[k];
+            for (int k = 0; k < MC; ++k) sz += (first ? Zq[k] : Z[k]) * y[k];
+            v += sz;
         }
-        tl.u[idx] = v;
+        dst[idx] = v;
     }
 }
 
-// w = S~ u for one camera row per 512-thread workgroup (Sn streamed as in k_cg_iter), row partials r.u and w.u.
+// One camera row per 512-thread workgroup: the product with S~ (row-contiguous Sn stream), the row's vector updates
+// and its partials for the next iteration (setup: w0 = S~ u0 and the partials of iteration 0).
 template <int D>
-__global__ __launch_bounds__(kCgThreads) void k_tl_spmv(int C, const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_j,
-                                                        const double* __restrict__ Sn, CgBufs cg, TlBufs tl) {
+__global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const int* __restrict__ nbr_ptr,
+                                                         const int* __restrict__ nbr_j, const double* __restrict__ Sn,
+                                                         const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
     using G = CgGeom<D>;
-    constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = G::BPR;
+    constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = G::BPR, MC = D + 1;
     __shared__ double red[kCgWaves][BPW][PPB];
+    __shared__ double sv[2][D];  // r and w of the row after the update
     if (cg.status[0] != 0) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int row = blockIdx.x;
+    const bool setup = it < 0;
     const int bw = (PPB <= 64) ? lane / PPB : 0;
     const int pc0 = (PPB <= 64) ? lane - bw * PPB : lane;
     const bool lane_on = (PPB <= 64) ? (bw < BPW) : true;
     const int slot = wv * BPW + bw;
     const int n0 = nbr_ptr[row], n1 = nbr_ptr[row + 1];
-    const double* u = tl.u;
+    const double* v = setup ? tl.u : cg.s[1];
+    // the row's own vector entries (independent of the product): in flight during the stream
+    const size_t own = (size_t)row * D + (lane < D ? lane : 0);
+    double vo = 0.0, u_ = 0.0, w_ = 0.0, r_ = 0.0, z_ = 0.0, q_ = 0.0, s_ = 0.0, p_ = 0.0, x_ = 0.0, al = 0.0, be = 0.0;
+    // wave 0's tail operands, independent of everything: row a of L (lanes < D) or column k of Z~ (lanes D..D+MC-1)
+    double tailop[D];
+    if (wv == 0 && lane < D) {
+        const double* L = Lf + (size_t)row * D * D + lane * D;
+#pragma unroll
+        for (int k = 0; k < D; ++k) tailop[k] = (k <= lane) ? L[k] : 0.0;
+    } else if (wv == 0 && lane < D + MC) {
+        const double* Z = tl.Zt + (size_t)row * D * MC + (lane - D);
+#pragma unroll
+        for (int a = 0; a < D; ++a) tailop[a] = Z[a * MC];
+    }
+    if (wv == 0 && lane < D) {
+        vo = v[own]; u_ = tl.u[own]; r_ = cg.r[0][own];
+        if (!setup) {
+            w_ = cg.w[0][own]; z_ = cg.w[1][own]; q_ = cg.r[1][own]; s_ = cg.s[0][own]; p_ = cg.p[own]; x_ = cg.x[own];
+            al = cg.hist[2 * it];
+            be = (it == 0) ? 0.0 : cg.hist[2 * it + 1] / cg.hist[2 * (it - 1) + 1];
+        }
+    }
     double acc[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; ++q) acc[q] = 0.0;
@@ -720,17 +715,17 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_spmv(int C, const int* __rest
             const int pc = pc0 + 64 * q;
             if (pc >= PPB) continue;
             const int bcol = 2 * (pc % HP);
-            const double2 sv = *reinterpret_cast<const double2*>(Sn + ((size_t)nn * D * DP + 2 * (size_t)pc));
+            const double2 svv = *reinterpret_cast<const double2*>(Sn + ((size_t)nn * D * DP + 2 * (size_t)pc));
             const size_t jx = (size_t)j * D + bcol;
             double u0, u1;
             if constexpr ((D & 1) == 0) {
-                const double2 uv = *reinterpret_cast<const double2*>(u + jx);
+                const double2 uv = *reinterpret_cast<const double2*>(v + jx);
                 u0 = uv.x; u1 = uv.y;
             } else {
-                u0 = u[jx];
-                u1 = (bcol + 1 < D) ? u[jx + 1] : 0.0;
+                u0 = v[jx];
+                u1 = (bcol + 1 < D) ? v[jx + 1] : 0.0;
             }
-            acc[q] += sv.x * u0 + sv.y * u1;
+            acc[q] += svv.x * u0 + svv.y * u1;
         }
     }
     if (lane_on) {
@@ -741,26 +736,56 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_spmv(int C, const int* __rest
         }
     }
     __syncthreads();
-    if (wv == 0) {
-        double g0 = 0.0, g1 = 0.0;
-        if (lane < D) {
-            const int a = lane;
-            double tot = 0.0;
-            for (int w = 0; w < kCgWaves; ++w)
+    if (wv != 0) return;
+    double g0 = 0.0, g1 = 0.0;
+    if (lane < D) {
+        const int a = lane;
+        double tot = 0.0;
+        for (int w = 0; w < kCgWaves; ++w)
 #pragma unroll
-                for (int bb = 0; bb < BPW; ++bb)
+            for (int bb = 0; bb < BPW; ++bb)
 #pragma unroll
-                    for (int k = 0; k < HP; ++k) tot += red[w][bb][a * HP + k];
-            const size_t own = (size_t)row * D + a;
-            const double uo = u[own];
-            const double wn = uo + tot;
-            cg.w[0][own] = wn;
-            g0 = cg.r[0][own] * uo;
-            g1 = wn * uo;
+                for (int k = 0; k < HP; ++k) tot += red[w][bb][a * HP + k];
+        const double prod = vo + tot;  // diagonal block of S~ is I
+        if (setup) {
+            w_ = prod;
+            cg.w[0][own] = w_;
+            cg.w[1][own] = 0.0;  // z
+            cg.r[1][own] = 0.0;  // q
+        } else {
+            const double zn = prod + be * z_;
+            const double qn = vo + be * q_;
+            const double sn = w_ + be * s_;
+            const double pn = u_ + be * p_;
+            x_ += al * pn;
+            r_ -= al * sn;
+            u_ -= al * qn;
+            w_ -= al * zn;
+            cg.w[1][own] = zn; cg.r[1][own] = qn; cg.s[0][own] = sn; cg.p[own] = pn; cg.x[own] = x_;
+            cg.r[0][own] = r_; tl.u[own] = u_; cg.w[0][own] = w_;
         }
-        g0 = wave_sum(g0); g1 = wave_sum(g1);
-        if (lane == 0) { tl.gd[row] = g0; tl.gd[C + row] = g1; }
+        sv[0][a] = r_;
+        sv[1][a] = w_;
+        g0 = r_ * u_;
+        g1 = w_ * u_;
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double g2 = 0.0, rr = 0.0;
+    if (lane < D) {  // (L r)_a for the true-residual norm
+        double lr = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (k <= lane) lr += tailop[k] * sv[0][k];
+        g2 = lr * lr;
+    } else if (lane < D + MC) {  // restriction of w: sum_a Z~[a][k] w_a
+#pragma unroll
+        for (int a = 0; a < D; ++a) rr += tailop[a] * sv[1][a];
+        tl.rowR[(size_t)tl.cpos[row] * MC + (lane - D)] = rr;
+    }
+    g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+    if (lane == 0) { tl.gd[row] = g0; tl.gd[C + row] = g1; tl.gd[2 * C + row] = g2; }
 }
 
 }  // namespace insfm

@@ -997,6 +997,7 @@ int ora_pcg(ora_t* h, double* xout) {
     /* two-level preconditioner M~^-1 = I + Z~ E^-1 Z~^T in the scaled space (block-Jacobi + coarse correction) */
     const int MC = D + 1, nc = h->nclust, m = nc * MC;
     int twolev = h->precond == 1 && nc > 0;
+    const int pipelined = twolev;  /* the two-level path uses the pipelined recurrence (with or without a usable E) */
     double *Zt = NULL, *Einv = NULL, *Rc = NULL, *yc = NULL, *u = h->r;
     if (twolev) {
         Zt = (double*)malloc(sizeof(double) * (size_t)C * D * MC);
@@ -1033,6 +1034,66 @@ int ora_pcg(ora_t* h, double* xout) {
     if (twolev) coarse_apply(h, Zt, Einv, Rc, yc, h->r, u);
     spmv_scaled(h, u, w);
     double bb2 = dot(h->b, h->b, n, tmp);
+    if (pipelined) {
+        /* Pipelined PCG (Ghysels & Vanroose 2014, preconditioned variant): the same iterates as PCG in exact
+         * arithmetic, with the preconditioner and the operator applied to w (m = M~^-1 w, n = S~ m) so that every
+         * iteration needs ONE reduction phase (gamma, delta, rho, and the coarse restriction of w) followed by one
+         * coarse solve and one SpMV; the GPU runs it as two kernels per iteration (k_tl_pc + k_tl_pspmv). */
+        double *mv = (double*)malloc(sizeof(double) * n), *nv = (double*)malloc(sizeof(double) * n);
+        double *qv = (double*)calloc(n, sizeof(double)), *zv = (double*)calloc(n, sizeof(double));
+        double gam = dot(h->r, u, n, tmp), del = dot(w, u, n, tmp), rho = bb2;
+        double gam_prev = 1.0, alpha_prev = 1.0;
+        double tol2 = h->pcg_tol * h->pcg_tol * bb2;
+        int k = 0, fail = 0;
+        for (;; ++k) {
+            if (rho <= tol2 || k >= h->pcg_max_iter) break;
+            double alpha, beta, den;
+            if (k == 0) { beta = 0.0; den = del; }
+            else { beta = gam / gam_prev; den = del - beta * gam / alpha_prev; }
+            if (!(den > 0.0)) { fail = 1; break; }
+            alpha = gam / den;
+            if (twolev) coarse_apply(h, Zt, Einv, Rc, yc, w, mv);
+            else memcpy(mv, w, sizeof(double) * n);
+            spmv_scaled(h, mv, nv);
+            for (size_t e = 0; e < n; ++e) {
+                zv[e] = nv[e] + beta * zv[e];
+                qv[e] = mv[e] + beta * qv[e];
+                sv[e] = w[e] + beta * sv[e];
+                h->p[e] = u[e] + beta * h->p[e];
+                h->x[e] += alpha * h->p[e];
+                h->r[e] -= alpha * sv[e];
+                u[e] -= alpha * qv[e];
+                w[e] -= alpha * zv[e];
+            }
+            gam_prev = gam; alpha_prev = alpha;
+            gam = dot(h->r, u, n, tmp);
+            del = dot(w, u, n, tmp);
+            for (int i = 0; i < C; ++i) {
+                const double* L = Lfac + (size_t)i * DD;
+                for (int a = 0; a < D; ++a) {
+                    double s = 0;
+                    for (int kk = 0; kk <= a; ++kk) s += L[a * D + kk] * h->r[(size_t)i * D + kk];
+                    rt[(size_t)i * D + a] = s;
+                }
+            }
+            rho = dot(rt, rt, n, tmp);
+        }
+        free(mv); free(nv); free(qv); free(zv);
+        free(rt);
+        free(Lfac);
+        if (Zt) { free(Zt); free(Einv); free(Rc); free(yc); free(u); }
+        h->stats[7] = twolev;
+        if (fail) return -1;
+        for (int i = 0; i < C; ++i) {
+            const double* Li = h->Minv + (size_t)i * DD;
+            for (int a = 0; a < D; ++a) {
+                double s = 0;
+                for (int kk = a; kk < D; ++kk) s += Li[kk * D + a] * h->x[(size_t)i * D + kk];
+                xout[(size_t)i * D + a] = s;
+            }
+        }
+        return k;
+    }
     double gam = dot(h->r, u, n, tmp), del = dot(w, u, n, tmp), rho = bb2;
     double gam_prev = 1.0, alpha_prev = 1.0;
     double tol2 = h->pcg_tol * h->pcg_tol * bb2;
