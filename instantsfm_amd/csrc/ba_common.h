@@ -24,6 +24,7 @@ struct CgBufs {
     double* hist;     // [maxit + 2][2]: alpha_i, gamma_i ; hist_bb at the end
     double* scal;     // [4]: alpha, beta, flag of the current recurrence step (written by k_cg_dots)
     int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
+    int* prog;        // host-mapped (two-level path): [0] iterations started, [1] status, [2] iterations, [3] coarse
 };
 
 

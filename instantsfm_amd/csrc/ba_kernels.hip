@@ -16,6 +16,8 @@
 // bitwise reproducible when desc.deterministic = 1 (the Schur row accumulation then uses one wave per row).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -1036,6 +1038,7 @@ struct insfm_ba {
     double* result = nullptr;
     int* flags = nullptr;
     double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
+    int* prog_host = nullptr;    // pinned, device-mapped: progress of the two-level CG (CgBufs::prog)
     std::vector<void*> allocs;
     // LM state
     double damping = 0.0, down = 0.0, loss = 0.0;
@@ -1448,6 +1451,62 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
         int it = 0;
         int* st = reinterpret_cast<int*>(h->host_res + 8);
+        if (h->tlon && h->prog_host) {
+            // Two-level path: no stream sync inside the CG.  k_tl_pc's lead workgroup publishes its progress into
+            // host-mapped memory; more iterations are enqueued while the GPU still has two or more pending, and the
+            // loop ends when the status word turns non-zero.  The few iterations enqueued past convergence exit at the
+            // device status flag.
+            volatile int* pg = h->prog_host;
+            pg[0] = pg[1] = pg[2] = pg[3] = 0;
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            auto enqueue = [&](int from, int to) -> int {
+                return with_D(D, [&](auto dc_) -> int {
+                    constexpr int DV = decltype(dc_)::value;
+                    for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
+                    return launch_err(h, "k_tl_pc/k_tl_pspmv");
+                });
+            };
+            rec(h, 8);
+            int enq = std::min(std::max(4, h->last_cg_iters + 2), maxit + 2);
+            if ((rc = enqueue(0, enq))) return rc;
+            long spins = 0;
+            for (;;) {
+                if (pg[1] != 0) break;
+                const int reached = pg[0];
+                if (enq < maxit + 2 && reached >= enq - 2) {
+                    const int to = std::min(enq + 4, maxit + 2);
+                    if ((rc = enqueue(enq, to))) return rc;
+                    enq = to;
+                    continue;
+                }
+                if ((++spins & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(h->stream);
+                    if (q == hipSuccess) {  // drained: everything enqueued has run
+                        std::atomic_thread_fence(std::memory_order_seq_cst);
+                        if (pg[1] != 0) break;
+                        if (enq >= maxit + 2) break;
+                        const int to = std::min(enq + 8, maxit + 2);
+                        if ((rc = enqueue(enq, to))) return rc;
+                        enq = to;
+                    } else if (q != hipErrorNotReady) {
+                        h->err = std::string("PCG: ") + hipGetErrorString(q);
+                        return INSFM_BA_EHIP;
+                    }
+                }
+#if defined(__x86_64__)
+                __builtin_ia32_pause();
+#endif
+            }
+            std::atomic_thread_fence(std::memory_order_seq_cst);
+            rec(h, 9);
+            if (h->timing) {
+                HIPCHK(hipStreamSynchronize(h->stream));
+                acc_time(h, 8, 9, 5);
+            }
+            h->cg_launches += enq;
+            st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
+            it = enq;
+        } else
         for (;;) {
             // the count grows by a few iterations per LM step as the damping drops: launch past the last count so most
             // solves need one host poll (a converged iteration costs ~1 us per launch: its kernels exit at the flag)
@@ -1666,6 +1725,7 @@ void insfm_ba_destroy(insfm_ba* h) {
     if (h->side) (void)hipStreamSynchronize(h->side);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->host_res) (void)hipHostFree(h->host_res);
+    if (h->prog_host) (void)hipHostFree(h->prog_host);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->side) {
@@ -2108,6 +2168,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
         if ((rc = dd(&tl.u, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Zt, cd * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.Ztc, cd * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.vc, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
         if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
         if ((rc = dd(&tl.rowR, (size_t)C * MC))) return fail(rc, "");
@@ -2154,6 +2216,13 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             return 0;
         });
         h->tlon = true;
+        void* pm = nullptr;
+        if (hipHostMalloc(&pm, sizeof(int) * 4, hipHostMallocMapped) == hipSuccess) {
+            h->prog_host = static_cast<int*>(pm);
+            void* dp = nullptr;
+            if (hipHostGetDevicePointer(&dp, pm, 0) == hipSuccess) h->cg.prog = static_cast<int*>(dp);
+            else { (void)hipHostFree(pm); h->prog_host = nullptr; }
+        }
     }
     if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
     if (const char* ts = std::getenv("INSFM_TL_SYNC")) h->tl_sync = std::atoi(ts) != 0;
@@ -2317,6 +2386,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 9: src = h->tl.u; n = h->tlon ? C * D : 0; break;
         case 10: src = h->cg.w[0]; n = C * D; break;
         case 11: src = h->tl.rowR; n = h->tlon ? C * (D + 1) : 0; break;  // restriction row partials
+        case 22: src = h->tl.Rc; n = h->tlon ? (size_t)h->tl.m : 0; break;  // k_tl_pc phase timestamps (PC_TRACE)
         case 12: src = h->Einvbuf[0]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 13: src = h->Einvbuf[1]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 14: src = h->tl.gd; n = h->tlon ? 2 * C : 0; break;

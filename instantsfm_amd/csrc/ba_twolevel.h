@@ -32,6 +32,8 @@ constexpr int kPS = kNB + 1;     // padded LDS row stride (odd: conflict-free co
 struct TlBufs {
     double* u;           // [C*D]  preconditioned residual
     double* Zt;          // [C][D][MC]
+    double* Ztc;         // [C][D][MC] the same rows in cluster-member order (cpos)
+    double* vc;          // [C][D] the vector k_tl_pc reads (r0 at setup, w after), rows in cluster-member order
     double* Rc;          // [m]   (debug) restriction
     double* gd;          // [3C]  row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2  (k_tl_pspmv)
     double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
@@ -114,6 +116,7 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
 #pragma unroll
         for (int l = a; l < D; ++l) s += L[l * D + a] * col[l];
         tl.Zt[((size_t)i * D + a) * MC + k] = s;
+        tl.Ztc[((size_t)tl.cpos[i] * D + a) * MC + k] = s;
     }
 }
 
@@ -493,6 +496,7 @@ __global__ __launch_bounds__(kThreads) void k_tl_rrest(int C, CgBufs cg, TlBufs 
 #pragma unroll
     for (int a = 0; a < D; ++a) s += Z[a * MC] * r[a];
     tl.rowR[(size_t)tl.cpos[i] * MC + k] = s;
+    if (k < D) tl.vc[(size_t)tl.cpos[i] * D + k] = r[k];
 }
 
 // Copy n doubles global -> LDS: U loads per thread in flight before their LDS stores (a plain strided loop waits for
@@ -528,51 +532,78 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     __shared__ double red[3][kCgWaves];
     __shared__ double sc[3];
     if (cg.status[0] != 0) return;
+#ifdef PC_TRACE
+#define PCT(k) if (blockIdx.x == 0 && threadIdx.x == 0 && it == 3) tl.Rc[k] = (double)wall_clock64();
+#else
+#define PCT(k)
+#endif
+    PCT(0)
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c = blockIdx.x, m = tl.m;
     const bool setup = it < 0, use = tl.ok[0] != 0;
     const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
-    if (setup && c == 0 && t == 0) cg.status[2] = tl.ok[0];  // reported as insfm_ba_stats.coarse_used
-    // every global load that does not depend on a reduction is issued before the first wait: the cluster's first row
-    // entry (a two-load chain: issued first), the scalar partials, the recurrence history, the restriction entry's
-    // member range, this cluster's E^-1 rows and the first pass of the restriction partials
-    const double* src = setup ? cg.r[0] : cg.w[0];
+    if (setup && c == 0 && t == 0) {
+        cg.status[2] = tl.ok[0];  // reported as insfm_ba_stats.coarse_used
+        if (cg.prog) __hip_atomic_store(cg.prog + 3, tl.ok[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // every global load that does not depend on a reduction is issued before the first wait (s_waitcnt retires loads
+    // in issue order, so anything consumed early -- the scalar partials -- is loaded last): this cluster's E^-1 rows
+    // and the first pass of the restriction partials (registers, stored to LDS below), the cluster's rows of the
+    // source vector and of Z~ (cluster-ordered copies: no index load in front), history, member ranges, partials
+    constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32;
+    const int np = (C + prows - 1) / prows;
+    const int nlr0 = min(C, prows) * MC;
+    double ev[UE], lrv[UR];
+    if (use) {
+#pragma unroll
+        for (int u = 0; u < UE; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < MC * m) ev[u] = Einv[(size_t)c * MC * m + q];
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < nlr0) lrv[u] = tl.rowR[q];
+        }
+    }
     const bool pon = t < ne * D;
     size_t pidx = 0;
     double vp = 0.0, Zq[MC];
-    if (pon) {
-        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;
-        vp = src[pidx];
+    if (pon) {  // the cluster's rows are contiguous in the cluster-ordered copies
+        const size_t ci = (size_t)e0 * D + t;
+        vp = tl.vc[ci];
         if (use) {
 #pragma unroll
-            for (int k = 0; k < MC; ++k) Zq[k] = tl.Zt[pidx * MC + k];
+            for (int k = 0; k < MC; ++k) Zq[k] = tl.Ztc[ci * MC + k];
         }
+        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;  // only the output store waits for it
     }
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    if (!setup)
-        for (int k = t; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
     double h_alpha = 1.0, h_gam = 1.0, h_bb = 0.0;
     if (!setup && t == 0) {
         if (it >= 1) { h_alpha = cg.hist[2 * (it - 1)]; h_gam = cg.hist[2 * (it - 1) + 1]; h_bb = cg.hist[2 * (maxit + 1)]; }
     }
     int rb0 = 0, rb1 = 0;
     if (use && t < m) { rb0 = tl.cl_ptr[t / MC]; rb1 = tl.cl_ptr[t / MC + 1]; }
-    const int np = (C + prows - 1) / prows;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (!setup) {
+#pragma unroll 4
+        for (int k = t; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
+    }
     if (use) {
-        constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads;
-        double ev[UE];
-#pragma unroll
-        for (int u = 0; u < UE; ++u) {
-            const int q = t + u * kCgThreads;
-            if (q < MC * m) ev[u] = Einv[(size_t)c * MC * m + q];
-        }
-        stage_lds<kCgThreads, 16>(LR, tl.rowR, min(C, prows) * MC);
 #pragma unroll
         for (int u = 0; u < UE; ++u) {
             const int q = t + u * kCgThreads;
             if (q < MC * m) EL[q] = ev[u];
         }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < nlr0) LR[q] = lrv[u];
+        }
+        if (nlr0 > UR * kCgThreads) stage_lds<kCgThreads, 16>(LR + UR * kCgThreads, tl.rowR + UR * kCgThreads,
+                                                                nlr0 - UR * kCgThreads);
     }
+    PCT(1)
     if (!setup) {
         const int i = it;
         g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
@@ -584,19 +615,32 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
             const double bb = (i == 0) ? rho : h_bb;
             double flag = 0.0;
             const bool lead = blockIdx.x == 0;
+            int done = 0;
             if (rho <= tol2_rel * bb || i >= maxit) {
                 flag = 1.0;
-                if (lead) { cg.status[1] = i; __threadfence(); cg.status[0] = 1; }
+                done = 1;
             } else {
                 const double bev = (i == 0) ? 0.0 : gam / h_gam;
                 const double den = (i == 0) ? del : del - bev * gam / h_alpha;
                 if (!(den > 0.0)) {
                     flag = 2.0;
-                    if (lead) { cg.status[1] = i; __threadfence(); cg.status[0] = 2; }
+                    done = 2;
                 } else if (lead) {
                     cg.hist[2 * i] = gam / den;
                     cg.hist[2 * i + 1] = gam;
                     if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
+                }
+            }
+            if (lead) {
+                if (done) { cg.status[1] = i; __threadfence(); cg.status[0] = done; }
+                // progress for the host, which enqueues more iterations without a stream sync (system-scope stores)
+                if (cg.prog) {
+                    if (done) {
+                        __hip_atomic_store(cg.prog + 2, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(cg.prog + 1, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                    } else {
+                        __hip_atomic_store(cg.prog + 0, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 }
             }
             sc[0] = flag;
@@ -604,13 +648,14 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         __syncthreads();
         if (sc[0] != 0.0) return;
     }
+    PCT(2)
     if (use) {
         // full restriction: entry (c', k) sums the row partials of cluster c' in ascending camera order (from LDS)
         for (int pass = 0; pass < np; ++pass) {
             const int r0 = pass * prows, r1 = min(C, r0 + prows);
             if (pass > 0) {
                 __syncthreads();
-                stage_lds<kCgThreads, 16>(LR, tl.rowR + (size_t)r0 * MC, (r1 - r0) * MC);
+                stage_lds<kCgThreads, 32>(LR, tl.rowR + (size_t)r0 * MC, (r1 - r0) * MC);
             }
             __syncthreads();
             for (int e = t; e < m; e += kCgThreads) {
@@ -623,6 +668,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
             }
         }
         __syncthreads();
+        PCT(3)
         constexpr int KPW = (MC + kCgWaves - 1) / kCgWaves, LPL = (kCoarseMax + 63) / 64;
         double sy[KPW];
 #pragma unroll
@@ -647,13 +693,14 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         __syncthreads();
     }
+    PCT(4)
     double* dst = setup ? tl.u : cg.s[1];
     for (int e = t; e < ne * D; e += kCgThreads) {
         const bool first = e == t;
         const size_t idx = first ? pidx : (size_t)tl.cl_cams[e0 + e / D] * D + e % D;
-        double v = first ? vp : src[idx];
+        double v = first ? vp : tl.vc[(size_t)e0 * D + e];
         if (use) {
-            const double* Z = tl.Zt + idx * MC;
+            const double* Z = tl.Ztc + ((size_t)e0 * D + e) * MC;
             double sz = 0.0;
 #pragma unroll
             for (int k = 0; k < MC; ++k) sz += (first ? Zq[k] : Z[k]) * y[k];
@@ -661,6 +708,8 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         dst[idx] = v;
     }
+    PCT(5)
+#undef PCT
 }
 
 // One camera row per 512-thread workgroup: the product with S~ (row-contiguous Sn stream), the row's vector updates
@@ -766,6 +815,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const in
         }
         sv[0][a] = r_;
         sv[1][a] = w_;
+        tl.vc[(size_t)tl.cpos[row] * D + a] = w_;
         g0 = r_ * u_;
         g1 = w_ * u_;
     }
