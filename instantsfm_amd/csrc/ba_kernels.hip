@@ -265,6 +265,85 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ c
     }
 }
 
+// Register form of k_lin_cams for D <= 9 (D(D+1)/2 + D accumulators per thread): one workgroup per camera, thread t
+// evaluates observations t, t + 256, ... of the camera and keeps its own partial sums of the upper triangle of U and
+// of g_c in registers (no per-batch LDS round trip, no 256-long dependent add chain per entry); the partials are then
+// summed by a fixed butterfly per wave and the 4 wave sums in wave order, and U is written with both triangles from
+// the upper one (a product commutes exactly, so U stays exactly symmetric).  Same point / uv pipeline as k_lin_cams.
+template <int M>
+__global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict__ cam_ptr, const int* __restrict__ cm_pt,
+                                                           const double* __restrict__ cm_uv, const double* __restrict__ pp,
+                                                           const double* __restrict__ cams, const double* __restrict__ pts,
+                                                           double delta, double* __restrict__ U, double* __restrict__ gc) {
+    constexpr int D = kD<M>, ST = kStride<M>, NU = D * (D + 1) / 2, NE = NU + D;
+    static_assert(D <= 9, "register accumulation is sized for D <= 9");
+    __shared__ double red[kWaves][NE];
+    const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int eb = cam_ptr[c], ee = cam_ptr[c + 1];
+    const double2* uv2 = reinterpret_cast<const double2*>(cm_uv);
+    double camv[ST];
+#pragma unroll
+    for (int k = 0; k < ST; ++k) camv[k] = cams[(size_t)c * ST + k];
+    const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+    double acc[NE];
+#pragma unroll
+    for (int m = 0; m < NE; ++m) acc[m] = 0.0;
+    double X[3] = {0.0, 0.0, 0.0};
+    double2 z = make_double2(0.0, 0.0), zn = z, znn = z;
+    int pn = 0, pnn = 0;
+    {
+        const int e0 = eb + t, e1 = e0 + kThreads;
+        if (e0 < ee) {
+            const int p0 = cm_pt[e0];
+            z = uv2[e0];
+            X[0] = pts[3 * (size_t)p0]; X[1] = pts[3 * (size_t)p0 + 1]; X[2] = pts[3 * (size_t)p0 + 2];
+        }
+        if (e1 < ee) { pn = cm_pt[e1]; zn = uv2[e1]; }
+    }
+    for (int e = eb + t; e < ee; e += kThreads) {
+        const bool hn = e + kThreads < ee, hnn = e + 2 * kThreads < ee;
+        double Xn[3] = {0.0, 0.0, 0.0};
+        if (hn) { Xn[0] = pts[3 * (size_t)pn]; Xn[1] = pts[3 * (size_t)pn + 1]; Xn[2] = pts[3 * (size_t)pn + 2]; }
+        if (hnn) { pnn = cm_pt[e + 2 * kThreads]; znn = uv2[e + 2 * kThreads]; }
+        const double uvo[2] = {z.x, z.y};
+        double r[2], Jc[2][D], Jp[2][3];
+        eval_obs<M, true>(camv, X, ppc, uvo, r, Jc, Jp);
+        const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+#pragma unroll
+        for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
+        r[0] *= sw; r[1] *= sw;
+        int m = 0;
+#pragma unroll
+        for (int a = 0; a < D; ++a)
+#pragma unroll
+            for (int b = a; b < D; ++b, ++m) acc[m] += Jc[0][a] * Jc[0][b] + Jc[1][a] * Jc[1][b];
+#pragma unroll
+        for (int a = 0; a < D; ++a) acc[NU + a] -= Jc[0][a] * r[0] + Jc[1][a] * r[1];
+        X[0] = Xn[0]; X[1] = Xn[1]; X[2] = Xn[2];
+        z = zn; pn = pnn; zn = znn;
+    }
+#pragma unroll
+    for (int m = 0; m < NE; ++m) {
+        const double v = wave_sum(acc[m]);
+        if (lane == 0) red[wv][m] = v;
+    }
+    __syncthreads();
+    for (int m = t; m < NE; m += kThreads) {
+        double s = red[0][m];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) s += red[w][m];
+        if (m < NU) {
+            int a = 0, rem = m;
+            while (rem >= D - a) { rem -= D - a; ++a; }
+            const int b = a + rem;
+            U[(size_t)c * D * D + a * D + b] = s;
+            U[(size_t)c * D * D + b * D + a] = s;
+        } else {
+            gc[(size_t)c * D + (m - NU)] = s;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // per-trial point preparation
 // ------------------------------------------------------------------------------------------------------------
@@ -1283,6 +1362,14 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         if (h->Pl > 0)
             k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
                                                                  pts_local, h->d.huber_delta, h->W, h->V, h->gp);
+        static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
+        if constexpr (D <= 9) {
+            if (!batch_form) {
+                k_lin_cams_reg<M><<<h->C, kThreads, 0, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams,
+                                                                    pts_local, h->d.huber_delta, h->U, h->gc);
+                return launch_err(h, "linearize");
+            }
+        }
         const size_t lds = sizeof(double) * kThreads * (2 * D + 2);
         k_lin_cams<M><<<h->C, kThreads, lds, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams, pts_local,
                                                           h->d.huber_delta, h->U, h->gc);
@@ -2187,7 +2274,13 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         hipError_t e = hipMemsetAsync(h->Linvbuf[0], 0, sizeof(double) * (size_t)m * m, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->Linvbuf[1], 0, sizeof(double) * (size_t)m * m, h->stream);
         if (e == hipSuccess) e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
-        if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking);
+        // The side stream (E build + factorization, off the critical path) runs at the lowest priority, so its
+        // workgroups do not take CUs from the CG iterations that overlap it.  INSFM_SIDE_PRIO overrides (experiments).
+        int prio_lo = 0, prio_hi = 0;
+        if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+        const char* sp = std::getenv("INSFM_SIDE_PRIO");
+        const int side_prio = sp ? std::atoi(sp) : prio_lo;
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_built, hipEventDisableTiming);
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);

@@ -757,25 +757,42 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const in
     double acc[PPL];
 #pragma unroll
     for (int q = 0; q < PPL; ++q) acc[q] = 0.0;
-    for (int nn = n0 + slot; lane_on && nn < n1; nn += BPR) {
-        const int j = nbr_j[nn];
+    // The lane's blocks are rounds k = 0, 1, ... of the row (nn = n0 + slot + k * BPR), taken RG rounds at a time:
+    // the RG neighbour indices are loaded together, then every Sn piece and vector entry of the group, with the indices
+    // of rounds past the row's end clamped to its last block (valid addresses, no branch around the loads, so the
+    // whole group is in flight at once) and their products dropped by a select.  Sums stay in round order.
+    constexpr int RG = 8;
+    for (int base = n0 + slot; lane_on && base < n1; base += RG * BPR) {
+        int jr[RG];
 #pragma unroll
-        for (int q = 0; q < PPL; ++q) {
-            const int pc = pc0 + 64 * q;
-            if (pc >= PPB) continue;
-            const int bcol = 2 * (pc % HP);
-            const double2 svv = *reinterpret_cast<const double2*>(Sn + ((size_t)nn * D * DP + 2 * (size_t)pc));
-            const size_t jx = (size_t)j * D + bcol;
-            double u0, u1;
-            if constexpr ((D & 1) == 0) {
-                const double2 uv = *reinterpret_cast<const double2*>(v + jx);
-                u0 = uv.x; u1 = uv.y;
-            } else {
-                u0 = v[jx];
-                u1 = (bcol + 1 < D) ? v[jx + 1] : 0.0;
+        for (int r = 0; r < RG; ++r) jr[r] = nbr_j[min(base + r * BPR, n1 - 1)];
+        double2 sg[RG][PPL], ug[RG][PPL];
+#pragma unroll
+        for (int r = 0; r < RG; ++r) {
+            const size_t nn = (size_t)min(base + r * BPR, n1 - 1);
+#pragma unroll
+            for (int q = 0; q < PPL; ++q) {
+                const int pc = min(pc0 + 64 * q, PPB - 1);
+                const int bcol = 2 * (pc % HP);
+                sg[r][q] = *reinterpret_cast<const double2*>(Sn + (nn * D * DP + 2 * (size_t)pc));
+                const size_t jx = (size_t)jr[r] * D + bcol;
+                if constexpr ((D & 1) == 0) {
+                    ug[r][q] = *reinterpret_cast<const double2*>(v + jx);
+                } else {
+                    ug[r][q].x = v[jx];
+                    ug[r][q].y = v[jx + (bcol + 1 < D ? 1 : 0)];
+                }
             }
-            acc[q] += svv.x * u0 + svv.y * u1;
         }
+#pragma unroll
+        for (int r = 0; r < RG; ++r)
+#pragma unroll
+            for (int q = 0; q < PPL; ++q) {
+                const int pc = pc0 + 64 * q;
+                const double u1 = ((D & 1) == 0 || 2 * (pc % HP) + 1 < D) ? ug[r][q].y : 0.0;
+                const double t2 = sg[r][q].x * ug[r][q].x + sg[r][q].y * u1;
+                if (base + r * BPR < n1 && pc < PPB) acc[q] += t2;
+            }
     }
     if (lane_on) {
 #pragma unroll
