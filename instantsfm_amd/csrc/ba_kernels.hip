@@ -1453,10 +1453,10 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_rrest<D><<<cdiv((long long)h->C * (D + 1), kThreads), kThreads, 0, h->stream>>>(h->C, h->cg, h->tl);
         k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
-        k_tl_pspmv<D><<<h->C, kCgThreads, 0, h->stream>>>(-1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
+        k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
     }
     k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
-    k_tl_pspmv<D><<<h->C, kCgThreads, 0, h->stream>>>(it, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
+    k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
 }
 
 // k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
@@ -2422,7 +2422,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             if (which == 2) {
                 launch_tl_iter<DV>(h, 1, h->d.pcg_max_iter, 0.0);
             } else if (which == 3) {
-                k_tl_pspmv<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
+                k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
                                                                    h->tl);
             } else if (which == 4) {
                 int rc2 = run_tl_basis(h, h->cams_cur, h->stream);

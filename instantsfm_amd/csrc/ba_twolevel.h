@@ -714,13 +714,22 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
 
 // One camera row per 512-thread workgroup: the product with S~ (row-contiguous Sn stream), the row's vector updates
 // and its partials for the next iteration (setup: w0 = S~ u0 and the partials of iteration 0).
-template <int D>
-__global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const int* __restrict__ nbr_ptr,
-                                                         const int* __restrict__ nbr_j, const double* __restrict__ Sn,
-                                                         const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
+// NT threads per workgroup: at 256, the 1000 rows of config 3 (4 waves each) are all resident at once at <= 128 VGPRs.
+#ifndef PSPMV_NT
+#define PSPMV_NT 256
+#endif
+#ifndef PSPMV_RG
+#define PSPMV_RG 8
+#endif
+constexpr int kPspmvThreads = PSPMV_NT;
+template <int D, int NT = kPspmvThreads>
+__global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, const int* __restrict__ nbr_ptr,
+                                                 const int* __restrict__ nbr_j, const double* __restrict__ Sn,
+                                                 const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
     using G = CgGeom<D>;
-    constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = G::BPR, MC = D + 1;
-    __shared__ double red[kCgWaves][BPW][PPB];
+    constexpr int NW = NT / 64;
+    constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = BPW * NW, MC = D + 1;
+    __shared__ double red[NW][BPW][PPB];
     __shared__ double sv[2][D];  // r and w of the row after the update
     if (cg.status[0] != 0) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -761,7 +770,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const in
     // the RG neighbour indices are loaded together, then every Sn piece and vector entry of the group, with the indices
     // of rounds past the row's end clamped to its last block (valid addresses, no branch around the loads, so the
     // whole group is in flight at once) and their products dropped by a select.  Sums stay in round order.
-    constexpr int RG = 8;
+    constexpr int RG = PSPMV_RG;
     for (int base = n0 + slot; lane_on && base < n1; base += RG * BPR) {
         int jr[RG];
 #pragma unroll
@@ -807,7 +816,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pspmv(int it, int C, const in
     if (lane < D) {
         const int a = lane;
         double tot = 0.0;
-        for (int w = 0; w < kCgWaves; ++w)
+        for (int w = 0; w < NW; ++w)
 #pragma unroll
             for (int bb = 0; bb < BPW; ++bb)
 #pragma unroll
