@@ -988,6 +988,80 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub(const int* __restrict__
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
 }
 
+// The same back-substitution with W_o^T dc re-derived from the observation instead of read from W: J~ is evaluated
+// again at the linearization point exactly as k_lin_points does (same inputs, same code: the same J~c, J~p) and
+// q_o = J~p^T (J~c dc).  It reads ~50 B per observation (uv, camera / point index, the run's points) instead of the
+// 192-B W record, and the evaluation costs less than the record's HBM time.
+template <int M>
+__global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
+                                                            const int* __restrict__ cam, const int* __restrict__ ptl,
+                                                            const double* __restrict__ uv, const double* __restrict__ pp,
+                                                            const double* __restrict__ cams, double delta,
+                                                            const double* __restrict__ dc, const double* __restrict__ V,
+                                                            const double* __restrict__ Vinv, const double* __restrict__ gp,
+                                                            const double* __restrict__ pts, double* __restrict__ dp,
+                                                            double* __restrict__ pts_new, double* __restrict__ part) {
+    constexpr int D = kD<M>, ST = kStride<M>;
+    __shared__ double red[kLinThreads];
+    __shared__ double q[kLinThreads][3];
+    const int t = threadIdx.x;
+    const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
+    const int p = tb + t;
+    const bool own = p < te;
+    double gain[1] = {0.0};
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
+    if (own) { t0 = gp[3 * (size_t)p]; t1 = gp[3 * (size_t)p + 1]; t2 = gp[3 * (size_t)p + 2]; }
+    if (dc) {
+        const int ob = pt_ptr[tb], oe = pt_ptr[te];
+        const int lo = own ? pt_ptr[p] : 0, hi = own ? pt_ptr[p + 1] : 0;
+        for (int base = ob; base < oe; base += kLinThreads) {
+            const int n = min(kLinThreads, oe - base);
+            if (t < n) {
+                const int o = base + t;
+                const int c = cam[o], pl = ptl[o];
+                const double X[3] = {pts[3 * (size_t)pl], pts[3 * (size_t)pl + 1], pts[3 * (size_t)pl + 2]};
+                const double2 z = reinterpret_cast<const double2*>(uv)[o];
+                const double uvo[2] = {z.x, z.y};
+                const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+                double d[D];
+                const double* dr = dc + (size_t)c * D;
+#pragma unroll
+                for (int a = 0; a < D; ++a) d[a] = dr[a];
+                double r[2], Jc[2][D], Jp[2][3];
+                eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
+                const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+                double e0 = 0.0, e1 = 0.0;
+#pragma unroll
+                for (int a = 0; a < D; ++a) { e0 += (Jc[0][a] * sw) * d[a]; e1 += (Jc[1][a] * sw) * d[a]; }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) q[t][k] = (Jp[0][k] * sw) * e0 + (Jp[1][k] * sw) * e1;
+            }
+            __syncthreads();
+            for (int o = max(lo, base); o < min(hi, base + n); ++o) {
+                t0 -= q[o - base][0]; t1 -= q[o - base][1]; t2 -= q[o - base][2];
+            }
+            __syncthreads();
+        }
+    }
+    if (own) {
+        const double* vi = Vinv + 6 * (size_t)p;
+        const double d0 = vi[0] * t0 + vi[1] * t1 + vi[2] * t2;
+        const double d1 = vi[1] * t0 + vi[3] * t1 + vi[4] * t2;
+        const double d2 = vi[2] * t0 + vi[4] * t1 + vi[5] * t2;
+        dp[3 * (size_t)p] = d0; dp[3 * (size_t)p + 1] = d1; dp[3 * (size_t)p + 2] = d2;
+        pts_new[3 * (size_t)p] = pts[3 * (size_t)p] + d0;
+        pts_new[3 * (size_t)p + 1] = pts[3 * (size_t)p + 1] + d1;
+        pts_new[3 * (size_t)p + 2] = pts[3 * (size_t)p + 2] + d2;
+        const double* v = V + 6 * (size_t)p;
+        const double Vd0 = v[0] * d0 + v[1] * d1 + v[2] * d2;
+        const double Vd1 = v[1] * d0 + v[3] * d1 + v[4] * d2;
+        const double Vd2 = v[2] * d0 + v[4] * d1 + v[5] * d2;
+        gain[0] = 2.0 * (t0 * d0 + t1 * d1 + t2 * d2) - (d0 * Vd0 + d1 * Vd1 + d2 * Vd2);
+    }
+    block_sum<1, kLinThreads>(gain, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
+}
+
 // Cameras: X <- Exp(dc_pose) X, intrinsics += dc_intr; gain part 2 g_c.dc - dc^T U dc (rank 0 only).
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_update_cams(int C, const double* __restrict__ cams, const double* __restrict__ dc,
@@ -1651,12 +1725,20 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (rc) return rc;
         return iters;
     }
-    int rc = with_D(D, [&](auto dc_) -> int {
+    static const bool backsub_w = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
+    int rc = backsub_w ? with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (h->Pl > 0)
             k_backsub<DV><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->W, dcp, h->V, h->Vinv,
                                                                   h->gp, pts_local, h->dp, h->pts_new, h->part_gp);
         return launch_err(h, "k_backsub");
+    }) : with_model(h->model, [&](auto mc) -> int {
+        constexpr int M = decltype(mc)::value;
+        if (h->Pl > 0)
+            k_backsub_rc<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
+                                                                     cams, h->d.huber_delta, dcp, h->V, h->Vinv, h->gp,
+                                                                     pts_local, h->dp, h->pts_new, h->part_gp);
+        return launch_err(h, "k_backsub_rc");
     });
     if (rc) return rc;
     rc = with_model(h->model, [&](auto mc) -> int {

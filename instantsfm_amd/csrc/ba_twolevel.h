@@ -531,7 +531,6 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     __shared__ double y[MC];
     __shared__ double red[3][kCgWaves];
     __shared__ double sc[3];
-    if (cg.status[0] != 0) return;
 #ifdef PC_TRACE
 #define PCT(k) if (blockIdx.x == 0 && threadIdx.x == 0 && it == 3) tl.Rc[k] = (double)wall_clock64();
 #else
@@ -540,55 +539,60 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     PCT(0)
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c = blockIdx.x, m = tl.m;
-    const bool setup = it < 0, use = tl.ok[0] != 0;
-    const int e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
-    if (setup && c == 0 && t == 0) {
-        cg.status[2] = tl.ok[0];  // reported as insfm_ba_stats.coarse_used
-        if (cg.prog) __hip_atomic_store(cg.prog + 3, tl.ok[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    // every global load that does not depend on a reduction is issued before the first wait (s_waitcnt retires loads
-    // in issue order, so anything consumed early -- the scalar partials -- is loaded last): this cluster's E^-1 rows
-    // and the first pass of the restriction partials (registers, stored to LDS below), the cluster's rows of the
-    // source vector and of Z~ (cluster-ordered copies: no index load in front), history, member ranges, partials
+    const bool setup = it < 0;
+    // Every global load that does not depend on another is issued before the first wait (s_waitcnt retires loads in
+    // issue order): the status word (a launch past convergence returns before any store), the coarse flag, the
+    // cluster's member range, its E^-1 rows and the first pass of the restriction partials (registers, stored to LDS
+    // below; E^-1 is loaded even when the coarse correction is off -- the buffer always exists), history, member
+    // ranges and the scalar partials.  Only the cluster's rows of the source vector and of Z~ wait for the range.
+    const int st0 = cg.status[0];
+    const int okv = tl.ok[0];
+    const int e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
     constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32;
     const int np = (C + prows - 1) / prows;
     const int nlr0 = min(C, prows) * MC;
     double ev[UE], lrv[UR];
-    if (use) {
+    // branch-free: indices past the end are clamped to the last valid element (a load under a divergent branch is
+    // waited for at the branch's join, which would serialize the batch)
 #pragma unroll
-        for (int u = 0; u < UE; ++u) {
-            const int q = t + u * kCgThreads;
-            if (q < MC * m) ev[u] = Einv[(size_t)c * MC * m + q];
-        }
+    for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kCgThreads, MC * m - 1)];
 #pragma unroll
-        for (int u = 0; u < UR; ++u) {
-            const int q = t + u * kCgThreads;
-            if (q < nlr0) lrv[u] = tl.rowR[q];
-        }
-    }
-    const bool pon = t < ne * D;
-    size_t pidx = 0;
-    double vp = 0.0, Zq[MC];
-    if (pon) {  // the cluster's rows are contiguous in the cluster-ordered copies
-        const size_t ci = (size_t)e0 * D + t;
-        vp = tl.vc[ci];
-        if (use) {
-#pragma unroll
-            for (int k = 0; k < MC; ++k) Zq[k] = tl.Ztc[ci * MC + k];
-        }
-        pidx = (size_t)tl.cl_cams[e0 + t / D] * D + t % D;  // only the output store waits for it
-    }
-    double h_alpha = 1.0, h_gam = 1.0, h_bb = 0.0;
-    if (!setup && t == 0) {
-        if (it >= 1) { h_alpha = cg.hist[2 * (it - 1)]; h_gam = cg.hist[2 * (it - 1) + 1]; h_bb = cg.hist[2 * (maxit + 1)]; }
-    }
-    int rb0 = 0, rb1 = 0;
-    if (use && t < m) { rb0 = tl.cl_ptr[t / MC]; rb1 = tl.cl_ptr[t / MC + 1]; }
+    for (int u = 0; u < UR; ++u) lrv[u] = tl.rowR[min(t + u * kCgThreads, nlr0 - 1)];
+    const int ih = max(it - 1, 0);
+    const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
+    const int tc = min(t / MC, tl.nc - 1);
+    const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
     if (!setup) {
-#pragma unroll 4
-        for (int k = t; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
+        const int nk = (C + kCgThreads - 1) / kCgThreads;
+        for (int u0 = 0; u0 < nk; u0 += 4) {
+            double a0[4], a1[4], a2[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = min(t + (u0 + r) * kCgThreads, C - 1);
+                a0[r] = tl.gd[k]; a1[r] = tl.gd[C + k]; a2[r] = tl.gd[2 * C + k];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (t + (u0 + r) * kCgThreads < C) { g0 += a0[r]; g1 += a1[r]; g2 += a2[r]; }
+        }
     }
+    const int ne = e1 - e0;
+    if (st0 != 0 || ne < 0) return;  // (ne < 0 never holds: it makes the branch wait for the range loads as well)
+    const bool use = okv != 0;
+    if (setup && c == 0 && t == 0) {
+        cg.status[2] = okv;  // reported as insfm_ba_stats.coarse_used
+        if (cg.prog) __hip_atomic_store(cg.prog + 3, okv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const bool pon = t < ne * D;
+    const int tp = min(t, ne * D - 1);
+    // the cluster's rows are contiguous in the cluster-ordered copies
+    const size_t ci = (size_t)e0 * D + tp;
+    const double vp = tl.vc[ci];
+    double Zq[MC];
+#pragma unroll
+    for (int k = 0; k < MC; ++k) Zq[k] = tl.Ztc[ci * MC + k];
+    const size_t pidx = (size_t)tl.cl_cams[e0 + tp / D] * D + tp % D;  // only the output store waits for it
     if (use) {
 #pragma unroll
         for (int u = 0; u < UE; ++u) {
