@@ -53,22 +53,25 @@ constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (
 // ------------------------------------------------------------------------------------------------------------
 // reductions
 // ------------------------------------------------------------------------------------------------------------
-// Fixed-order block reduction of NV values per thread; result valid in thread 0 (and returned to all).
+// Fixed-order block reduction of NV values per thread, returned to every thread: a butterfly per wave, then the wave
+// sums in wave order (one barrier instead of one per tree level).
 template <int NV, int NT = kThreads>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= NT*NV doubles */) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= NV * NT / 64 doubles */) {
+    constexpr int NW = NT / 64;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) sh[k * NT + t] = v[k];
-    __syncthreads();
-    for (int s = NT / 2; s >= 1; s >>= 1) {
-        if (t < s) {
-#pragma unroll
-            for (int k = 0; k < NV; ++k) sh[k * NT + t] += sh[k * NT + t + s];
-        }
-        __syncthreads();
+    for (int k = 0; k < NV; ++k) {
+        const double s = wave_sum(v[k]);
+        if (lane == 0) sh[k * NW + wv] = s;
     }
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = sh[k * NT];
+    for (int k = 0; k < NV; ++k) {
+        double s = sh[k * NW];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s += sh[k * NW + w];
+        v[k] = s;
+    }
     __syncthreads();
 }
 
@@ -1100,14 +1103,14 @@ __global__ __launch_bounds__(kThreads) void k_update_cams(int C, const double* _
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
 }
 
-// Huber loss and sum ||r||^2 (block partials).
+// Huber loss and sum ||r||^2 (block partials).  (Measured: 4 observations per thread, loads hoisted, ran 25 -> 33 us.)
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
                                                    const double* __restrict__ uv, const double* __restrict__ pp,
                                                    const double* __restrict__ cams, const double* __restrict__ pts,
                                                    double delta, double* __restrict__ part) {
     constexpr int ST = kStride<M>;
-    __shared__ double red[2 * kThreads];
+    __shared__ double red[2 * kWaves];
     const int o = blockIdx.x * kThreads + threadIdx.x;
     double v[2] = {0.0, 0.0};
     if (o < Nl) {
@@ -1475,7 +1478,9 @@ int run_tl_build(insfm_ba* h, int slot, hipStream_t stream) {
     tl.E = h->Ebuf[slot];
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
-        k_tl_erow<DV><<<C, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
+        static const int grid_cap = [] { const char* e = std::getenv("INSFM_EROW_GRID"); return e ? std::atoi(e) : 256; }();
+        const int grid = (grid_cap > 0 && stream != h->stream) ? std::min(C, grid_cap) : C;
+        k_tl_erow<DV><<<grid, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
         k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, stream>>>(tl);
         return launch_err(h, "k_tl_erow/ereduce");
     });
@@ -2463,9 +2468,9 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
     if (pt_bytes) HIPCHK(hipMemcpyAsync(h->pts_cur, pts_user + 3 * (size_t)h->p0, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
     int rc = lm_step(h, st);
     if (rc) return rc;
+    // stream-ordered write-back (no host wait: the step's loss is already on the host)
     HIPCHK(hipMemcpyAsync(cams_user, h->cams_cur, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
     if (pt_bytes) HIPCHK(hipMemcpyAsync(pts_user + 3 * (size_t)h->p0, h->pts_cur, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
     return INSFM_BA_OK;
 }
 

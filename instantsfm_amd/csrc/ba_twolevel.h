@@ -141,7 +141,11 @@ __global__ __launch_bounds__(kThreads) void k_tl_erow(int C, const int* __restri
     double* Zj = Sb + CH * D * DP;            // [CH][D][MC]
     double* T = Zj + CH * D * MC;             // [CH][D][MC]
     double* acc = T + CH * D * MC;            // [nseg_row][MC][MC]
-    const int i = blockIdx.x, t = threadIdx.x;
+    const int t = threadIdx.x;
+    // rows strided over the grid: the side stream's launch is capped at a few workgroups so it does not take the CUs'
+    // LDS from the CG launches it overlaps (k_tl_pc needs a large LDS slice per workgroup)
+    for (int i = blockIdx.x; i < C; i += gridDim.x) {
+    __syncthreads();
     const int n0 = nbr_ptr[i], n1 = nbr_ptr[i + 1];
     const int s0 = tl.rseg_ptr[i], ns = tl.rseg_ptr[i + 1] - s0;
     const int nout = ns * MM;
@@ -194,6 +198,7 @@ __global__ __launch_bounds__(kThreads) void k_tl_erow(int C, const int* __restri
     }
     __syncthreads();
     for (int o = t; o < nout; o += kThreads) tl.Oseg[(size_t)s0 * MM + o] = acc[o];
+    }
 }
 
 // One thread per entry of E: fixed-order sum of the cluster pair's segments (rows ascending); an exactly-zero
