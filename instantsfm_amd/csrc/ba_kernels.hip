@@ -112,18 +112,21 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
                                                          double* __restrict__ gp) {
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
     // is longer), one thread per observation: coalesced uv / cam / point loads and 192-B W records written by
-    // consecutive lanes.  Each observation's V / g_p terms go to LDS and one thread per track adds them in observation
-    // order -- the same sequence of additions as a thread walking its track.
+    // consecutive lanes (16 B per lane).  Each observation's V / g_p terms go to LDS and one thread per track adds them
+    // in observation order -- the same sequence of additions as a thread walking its track.  The terms reuse the W
+    // staging area once the records are stored (one 25.6-KB LDS buffer: 6 workgroups per CU instead of 4).
     constexpr int D = kD<M>, ST = kStride<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride: no bank conflicts
-    __shared__ double ct[kLinThreads][9];
-    __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here
+    static_assert(WRP >= 9, "the V / g terms reuse a W staging row");
+    __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here; then the V / g terms
     const int t = threadIdx.x;
     const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
     const int ob = pt_ptr[tb], oe = pt_ptr[te];
     double Vs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int tr = tb + t;  // the track this thread sums (tracks of the run)
+    const int tlo = tr < te ? pt_ptr[tr] : 0, thi = tr < te ? pt_ptr[tr + 1] : 0;
     for (int base = ob; base < oe; base += kLinThreads) {
         const int o = base + t;
+        double cv[9];
         if (o < oe) {
             const int c = cam[o], p = ptl[o];
             const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
@@ -143,25 +146,40 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             for (int a = 0; a < D; ++a)
 #pragma unroll
                 for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
-            ct[t][0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
-            ct[t][1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
-            ct[t][2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
-            ct[t][3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
-            ct[t][4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
-            ct[t][5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+            cv[0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
+            cv[1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
+            cv[2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
+            cv[3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
+            cv[4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
+            cv[5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) ct[t][6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
+            for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
         }
         __syncthreads();
-        {   // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive doubles
-            const int n = min(kLinThreads, oe - base);
+        const int n = min(kLinThreads, oe - base);
+        if constexpr ((WR & 1) == 0) {
+            // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive
+            // 16-B pairs (WR even: a pair never crosses a record, and every record starts 16-B aligned)
+            double2* dst = reinterpret_cast<double2*>(W + (size_t)base * WR);
+            for (int k2 = t; k2 < n * (WR / 2); k2 += kLinThreads) {
+                const int k = 2 * k2, rec = k / WR, e = k - rec * WR;
+                const double* src = wst + rec * WRP + e;
+                dst[k2] = make_double2(src[0], src[1]);
+            }
+        } else {
             double* dst = W + (size_t)base * WR;
             for (int k = t; k < n * WR; k += kLinThreads) dst[k] = wst[(k / WR) * WRP + k % WR];
         }
+        __syncthreads();
+        if (o < oe) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) wst[(size_t)t * 9 + k] = cv[k];
+        }
+        __syncthreads();
         if (tr < te) {
-            const int lo = max(pt_ptr[tr], base), hi = min(pt_ptr[tr + 1], base + kLinThreads);
+            const int lo = max(tlo, base), hi = min(thi, base + kLinThreads);
             for (int q = lo; q < hi; ++q) {
-                const double* cq = ct[q - base];
+                const double* cq = wst + (size_t)(q - base) * 9;
 #pragma unroll
                 for (int k = 0; k < 6; ++k) Vs[k] += cq[k];
 #pragma unroll
@@ -1148,6 +1166,13 @@ __global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ c
     }
 }
 
+// flags[0..3] = 0, status[0..3] = 0
+__global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) {
+    const int t = threadIdx.x;
+    if (t < 4) flags[t] = 0;
+    else if (t < 8) status[t - 4] = 0;
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
@@ -1571,7 +1596,12 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
-    HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
+    // the non-PD flag and the CG status word, zeroed by one tiny launch (the runtime's fill kernel takes ~6 us each)
+    k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
+    {
+        const int rc0 = launch_err(h, "k_zero_words");
+        if (rc0) return rc0;
+    }
     const bool gpk = h->kind == 1;
     // global positioning: the scale-eliminated blocks are already damped, so k_schur takes U'/g'_c as they are
     const double* Uin = gpk ? h->Up : h->U;
@@ -1599,7 +1629,6 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         rec(h, 7);
         rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
         if (rc) return rc;
-        HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
         if (h->built_pending) {  // the side stream's E build of the previous solve still reads S~ / Z~
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_built, 0));
             h->built_pending = false;
