@@ -570,59 +570,71 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
 // ------------------------------------------------------------------------------------------------------------
 // PCG on the reduced camera system
 // ------------------------------------------------------------------------------------------------------------
-// One wave per camera: Cholesky S_ii = L L^T and L^-1 (lane 0 on an LDS copy), r0 = L^-1 b, zero p/x/s.
+// One wave per camera, in registers: lane r holds row r of S_ii and factors it right-looking (pivot and column
+// entries broadcast with readlane), so S_ii = L L^T costs D short steps instead of a lane-0 loop over LDS; lane c
+// then forms column c of L^-1 by forward substitution, and r0 = L^-1 b, zero p/x/s.  Same operations in the same
+// order as the left-looking entry-wise loops (a[c] -= L[r][j] L[c][j] for j ascending, L[r][c] = s / L[c][c],
+// I[r][c] = -sum_k L[r][k] I[k][c] / L[r][r]).
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, const double* __restrict__ S,
                                                         const double* __restrict__ b, double* __restrict__ Lf,
                                                         double* __restrict__ Li, CgBufs cg) {
     constexpr int DD = D * D;
-    __shared__ double A[kWaves][DD];
-    __shared__ double L[kWaves][DD];
-    __shared__ double I[kWaves][DD];
-    __shared__ int bad[kWaves];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = blockIdx.x * kWaves + wv;
     if (i >= C) return;
+    const int rl = min(lane, D - 1);
     const double* blk = S + (size_t)row_ptr[i] * DD;
-    for (int k = lane; k < DD; k += 64) { A[wv][k] = blk[k]; L[wv][k] = 0.0; I[wv][k] = 0.0; }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (lane == 0) {
-        int ok = 1;
-        for (int r = 0; r < D && ok; ++r)
-            for (int c = 0; c <= r; ++c) {
-                double s = A[wv][r * D + c];
-                for (int k = 0; k < c; ++k) s -= L[wv][r * D + k] * L[wv][c * D + k];
-                if (r == c) {
-                    if (!(s > 0.0)) { ok = 0; break; }
-                    L[wv][r * D + r] = sqrt(s);
-                } else {
-                    L[wv][r * D + c] = s / L[wv][c * D + c];
-                }
-            }
-        if (ok) {
-            for (int r = 0; r < D; ++r) {
-                I[wv][r * D + r] = 1.0 / L[wv][r * D + r];
-                for (int c = 0; c < r; ++c) {
-                    double s = 0.0;
-                    for (int k = c; k < r; ++k) s -= L[wv][r * D + k] * I[wv][k * D + c];
-                    I[wv][r * D + c] = s / L[wv][r * D + r];
-                }
-            }
-        } else {
-            atomicMax(cg.status, 2);
+    double a[D];
+#pragma unroll
+    for (int c = 0; c < D; ++c) a[c] = blk[rl * D + c];
+    const double bl = b[(size_t)i * D + rl];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        double piv = readlane_d(a[j], j);
+        if (!(piv > 0.0)) { ok = false; piv = 1.0; }
+        const double ljj = sqrt(piv);
+        const double lrj = (lane == j) ? ljj : ((lane > j) ? a[j] / ljj : 0.0);
+        a[j] = lrj;
+#pragma unroll
+        for (int c = j + 1; c < D; ++c) {
+            const double lcj = readlane_d(lrj, c);
+            if (lane >= c) a[c] -= lrj * lcj;
         }
-        bad[wv] = !ok;
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k = lane; k < DD; k += 64) { Lf[(size_t)i * DD + k] = L[wv][k]; Li[(size_t)i * DD + k] = I[wv][k]; }
+#pragma unroll
+    for (int c = 0; c < D; ++c)
+        if (c > lane) a[c] = 0.0;
+    // column `lane` of L^-1: x[r] = (delta_rc - sum_{k<r} L[r][k] x[k]) / L[r][r]
+    double x[D];
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        double s = 0.0;  // (x[k] = 0 for k < lane: those terms leave s unchanged)
+#pragma unroll
+        for (int k = 0; k < r; ++k) s -= readlane_d(a[k], r) * x[k];
+        x[r] = (r >= lane) ? ((r == lane) ? 1.0 / readlane_d(a[r], r) : s / readlane_d(a[r], r)) : 0.0;
+    }
+    if (!ok && lane == 0) atomicMax(cg.status, 2);
     if (lane < D) {
-        const int a = lane;
-        double s = 0.0;
-        for (int k = 0; k <= a; ++k) s += I[wv][a * D + k] * b[(size_t)i * D + k];
-        const size_t idx = (size_t)i * D + a;
-        cg.r[0][idx] = bad[wv] ? 0.0 : s;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            Lf[(size_t)i * DD + lane * D + c] = a[c];
+            Li[(size_t)i * DD + c * D + lane] = ok ? x[c] : 0.0;
+        }
+    }
+    // r0 = L^-1 b: row a of L^-1 is (x[a] of lanes 0..a)
+    double r0 = 0.0;
+#pragma unroll
+    for (int aa = 0; aa < D; ++aa) {
+        double sacc = 0.0;
+#pragma unroll
+        for (int k = 0; k <= aa; ++k) sacc += readlane_d(x[aa], k) * readlane_d(bl, k);
+        if (lane == aa) r0 = sacc;
+    }
+    if (lane < D) {
+        const size_t idx = (size_t)i * D + lane;
+        cg.r[0][idx] = ok ? r0 : 0.0;
         cg.r[1][idx] = 0.0;
         cg.w[0][idx] = 0.0; cg.w[1][idx] = 0.0;
         cg.s[0][idx] = 0.0; cg.s[1][idx] = 0.0;
