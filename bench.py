@@ -108,13 +108,19 @@ def run_gp(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
+    # INSFM_DIST_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share devices, the reduced
+    # system goes through host memory); the measured configuration is RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("INSFM_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     prob = make_gp_problem(1000, 200000, track_len=10, seed=args.seed, init="random")
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = GlobalPositioner(prob.trans, prob.cam_idx, prob.pt_idx, prob.fcam, prob.sfree, prob.n_cams, prob.n_points,
@@ -143,7 +149,7 @@ def run_gp(args):
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     final_loss, rmse = eng.cost(*par)
@@ -259,7 +265,7 @@ def run_tracks(args):
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     n_tracks, n_rows = int(counts[0]), int(counts[1])
@@ -471,13 +477,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
-    dev = torch.device("cuda", local)
+    # INSFM_DIST_BACKEND=gloo rehearses the N-rank path on a box with fewer GPUs (ranks share devices, the reduced
+    # system goes through host memory); the measured configuration is RCCL ("nccl"), one rank per GPU.
+    backend = os.environ.get("INSFM_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     prob = make_config(args.config, seed=args.seed)
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
@@ -509,7 +521,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     final_loss, rmse = eng.cost(cams, pts)
