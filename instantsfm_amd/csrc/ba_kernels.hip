@@ -1540,6 +1540,14 @@ int run_tl_factor(insfm_ba* h, int slot, hipStream_t stream) {
 // solve when this is the first solve after a linearization (it starts right away), otherwise at its own (it waits
 // for the factorization) -- the oracle's lag rule (ora_pcg).  The next solve's k_cg_scale / k_tl_basis overwrite
 // S~ / Z~, so they wait for ev_built (run_solve).
+#ifndef CG_AHEAD
+#define CG_AHEAD 2
+#endif
+#ifndef CG_INIT_BACK
+#define CG_INIT_BACK 2
+#endif
+constexpr int kCgAhead = CG_AHEAD;  // CG iterations the host keeps queued ahead of the device (pipelined two-level PCG)
+
 int run_tl_setup(insfm_ba* h, const double* cams) {
     const int slot = (int)(h->tl_solves & 1);
     hipStream_t fs = h->tl_sync ? h->stream : h->side;
@@ -1674,14 +1682,18 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 });
             };
             rec(h, 8);
-            int enq = std::min(std::max(4, h->last_cg_iters + 2), maxit + 2);
+            // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step);
+            // the loop below tops up one iteration at a time
+            int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
             if ((rc = enqueue(0, enq))) return rc;
             long spins = 0;
             for (;;) {
                 if (pg[1] != 0) break;
+                // keep about kCgAhead iterations queued, one at a time: every iteration queued past convergence
+                // costs ~10 us of early-exit launches (chunks of 4 left 5 such iterations per solve)
                 const int reached = pg[0];
-                if (enq < maxit + 2 && reached >= enq - 2) {
-                    const int to = std::min(enq + 4, maxit + 2);
+                if (enq < maxit + 2 && reached >= enq - kCgAhead) {
+                    const int to = std::min(enq + 1, maxit + 2);
                     if ((rc = enqueue(enq, to))) return rc;
                     enq = to;
                     continue;
