@@ -2399,7 +2399,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd(&tl.vc, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
         if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
-        if ((rc = dd(&tl.rowR, (size_t)C * MC))) return fail(rc, "");
+        if ((rc = dd(&tl.rowR, (size_t)C * MC + 2))) return fail(rc, "");  // +2: k_tl_pc reads it in 16-B pairs
         if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
         for (int sl = 0; sl < 2; ++sl) {
             if ((rc = dd(&h->Ebuf[sl], (size_t)m * m))) return fail(rc, "");

@@ -553,16 +553,18 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     const int st0 = cg.status[0];
     const int okv = tl.ok[0];
     const int e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
-    constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32;
+    constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32, UR2 = UR / 2;
     const int np = (C + prows - 1) / prows;
     const int nlr0 = min(C, prows) * MC;
-    double ev[UE], lrv[UR];
+    double ev[UE];
+    double2 lrv[UR2];  // restriction partials in 16-B pairs (rowR is 16-B aligned and padded by 2)
     // branch-free: indices past the end are clamped to the last valid element (a load under a divergent branch is
     // waited for at the branch's join, which would serialize the batch)
 #pragma unroll
     for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kCgThreads, MC * m - 1)];
 #pragma unroll
-    for (int u = 0; u < UR; ++u) lrv[u] = tl.rowR[min(t + u * kCgThreads, nlr0 - 1)];
+    for (int u = 0; u < UR2; ++u)
+        lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kCgThreads, (nlr0 - 1) / 2)];
     const int ih = max(it - 1, 0);
     const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
     const int tc = min(t / MC, tl.nc - 1);
@@ -605,9 +607,10 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
             if (q < MC * m) EL[q] = ev[u];
         }
 #pragma unroll
-        for (int u = 0; u < UR; ++u) {
-            const int q = t + u * kCgThreads;
-            if (q < nlr0) LR[q] = lrv[u];
+        for (int u = 0; u < UR2; ++u) {
+            const int q = 2 * (t + u * kCgThreads);
+            if (q < nlr0) LR[q] = lrv[u].x;
+            if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
         }
         if (nlr0 > UR * kCgThreads) stage_lds<kCgThreads, 16>(LR + UR * kCgThreads, tl.rowR + UR * kCgThreads,
                                                                 nlr0 - UR * kCgThreads);
