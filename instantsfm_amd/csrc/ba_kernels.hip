@@ -1212,6 +1212,7 @@ struct insfm_ba {
     double* Sn = nullptr;  // row-contiguous scaled neighbour blocks for the CG (both triangles, padded rows)
     int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
+    int nbr_stride = 0;  // > 0: every CG row has exactly nbr_stride neighbour slots (padded), row r starts at r * stride
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
@@ -1577,10 +1578,12 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_rrest<D><<<cdiv((long long)h->C * (D + 1), kThreads), kThreads, 0, h->stream>>>(h->C, h->cg, h->tl);
         k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
-        k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
+        k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
+                                                              h->cg, h->tl);
     }
     k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
-    k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg, h->tl);
+    k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
+                                                          h->cg, h->tl);
 }
 
 // k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
@@ -2113,6 +2116,34 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int k = lop[i]; k < lop[i + 1]; ++k) { plo[loblk[k]] = (int)nj.size(); nj.push_back(locol[k]); }
         nptr[i + 1] = (int)nj.size();
     }
+    // Equal-length rows (every row padded to the longest with zero blocks of neighbour = the row itself) when that
+    // costs at most 10 % more slots: the CG's product kernel then derives a row's range from its index instead of
+    // loading nbr_ptr first (one dependent memory round trip less per iteration).  The padded blocks stay zero (Sn is
+    // cleared at create and k_cg_scale never writes them), so every consumer of the lists may walk them unchanged.
+    {
+        int stride = 0;
+        for (int i = 0; i < C; ++i) stride = std::max(stride, nptr[i + 1] - nptr[i]);
+        const int64_t nn = (int64_t)nj.size();
+        if (stride > 0 && nn > 0 && (int64_t)C * stride * 10 <= nn * 11) {
+            std::vector<int> nj2((size_t)C * stride), nptr2(C + 1);
+            for (int i = 0; i < C; ++i) {
+                nptr2[i] = i * stride;
+                for (int q = nptr[i]; q < nptr[i + 1]; ++q) nj2[(size_t)i * stride + (q - nptr[i])] = nj[q];
+                for (int q = nptr[i + 1] - nptr[i]; q < stride; ++q) nj2[(size_t)i * stride + q] = i;
+            }
+            nptr2[C] = C * stride;
+            // remap the Sn slots of every upper block (row i = brow[e] for pos_up, row cols[e] for pos_lo)
+            for (int e = 0; e < h->nnzb; ++e) {
+                if (e == rptr[brow[e]]) continue;  // diagonal block: no slot
+                const int i = brow[e], j = cols[e];
+                pup[e] = i * stride + (pup[e] - nptr[i]);
+                plo[e] = j * stride + (plo[e] - nptr[j]);
+            }
+            nj.swap(nj2);
+            nptr.swap(nptr2);
+            h->nbr_stride = stride;
+        }
+    }
     h->n_nbr = (int64_t)nj.size();
     for (int i = 0; i < C; ++i) { pup[rptr[i]] = 0; plo[rptr[i]] = 0; }  // diagonal blocks: unused slots
     if (nj.empty()) nj.push_back(0);
@@ -2207,8 +2238,9 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = upload(h, &h->pos_lo, plo.data(), plo.size()))) return fail(rc, "");
     {
         const int DPd = D + (D & 1);
-        if ((rc = dalloc(h, (void**)&h->Sn, sizeof(double) * (size_t)std::max<int64_t>(h->n_nbr, 1) * D * DPd)))
-            return fail(rc, "");
+        const size_t snb = sizeof(double) * (size_t)std::max<int64_t>(h->n_nbr, 1) * D * DPd;
+        if ((rc = dalloc(h, (void**)&h->Sn, snb))) return fail(rc, "");
+        if (hipMemsetAsync(h->Sn, 0, snb, h->stream) != hipSuccess) return fail(INSFM_BA_EHIP, "Sn clear");
     }
     if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
     auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
@@ -2562,7 +2594,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             if (which == 2) {
                 launch_tl_iter<DV>(h, 1, h->d.pcg_max_iter, 0.0);
             } else if (which == 3) {
-                k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(1, h->C, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
+                k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
                                                                    h->tl);
             } else if (which == 4) {
                 int rc2 = run_tl_basis(h, h->cams_cur, h->stream);

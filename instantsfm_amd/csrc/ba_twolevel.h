@@ -735,7 +735,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
 #endif
 constexpr int kPspmvThreads = PSPMV_NT;
 template <int D, int NT = kPspmvThreads>
-__global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, const int* __restrict__ nbr_ptr,
+__global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, const int* __restrict__ nbr_ptr,
                                                  const int* __restrict__ nbr_j, const double* __restrict__ Sn,
                                                  const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
     using G = CgGeom<D>;
@@ -751,7 +751,8 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, const int* __res
     const int pc0 = (PPB <= 64) ? lane - bw * PPB : lane;
     const bool lane_on = (PPB <= 64) ? (bw < BPW) : true;
     const int slot = wv * BPW + bw;
-    const int n0 = nbr_ptr[row], n1 = nbr_ptr[row + 1];
+    // equal-length (padded) rows: the range follows from the row index, no load in front of the stream
+    const int n0 = stride > 0 ? row * stride : nbr_ptr[row], n1 = stride > 0 ? n0 + stride : nbr_ptr[row + 1];
     const double* v = setup ? tl.u : cg.s[1];
     // the row's own vector entries (independent of the product): in flight during the stream
     const size_t own = (size_t)row * D + (lane < D ? lane : 0);
