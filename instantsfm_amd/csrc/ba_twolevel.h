@@ -556,6 +556,19 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32, UR2 = UR / 2;
     const int np = (C + prows - 1) / prows;
     const int nlr0 = min(C, prows) * MC;
+    // the scalar partials and the history first: the recurrence scalars below wait only for them (loads retire in
+    // issue order), so that reduction overlaps the E^-1 / restriction batch still in flight
+    // the first GK partials per thread are held in registers and summed at the scalar phase (a summing loop here
+    // would wait for them before the batch below is issued); rows past GK * kCgThreads are summed there too
+    constexpr int GK = 2;
+    double ga0[GK], ga1[GK], ga2[GK];
+#pragma unroll
+    for (int r = 0; r < GK; ++r) {
+        const int k = min(t + r * kCgThreads, C - 1);
+        ga0[r] = tl.gd[k]; ga1[r] = tl.gd[C + k]; ga2[r] = tl.gd[2 * C + k];
+    }
+    const int ih = max(it - 1, 0);
+    const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
     double ev[UE];
     double2 lrv[UR2];  // restriction partials in 16-B pairs (rowR is 16-B aligned and padded by 2)
     // branch-free: indices past the end are clamped to the last valid element (a load under a divergent branch is
@@ -565,25 +578,8 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
 #pragma unroll
     for (int u = 0; u < UR2; ++u)
         lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kCgThreads, (nlr0 - 1) / 2)];
-    const int ih = max(it - 1, 0);
-    const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
     const int tc = min(t / MC, tl.nc - 1);
     const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
-    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    if (!setup) {
-        const int nk = (C + kCgThreads - 1) / kCgThreads;
-        for (int u0 = 0; u0 < nk; u0 += 4) {
-            double a0[4], a1[4], a2[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int k = min(t + (u0 + r) * kCgThreads, C - 1);
-                a0[r] = tl.gd[k]; a1[r] = tl.gd[C + k]; a2[r] = tl.gd[2 * C + k];
-            }
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (t + (u0 + r) * kCgThreads < C) { g0 += a0[r]; g1 += a1[r]; g2 += a2[r]; }
-        }
-    }
     const int ne = e1 - e0;
     if (st0 != 0 || ne < 0) return;  // (ne < 0 never holds: it makes the branch wait for the range loads as well)
     const bool use = okv != 0;
@@ -600,24 +596,14 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
 #pragma unroll
     for (int k = 0; k < MC; ++k) Zq[k] = tl.Ztc[ci * MC + k];
     const size_t pidx = (size_t)tl.cl_cams[e0 + tp / D] * D + tp % D;  // only the output store waits for it
-    if (use) {
-#pragma unroll
-        for (int u = 0; u < UE; ++u) {
-            const int q = t + u * kCgThreads;
-            if (q < MC * m) EL[q] = ev[u];
-        }
-#pragma unroll
-        for (int u = 0; u < UR2; ++u) {
-            const int q = 2 * (t + u * kCgThreads);
-            if (q < nlr0) LR[q] = lrv[u].x;
-            if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
-        }
-        if (nlr0 > UR * kCgThreads) stage_lds<kCgThreads, 16>(LR + UR * kCgThreads, tl.rowR + UR * kCgThreads,
-                                                                nlr0 - UR * kCgThreads);
-    }
     PCT(1)
     if (!setup) {
         const int i = it;
+        double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+#pragma unroll
+        for (int r = 0; r < GK; ++r)
+            if (t + r * kCgThreads < C) { g0 += ga0[r]; g1 += ga1[r]; g2 += ga2[r]; }
+        for (int k = t + GK * kCgThreads; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
         g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
         if (lane == 0) { red[0][wv] = g0; red[1][wv] = g1; red[2][wv] = g2; }
         __syncthreads();
@@ -659,6 +645,21 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         __syncthreads();
         if (sc[0] != 0.0) return;
+    }
+    if (use) {
+#pragma unroll
+        for (int u = 0; u < UE; ++u) {
+            const int q = t + u * kCgThreads;
+            if (q < MC * m) EL[q] = ev[u];
+        }
+#pragma unroll
+        for (int u = 0; u < UR2; ++u) {
+            const int q = 2 * (t + u * kCgThreads);
+            if (q < nlr0) LR[q] = lrv[u].x;
+            if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
+        }
+        if (nlr0 > UR * kCgThreads) stage_lds<kCgThreads, 16>(LR + UR * kCgThreads, tl.rowR + UR * kCgThreads,
+                                                                nlr0 - UR * kCgThreads);
     }
     PCT(2)
     if (use) {
