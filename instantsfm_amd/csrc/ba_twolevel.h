@@ -755,27 +755,28 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     // equal-length (padded) rows: the range follows from the row index, no load in front of the stream
     const int n0 = stride > 0 ? row * stride : nbr_ptr[row], n1 = stride > 0 ? n0 + stride : nbr_ptr[row + 1];
     const double* v = setup ? tl.u : cg.s[1];
-    // the row's own vector entries (independent of the product): in flight during the stream
-    const size_t own = (size_t)row * D + (lane < D ? lane : 0);
-    double vo = 0.0, u_ = 0.0, w_ = 0.0, r_ = 0.0, z_ = 0.0, q_ = 0.0, s_ = 0.0, p_ = 0.0, x_ = 0.0, al = 0.0, be = 0.0;
-    // wave 0's tail operands, independent of everything: row a of L (lanes < D) or column k of Z~ (lanes D..D+MC-1)
+    // The row's own vector entries and wave 0's tail operands (row a of L for lanes a < D, column k of Z~ for lanes
+    // D + k), independent of the product, are loaded by wave 0 under a wave-uniform branch with clamped lane
+    // indices: no lane divergence around the loads, so they stay in flight during wave 0's stream instead of being
+    // waited for before it.
+    const int la = min(lane, D - 1);
+    const size_t own = (size_t)row * D + la;
+    double vo = 0.0, u_ = 0.0, w_ = 0.0, r_ = 0.0, z_ = 0.0, q_ = 0.0, s_ = 0.0, p_ = 0.0, x_ = 0.0;
+    double al = 0.0, hg1 = 1.0, hg0 = 1.0;
     double tailop[D];
-    if (wv == 0 && lane < D) {
-        const double* L = Lf + (size_t)row * D * D + lane * D;
 #pragma unroll
-        for (int k = 0; k < D; ++k) tailop[k] = (k <= lane) ? L[k] : 0.0;
-    } else if (wv == 0 && lane < D + MC) {
-        const double* Z = tl.Zt + (size_t)row * D * MC + (lane - D);
+    for (int k = 0; k < D; ++k) tailop[k] = 0.0;
+    if (__builtin_amdgcn_readfirstlane(wv) == 0) {
+        const bool isL = lane < D;
+        const double* tb = isL ? Lf + (size_t)row * D * D + lane * D
+                               : tl.Zt + (size_t)row * D * MC + min(max(lane - D, 0), MC - 1);
+        const int ts = isL ? 1 : MC;
 #pragma unroll
-        for (int a = 0; a < D; ++a) tailop[a] = Z[a * MC];
-    }
-    if (wv == 0 && lane < D) {
+        for (int k = 0; k < D; ++k) tailop[k] = tb[k * ts];  // (L's upper part is masked at the use)
         vo = v[own]; u_ = tl.u[own]; r_ = cg.r[0][own];
-        if (!setup) {
-            w_ = cg.w[0][own]; z_ = cg.w[1][own]; q_ = cg.r[1][own]; s_ = cg.s[0][own]; p_ = cg.p[own]; x_ = cg.x[own];
-            al = cg.hist[2 * it];
-            be = (it == 0) ? 0.0 : cg.hist[2 * it + 1] / cg.hist[2 * (it - 1) + 1];
-        }
+        w_ = cg.w[0][own]; z_ = cg.w[1][own]; q_ = cg.r[1][own]; s_ = cg.s[0][own]; p_ = cg.p[own]; x_ = cg.x[own];
+        const int ia = max(it, 0), ib = max(it - 1, 0);
+        al = cg.hist[2 * ia]; hg1 = cg.hist[2 * ia + 1]; hg0 = cg.hist[2 * ib + 1];
     }
     double acc[PPL];
 #pragma unroll
@@ -842,6 +843,7 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
             cg.w[1][own] = 0.0;  // z
             cg.r[1][own] = 0.0;  // q
         } else {
+            const double be = (it == 0) ? 0.0 : hg1 / hg0;
             const double zn = prod + be * z_;
             const double qn = vo + be * q_;
             const double sn = w_ + be * s_;
