@@ -1021,6 +1021,45 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub(const int* __restrict__
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
 }
 
+// Cameras: X <- Exp(dc_pose) X, intrinsics += dc_intr; gain part 2 g_c.dc - dc^T U dc (rank 0 only).  One block of NT
+// cameras per call; the block's gain partial goes to part[blk].
+template <int M, int NT>
+__device__ __forceinline__ void update_cams_block(int blk, int C, const double* __restrict__ cams,
+                                                  const double* __restrict__ dc, const double* __restrict__ U,
+                                                  const double* __restrict__ gc, int with_gain,
+                                                  double* __restrict__ cams_new, double* __restrict__ part,
+                                                  double* red /* >= NT / 64 doubles */) {
+    constexpr int D = kD<M>, ST = kStride<M>, NI = Model<M>::NI;
+    const int c = blk * NT + threadIdx.x;
+    double gain[1] = {0.0};
+    if (c < C) {
+        const double* x = cams + (size_t)c * ST;
+        double* o = cams_new + (size_t)c * ST;
+        if (dc) {
+            const double* d = dc + (size_t)c * D;
+            retract_pose(x, d, o);
+#pragma unroll
+            for (int k = 0; k < NI; ++k) o[7 + k] = x[7 + k] + d[6 + k];
+            if (with_gain) {
+                const double* Uc = U + (size_t)c * D * D;
+                double quad = 0.0, lin = 0.0;
+                for (int a = 0; a < D; ++a) {
+                    double s = 0.0;
+                    for (int bb = 0; bb < D; ++bb) s += Uc[a * D + bb] * d[bb];
+                    quad += d[a] * s;
+                    lin += gc[(size_t)c * D + a] * d[a];
+                }
+                gain[0] = 2.0 * lin - quad;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < ST; ++k) o[k] = x[k];
+        }
+    }
+    block_sum<1, NT>(gain, red);
+    if (threadIdx.x == 0) part[blk] = gain[0];
+}
+
 // The same back-substitution with W_o^T dc re-derived from the observation instead of read from W: J~ is evaluated
 // again at the linearization point exactly as k_lin_points does (same inputs, same code: the same J~c, J~p) and
 // q_o = J~p^T (J~c dc).  It reads ~50 B per observation (uv, camera / point index, the run's points) instead of the
@@ -1033,10 +1072,17 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restric
                                                             const double* __restrict__ dc, const double* __restrict__ V,
                                                             const double* __restrict__ Vinv, const double* __restrict__ gp,
                                                             const double* __restrict__ pts, double* __restrict__ dp,
-                                                            double* __restrict__ pts_new, double* __restrict__ part) {
+                                                            double* __restrict__ pts_new, double* __restrict__ part,
+                                                            int nrun, int C, const double* __restrict__ U,
+                                                            const double* __restrict__ gc, int with_gain,
+                                                            double* __restrict__ cams_new, double* __restrict__ part_gc) {
     constexpr int D = kD<M>, ST = kStride<M>;
     __shared__ double red[kLinThreads];
     __shared__ double q[kLinThreads][3];
+    if ((int)blockIdx.x >= nrun) {  // the camera update rides along as the launch's last blocks (no separate launch)
+        update_cams_block<M, kLinThreads>(blockIdx.x - nrun, C, cams, dc, U, gc, with_gain, cams_new, part_gc, red);
+        return;
+    }
     const int t = threadIdx.x;
     const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
     const int p = tb + t;
@@ -1095,42 +1141,13 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restric
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
 }
 
-// Cameras: X <- Exp(dc_pose) X, intrinsics += dc_intr; gain part 2 g_c.dc - dc^T U dc (rank 0 only).
 template <int M>
-__global__ __launch_bounds__(kThreads) void k_update_cams(int C, const double* __restrict__ cams, const double* __restrict__ dc,
-                                                          const double* __restrict__ U, const double* __restrict__ gc,
-                                                          int with_gain, double* __restrict__ cams_new,
-                                                          double* __restrict__ part) {
-    constexpr int D = kD<M>, ST = kStride<M>, NI = Model<M>::NI;
-    __shared__ double red[kThreads];
-    const int c = blockIdx.x * kThreads + threadIdx.x;
-    double gain[1] = {0.0};
-    if (c < C) {
-        const double* x = cams + (size_t)c * ST;
-        double* o = cams_new + (size_t)c * ST;
-        if (dc) {
-            const double* d = dc + (size_t)c * D;
-            retract_pose(x, d, o);
-#pragma unroll
-            for (int k = 0; k < NI; ++k) o[7 + k] = x[7 + k] + d[6 + k];
-            if (with_gain) {
-                const double* Uc = U + (size_t)c * D * D;
-                double quad = 0.0, lin = 0.0;
-                for (int a = 0; a < D; ++a) {
-                    double s = 0.0;
-                    for (int bb = 0; bb < D; ++bb) s += Uc[a * D + bb] * d[bb];
-                    quad += d[a] * s;
-                    lin += gc[(size_t)c * D + a] * d[a];
-                }
-                gain[0] = 2.0 * lin - quad;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < ST; ++k) o[k] = x[k];
-        }
-    }
-    block_sum<1>(gain, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
+__global__ __launch_bounds__(kLinThreads) void k_update_cams(int C, const double* __restrict__ cams, const double* __restrict__ dc,
+                                                             const double* __restrict__ U, const double* __restrict__ gc,
+                                                             int with_gain, double* __restrict__ cams_new,
+                                                             double* __restrict__ part) {
+    __shared__ double red[kLinThreads / 64];
+    update_cams_block<M, kLinThreads>(blockIdx.x, C, cams, dc, U, gc, with_gain, cams_new, part, red);
 }
 
 // Huber loss and sum ||r||^2 (block partials).  (Measured: 4 observations per thread, loads hoisted, ran 25 -> 33 us.)
@@ -1795,20 +1812,22 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         return launch_err(h, "k_backsub");
     }) : with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
-        if (h->Pl > 0)
-            k_backsub_rc<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
-                                                                     cams, h->d.huber_delta, dcp, h->V, h->Vinv, h->gp,
-                                                                     pts_local, h->dp, h->pts_new, h->part_gp);
+        const int nrun = h->Pl > 0 ? h->n_lin : 0;  // point runs, then the camera-update blocks
+        k_backsub_rc<M><<<nrun + h->n_gc, kLinThreads, 0, h->stream>>>(
+            h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, h->d.huber_delta, dcp, h->V, h->Vinv, h->gp,
+            pts_local, h->dp, h->pts_new, h->part_gp, nrun, h->C, h->U, h->gc, h->d.rank == 0, h->cams_new, h->part_gc);
         return launch_err(h, "k_backsub_rc");
     });
     if (rc) return rc;
-    rc = with_model(h->model, [&](auto mc) -> int {
-        constexpr int M = decltype(mc)::value;
-        k_update_cams<M><<<h->n_gc, kThreads, 0, h->stream>>>(h->C, cams, dcp, h->U, h->gc, h->d.rank == 0, h->cams_new,
-                                                               h->part_gc);
-        return launch_err(h, "k_update_cams");
-    });
-    if (rc) return rc;
+    if (backsub_w) {
+        rc = with_model(h->model, [&](auto mc) -> int {
+            constexpr int M = decltype(mc)::value;
+            k_update_cams<M><<<h->n_gc, kLinThreads, 0, h->stream>>>(h->C, cams, dcp, h->U, h->gc, h->d.rank == 0,
+                                                                     h->cams_new, h->part_gc);
+            return launch_err(h, "k_update_cams");
+        });
+        if (rc) return rc;
+    }
     return iters;
 }
 
@@ -2285,7 +2304,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->n_gp_grp = std::max(1, cdiv((long long)Pl * kGPG, kThreads));
     if (kind == 1) h->n_gp = h->n_gp_grp;  // the gain partials of k_gp_backsub
     else h->n_gp = std::max(1, h->n_lin);   // one per run of k_backsub
-    h->n_gc = std::max(1, cdiv(C, kThreads));
+    h->n_gc = std::max(1, cdiv(C, kLinThreads));  // camera-update blocks (ride along with k_backsub_rc)
     if ((rc = dd(&h->part_cost, 2 * (size_t)h->n_cost))) return fail(rc, "");
     if ((rc = dd(&h->part_gp, (size_t)h->n_gp))) return fail(rc, "");
     if ((rc = dd(&h->part_gc, (size_t)h->n_gc))) return fail(rc, "");
