@@ -650,7 +650,7 @@ template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __restrict__ blk_row, const int* __restrict__ col,
                                                        const int* __restrict__ row_ptr, const int* __restrict__ pos_up,
                                                        const int* __restrict__ pos_lo, const double* __restrict__ Li,
-                                                       double* __restrict__ S, double* __restrict__ Sn) {
+                                                       double* __restrict__ S, double* __restrict__ Sn, int keep_S) {
     constexpr int DD = D * D;
     constexpr int DP = D + (D & 1);
     __shared__ double T[kWaves][DD];
@@ -663,7 +663,8 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
     const int i = blk_row[e], j = col[e];
     double* blk = S + (size_t)e * DD;
     if (e == row_ptr[i]) {
-        for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
+        if (keep_S)
+            for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
         return;
     }
     // the block and both factors' inverses staged together (every load in flight at once), the result kept in LDS for
@@ -692,7 +693,7 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
         double v = 0.0;
         if (bb < D) {
             for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Lb[wv][bb * D + m];
-            blk[a * D + bb] = v;
+            if (keep_S) blk[a * D + bb] = v;  // the scaled upper S is only read by the debug getter
             Sb[wv][a * D + bb] = v;
         }
         up[k] = v;
@@ -1230,6 +1231,7 @@ struct insfm_ba {
     int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
     int nbr_stride = 0;  // > 0: every CG row has exactly nbr_stride neighbour slots (padded), row r starts at r * stride
+    int keep_S = 0;      // write the scaled S~ back into S (only the debug getters read it; set by the debug entry points)
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
@@ -1677,7 +1679,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             constexpr int DV = decltype(dc_)::value;
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg);
             k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
-                                                                            h->pos_up, h->pos_lo, h->Li, h->S, h->Sn);
+                                                                            h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
             return launch_err(h, "k_cg_factor/scale");
         });
         if (rc) return rc;
@@ -2580,6 +2582,7 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
 
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts) {
     if (!h || !cams || !pts || h->kind != 0) return INSFM_BA_EINVAL;
+    h->keep_S = 1;
     HIPCHK(hipMemcpyAsync(h->cams_cur, cams, sizeof(double) * (size_t)h->C * h->stride, hipMemcpyDeviceToDevice, h->stream));
     if (h->Pl)
         HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * (size_t)h->Pl * 3, hipMemcpyDeviceToDevice,
@@ -2592,6 +2595,7 @@ int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts)
 
 int insfm_ba_debug_solve(insfm_ba* h, double f) {
     if (!h) return INSFM_BA_EINVAL;
+    h->keep_S = 1;
     // solves around the parameters last passed to insfm_ba_debug_linearize
     int it = run_solve(h, f, h->cams_cur, h->pts_cur);
     HIPCHK(hipStreamSynchronize(h->stream));
@@ -2741,6 +2745,7 @@ int insfm_gp_cost(insfm_ba* h, const double* pos, const double* pts, const doubl
 
 int insfm_gp_debug_linearize(insfm_ba* h, const double* pos, const double* pts, const double* scales) {
     if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
+    h->keep_S = 1;
     int rc = gp_load(h, pos, pts, scales, h->scl_cur);
     if (rc) return rc;
     if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
