@@ -1518,13 +1518,13 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
 int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
     const int C = h->C;
     if (h->kind == 1) {
-        k_tl_basis<kGP><<<cdiv(C * 4, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl);
+        k_tl_basis<kGP><<<cdiv(C * 4, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
         return launch_err(h, "k_tl_basis");
     }
     return with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int MC = kD<M> + 1;
-        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl);
+        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
         return launch_err(h, "k_tl_basis");
     });
 }
@@ -1594,7 +1594,7 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
 template <int D>
 void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
     if (it == 0) {  // setup: restriction of r0, u0 = M~^-1 r0, w0 = S~ u0 and the partials of iteration 0
-        k_tl_rrest<D><<<cdiv((long long)h->C * (D + 1), kThreads), kThreads, 0, h->stream>>>(h->C, h->cg, h->tl);
+        // (the restriction of r0 was formed by k_tl_basis)
         k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
         k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,

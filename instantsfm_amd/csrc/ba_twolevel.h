@@ -59,7 +59,7 @@ struct TlBufs {
 // One thread per (camera i, coarse column k): column k of G_i at the linearization point and Z~_i[:,k] = L_i^T G_i[:,k].
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __restrict__ cams, const double* __restrict__ Lf,
-                                                       TlBufs tl) {
+                                                       TlBufs tl, const double* __restrict__ r0) {
     constexpr int D = kD<M>, MC = D + 1, ST = kStride<M>;
     const int g = blockIdx.x * kThreads + threadIdx.x;
     if (g >= C * MC) return;
@@ -110,6 +110,8 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
         }
     }
     const double* L = Lf + (size_t)i * D * D;
+    const double* r = r0 + (size_t)i * D;
+    double rr = 0.0;  // restriction partial of the CG's starting residual (was k_tl_rrest): sum_a Z~[a][k] r0_a
 #pragma unroll
     for (int a = 0; a < D; ++a) {
         double s = 0.0;
@@ -117,7 +119,10 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
         for (int l = a; l < D; ++l) s += L[l * D + a] * col[l];
         tl.Zt[((size_t)i * D + a) * MC + k] = s;
         tl.Ztc[((size_t)tl.cpos[i] * D + a) * MC + k] = s;
+        rr += s * r[a];
     }
+    tl.rowR[(size_t)tl.cpos[i] * MC + k] = rr;
+    if (k < D) tl.vc[(size_t)tl.cpos[i] * D + k] = r[k];
 }
 
 template <int D>
