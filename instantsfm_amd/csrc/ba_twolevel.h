@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
     }
     const double* L = Lf + (size_t)i * D * D;
     const double* r = r0 + (size_t)i * D;
-    double rr = 0.0;  // restriction partial of the CG's starting residual (was k_tl_rrest): sum_a Z~[a][k] r0_a
+    double rr = 0.0;  // restriction partial of the CG's starting residual sum_a Z~[a][k] r0_a, a ascending
 #pragma unroll
     for (int a = 0; a < D; ++a) {
         double s = 0.0;
@@ -490,24 +490,8 @@ __global__ __launch_bounds__(256) void k_tl_gram(int m, const double* __restrict
 //   k_tl_pspmv (one workgroup per camera row): n = S~ m, then z = n + beta z, q = m + beta q, s = w + beta s,
 //              p = u + beta p, x += alpha p, r -= alpha s, u -= alpha q, w -= alpha z for the row, and the row's
 //              partials for iteration i + 1.
-// Two launches per iteration instead of three.  Setup (it = -1): k_tl_rrest (Z~^T r0 per row), k_tl_pc (u0 = r0 + Z~ y),
+// Two launches per iteration instead of three.  Setup (it = -1): k_tl_basis forms Z~^T r0 per row, k_tl_pc (u0 = r0 + Z~ y),
 // k_tl_pspmv (w0 = S~ u0 and the partials of iteration 0).  Buffers: q = cg.r[1], z = cg.w[1], m = cg.s[1].
-
-// rowR[i][k] = sum_a Z~_i[a][k] r_i[a]  (a ascending)
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_tl_rrest(int C, CgBufs cg, TlBufs tl) {
-    constexpr int MC = D + 1;
-    const int g = blockIdx.x * kThreads + threadIdx.x;
-    if (g >= C * MC) return;
-    const int i = g / MC, k = g % MC;
-    const double* Z = tl.Zt + (size_t)i * D * MC + k;
-    const double* r = cg.r[0] + (size_t)i * D;
-    double s = 0.0;
-#pragma unroll
-    for (int a = 0; a < D; ++a) s += Z[a * MC] * r[a];
-    tl.rowR[(size_t)tl.cpos[i] * MC + k] = s;
-    if (k < D) tl.vc[(size_t)tl.cpos[i] * D + k] = r[k];
-}
 
 // Copy n doubles global -> LDS: U loads per thread in flight before their LDS stores (a plain strided loop waits for
 // every load before its store).
