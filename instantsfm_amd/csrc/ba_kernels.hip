@@ -370,8 +370,10 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict
 // ------------------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* __restrict__ V, const double* __restrict__ gp,
                                                          double f, double cmin, double cmax, double* __restrict__ Vinv,
-                                                         double* __restrict__ y, int* __restrict__ flags) {
+                                                         double* __restrict__ y, int* __restrict__ flags,
+                                                         int* __restrict__ status) {
     const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0;  // the CG status word of this solve
     if (p >= Pl) return;
     double s[6];
 #pragma unroll
@@ -1182,7 +1184,7 @@ __global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict
 // All five are summed across ranks, so every rank takes the same accept / reject / fail branch.
 __global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ cost_part, int ncost,
                                                     const double* __restrict__ gp_part, int ngp,
-                                                    const double* __restrict__ gc_part, int ngc, const int* __restrict__ flags,
+                                                    const double* __restrict__ gc_part, int ngc, int* __restrict__ flags,
                                                     double* __restrict__ result) {
     __shared__ double red[2 * kThreads];
     double c2[2];
@@ -1193,6 +1195,7 @@ __global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ c
     if (threadIdx.x == 0) {
         result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0];
         result[4] = (double)flags[0];
+        flags[0] = 0;  // consumed: the next solve's point preparation starts from a clear flag
     }
 }
 
@@ -1231,6 +1234,7 @@ struct insfm_ba {
     int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
     int nbr_stride = 0;  // > 0: every CG row has exactly nbr_stride neighbour slots (padded), row r starts at r * stride
+    bool flags_dirty = false;  // a solve's point preparation ran and no k_final has consumed (cleared) its flag yet
     int keep_S = 0;      // write the scaled S~ back into S (only the debug getters read it; set by the debug entry points)
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
@@ -1638,12 +1642,14 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
-    // the non-PD flag and the CG status word, zeroed by one tiny launch (the runtime's fill kernel takes ~6 us each)
-    k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
-    {
+    // The non-PD flag is cleared by the k_final that consumed it and the CG status word by k_point_prep; one tiny
+    // launch clears both only when that chain is broken (a solve not followed by a cost, or no local points).
+    if (h->flags_dirty || h->Pl == 0 || h->kind == 1) {
+        k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
         const int rc0 = launch_err(h, "k_zero_words");
         if (rc0) return rc0;
     }
+    h->flags_dirty = true;
     const bool gpk = h->kind == 1;
     // global positioning: the scale-eliminated blocks are already damped, so k_schur takes U'/g'_c as they are
     const double* Uin = gpk ? h->Up : h->U;
@@ -1661,7 +1667,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                                                                      h->gpc);
     } else if (h->Pl > 0)
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
-                                                                       h->Vinv, h->y, h->flags);
+                                                                       h->Vinv, h->y, h->flags, h->cg.status);
     int iters = 0;
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
@@ -1843,6 +1849,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
                                                h->n_gp, nullptr, 0, h->flags, h->result);
         int rc = launch_err(h, "k_gp_cost/k_final");
         if (rc) return rc;
+        h->flags_dirty = false;
         rc = allreduce(h, h->result, 5);
         if (rc) return rc;
         HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
@@ -1859,6 +1866,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
         return launch_err(h, "k_cost/k_final");
     });
     if (rc) return rc;
+    h->flags_dirty = false;
     rc = allreduce(h, h->result, 5);
     if (rc) return rc;
     HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
