@@ -43,6 +43,10 @@ constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgr
 #define INSFM_SCHUR_WAVES 8
 #endif
 constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (non-deterministic mode)
+#ifndef LIN_CAMS_NT
+#define LIN_CAMS_NT 128  // k_lin_cams_reg threads per camera (measured 128 / 192 / 256 / 320: 0.156 / 0.161 / 0.167 / 0.194 ms linearize)
+#endif
+constexpr int kCostThreads = 256;  // k_cost workgroup size (64 / 128 / 512: same time, 25-26 us)
 #ifndef SCHUR_MINW
 #define SCHUR_MINW 1  // k_schur launch bound: minimum waves per SIMD (caps VGPRs: 4 -> 128)
 #endif
@@ -291,14 +295,15 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams(const int* __restrict__ c
 // of g_c in registers (no per-batch LDS round trip, no 256-long dependent add chain per entry); the partials are then
 // summed by a fixed butterfly per wave and the 4 wave sums in wave order, and U is written with both triangles from
 // the upper one (a product commutes exactly, so U stays exactly symmetric).  Same point / uv pipeline as k_lin_cams.
-template <int M>
-__global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict__ cam_ptr, const int* __restrict__ cm_pt,
+template <int M, int NT = LIN_CAMS_NT>
+__global__ __launch_bounds__(NT) void k_lin_cams_reg(const int* __restrict__ cam_ptr, const int* __restrict__ cm_pt,
                                                            const double* __restrict__ cm_uv, const double* __restrict__ pp,
                                                            const double* __restrict__ cams, const double* __restrict__ pts,
                                                            double delta, double* __restrict__ U, double* __restrict__ gc) {
     constexpr int D = kD<M>, ST = kStride<M>, NU = D * (D + 1) / 2, NE = NU + D;
     static_assert(D <= 9, "register accumulation is sized for D <= 9");
-    __shared__ double red[kWaves][NE];
+    constexpr int NW = NT / 64;
+    __shared__ double red[NW][NE];
     const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int eb = cam_ptr[c], ee = cam_ptr[c + 1];
     const double2* uv2 = reinterpret_cast<const double2*>(cm_uv);
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict
     double2 z = make_double2(0.0, 0.0), zn = z, znn = z;
     int pn = 0, pnn = 0;
     {
-        const int e0 = eb + t, e1 = e0 + kThreads;
+        const int e0 = eb + t, e1 = e0 + NT;
         if (e0 < ee) {
             const int p0 = cm_pt[e0];
             z = uv2[e0];
@@ -321,11 +326,11 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict
         }
         if (e1 < ee) { pn = cm_pt[e1]; zn = uv2[e1]; }
     }
-    for (int e = eb + t; e < ee; e += kThreads) {
-        const bool hn = e + kThreads < ee, hnn = e + 2 * kThreads < ee;
+    for (int e = eb + t; e < ee; e += NT) {
+        const bool hn = e + NT < ee, hnn = e + 2 * NT < ee;
         double Xn[3] = {0.0, 0.0, 0.0};
         if (hn) { Xn[0] = pts[3 * (size_t)pn]; Xn[1] = pts[3 * (size_t)pn + 1]; Xn[2] = pts[3 * (size_t)pn + 2]; }
-        if (hnn) { pnn = cm_pt[e + 2 * kThreads]; znn = uv2[e + 2 * kThreads]; }
+        if (hnn) { pnn = cm_pt[e + 2 * NT]; znn = uv2[e + 2 * NT]; }
         const double uvo[2] = {z.x, z.y};
         double r[2], Jc[2][D], Jp[2][3];
         eval_obs<M, true>(camv, X, ppc, uvo, r, Jc, Jp);
@@ -349,10 +354,10 @@ __global__ __launch_bounds__(kThreads) void k_lin_cams_reg(const int* __restrict
         if (lane == 0) red[wv][m] = v;
     }
     __syncthreads();
-    for (int m = t; m < NE; m += kThreads) {
+    for (int m = t; m < NE; m += NT) {
         double s = red[0][m];
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) s += red[w][m];
+        for (int w = 1; w < NW; ++w) s += red[w][m];
         if (m < NU) {
             int a = 0, rem = m;
             while (rem >= D - a) { rem -= D - a; ++a; }
@@ -1155,13 +1160,13 @@ __global__ __launch_bounds__(kLinThreads) void k_update_cams(int C, const double
 
 // Huber loss and sum ||r||^2 (block partials).  (Measured: 4 observations per thread, loads hoisted, ran 25 -> 33 us.)
 template <int M>
-__global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
-                                                   const double* __restrict__ uv, const double* __restrict__ pp,
-                                                   const double* __restrict__ cams, const double* __restrict__ pts,
-                                                   double delta, double* __restrict__ part) {
+__global__ __launch_bounds__(kCostThreads) void k_cost(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
+                                                       const double* __restrict__ uv, const double* __restrict__ pp,
+                                                       const double* __restrict__ cams, const double* __restrict__ pts,
+                                                       double delta, double* __restrict__ part) {
     constexpr int ST = kStride<M>;
-    __shared__ double red[2 * kWaves];
-    const int o = blockIdx.x * kThreads + threadIdx.x;
+    __shared__ double red[2 * (kCostThreads / 64)];
+    const int o = blockIdx.x * kCostThreads + threadIdx.x;
     double v[2] = {0.0, 0.0};
     if (o < Nl) {
         const int c = cam[o], p = ptl[o];
@@ -1176,7 +1181,7 @@ __global__ __launch_bounds__(kThreads) void k_cost(int Nl, const int* __restrict
         v[0] = rs < delta ? s : 2.0 * delta * rs - delta * delta;
         v[1] = s;
     }
-    block_sum<2>(v, red);
+    block_sum<2, kCostThreads>(v, red);
     if (threadIdx.x == 0) { part[2 * (size_t)blockIdx.x] = v[0]; part[2 * (size_t)blockIdx.x + 1] = v[1]; }
 }
 
@@ -1503,7 +1508,7 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
         if constexpr (D <= 9) {
             if (!batch_form) {
-                k_lin_cams_reg<M><<<h->C, kThreads, 0, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams,
+                k_lin_cams_reg<M><<<h->C, LIN_CAMS_NT, 0, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams,
                                                                     pts_local, h->d.huber_delta, h->U, h->gc);
                 return launch_err(h, "linearize");
             }
@@ -1859,7 +1864,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         if (h->Nl > 0)
-            k_cost<M><<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
+            k_cost<M><<<h->n_cost, kCostThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
                                                              h->d.huber_delta, h->part_cost);
         k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
                                                h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result);
@@ -2309,7 +2314,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = dd(&h->cams_new, (size_t)C * ST))) return fail(rc, "");
     if ((rc = dd(&h->pts_cur, (size_t)std::max(Pl, 1) * 3))) return fail(rc, "");
     if ((rc = dd(&h->pts_new, (size_t)std::max(Pl, 1) * 3))) return fail(rc, "");
-    h->n_cost = std::max(1, cdiv(Nl, kThreads));
+    h->n_cost = std::max(1, cdiv(Nl, kind == 1 ? kThreads : kCostThreads));
     h->n_gp = std::max(1, cdiv(Pl, kThreads));
     h->n_gp_grp = std::max(1, cdiv((long long)Pl * kGPG, kThreads));
     if (kind == 1) h->n_gp = h->n_gp_grp;  // the gain partials of k_gp_backsub
