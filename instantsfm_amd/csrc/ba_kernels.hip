@@ -1604,12 +1604,12 @@ template <int D>
 void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
     if (it == 0) {  // setup: restriction of r0, u0 = M~^-1 r0, w0 = S~ u0 and the partials of iteration 0
         // (the restriction of r0 was formed by k_tl_basis)
-        k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
+        k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
         k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
                                                               h->cg, h->tl);
     }
-    k_tl_pc<D><<<h->tl.nc, kCgThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
+    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
     k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
                                                           h->cg, h->tl);
 }

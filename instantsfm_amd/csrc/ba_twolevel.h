@@ -513,9 +513,14 @@ __device__ __forceinline__ void stage_lds(double* dst, const double* __restrict_
     }
 }
 
+#ifndef PC_NT
+#define PC_NT 512
+#endif
+constexpr int kPcThreads = PC_NT, kPcWaves = PC_NT / 64;  // k_tl_pc workgroup (256 / 512 / 1024: 11.0 / 8.8 / 9.1 us)
+
 // prows: restriction row partials staged in LDS per pass (rows in cluster order; the host sizes it to the LDS budget)
 template <int D>
-__global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, double tol2_rel, int prows, CgBufs cg,
+__global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, double tol2_rel, int prows, CgBufs cg,
                                                       TlBufs tl, const double* __restrict__ Einv) {
     constexpr int MC = D + 1;
     extern __shared__ double lds[];
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     double* EL = LR + (size_t)prows * MC;     // [MC][m] this cluster's rows of E^-1
     double* Rs = EL + (size_t)MC * tl.m;      // [m] full restriction
     __shared__ double y[MC];
-    __shared__ double red[3][kCgWaves];
+    __shared__ double red[3][kPcWaves];
     __shared__ double sc[3];
 #ifdef PC_TRACE
 #define PCT(k) if (blockIdx.x == 0 && threadIdx.x == 0 && it == 3) tl.Rc[k] = (double)wall_clock64();
@@ -542,18 +547,18 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     const int st0 = cg.status[0];
     const int okv = tl.ok[0];
     const int e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
-    constexpr int UE = (MC * kCoarseMax + kCgThreads - 1) / kCgThreads, UR = 32, UR2 = UR / 2;
+    constexpr int UE = (MC * kCoarseMax + kPcThreads - 1) / kPcThreads, UR = 16384 / kPcThreads, UR2 = UR / 2;
     const int np = (C + prows - 1) / prows;
     const int nlr0 = min(C, prows) * MC;
     // the scalar partials and the history first: the recurrence scalars below wait only for them (loads retire in
     // issue order), so that reduction overlaps the E^-1 / restriction batch still in flight
     // the first GK partials per thread are held in registers and summed at the scalar phase (a summing loop here
-    // would wait for them before the batch below is issued); rows past GK * kCgThreads are summed there too
+    // would wait for them before the batch below is issued); rows past GK * kPcThreads are summed there too
     constexpr int GK = 2;
     double ga0[GK], ga1[GK], ga2[GK];
 #pragma unroll
     for (int r = 0; r < GK; ++r) {
-        const int k = min(t + r * kCgThreads, C - 1);
+        const int k = min(t + r * kPcThreads, C - 1);
         ga0[r] = tl.gd[k]; ga1[r] = tl.gd[C + k]; ga2[r] = tl.gd[2 * C + k];
     }
     const int ih = max(it - 1, 0);
@@ -563,10 +568,10 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     // branch-free: indices past the end are clamped to the last valid element (a load under a divergent branch is
     // waited for at the branch's join, which would serialize the batch)
 #pragma unroll
-    for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kCgThreads, MC * m - 1)];
+    for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kPcThreads, MC * m - 1)];
 #pragma unroll
     for (int u = 0; u < UR2; ++u)
-        lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kCgThreads, (nlr0 - 1) / 2)];
+        lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kPcThreads, (nlr0 - 1) / 2)];
     const int tc = min(t / MC, tl.nc - 1);
     const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
     const int ne = e1 - e0;
@@ -591,14 +596,14 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         double g0 = 0.0, g1 = 0.0, g2 = 0.0;
 #pragma unroll
         for (int r = 0; r < GK; ++r)
-            if (t + r * kCgThreads < C) { g0 += ga0[r]; g1 += ga1[r]; g2 += ga2[r]; }
-        for (int k = t + GK * kCgThreads; k < C; k += kCgThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
+            if (t + r * kPcThreads < C) { g0 += ga0[r]; g1 += ga1[r]; g2 += ga2[r]; }
+        for (int k = t + GK * kPcThreads; k < C; k += kPcThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
         g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
         if (lane == 0) { red[0][wv] = g0; red[1][wv] = g1; red[2][wv] = g2; }
         __syncthreads();
         if (t == 0) {
             double gam = 0.0, del = 0.0, rho = 0.0;
-            for (int w = 0; w < kCgWaves; ++w) { gam += red[0][w]; del += red[1][w]; rho += red[2][w]; }
+            for (int w = 0; w < kPcWaves; ++w) { gam += red[0][w]; del += red[1][w]; rho += red[2][w]; }
             const double bb = (i == 0) ? rho : h_bb;
             double flag = 0.0;
             const bool lead = blockIdx.x == 0;
@@ -638,17 +643,17 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     if (use) {
 #pragma unroll
         for (int u = 0; u < UE; ++u) {
-            const int q = t + u * kCgThreads;
+            const int q = t + u * kPcThreads;
             if (q < MC * m) EL[q] = ev[u];
         }
 #pragma unroll
         for (int u = 0; u < UR2; ++u) {
-            const int q = 2 * (t + u * kCgThreads);
+            const int q = 2 * (t + u * kPcThreads);
             if (q < nlr0) LR[q] = lrv[u].x;
             if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
         }
-        if (nlr0 > UR * kCgThreads) stage_lds<kCgThreads, 16>(LR + UR * kCgThreads, tl.rowR + UR * kCgThreads,
-                                                                nlr0 - UR * kCgThreads);
+        if (nlr0 > UR * kPcThreads) stage_lds<kPcThreads, 16>(LR + UR * kPcThreads, tl.rowR + UR * kPcThreads,
+                                                                nlr0 - UR * kPcThreads);
     }
     PCT(2)
     if (use) {
@@ -657,10 +662,10 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
             const int r0 = pass * prows, r1 = min(C, r0 + prows);
             if (pass > 0) {
                 __syncthreads();
-                stage_lds<kCgThreads, 32>(LR, tl.rowR + (size_t)r0 * MC, (r1 - r0) * MC);
+                stage_lds<kPcThreads, 32>(LR, tl.rowR + (size_t)r0 * MC, (r1 - r0) * MC);
             }
             __syncthreads();
-            for (int e = t; e < m; e += kCgThreads) {
+            for (int e = t; e < m; e += kPcThreads) {
                 const int k = e % MC;
                 const int b0 = max(e == t ? rb0 : tl.cl_ptr[e / MC], r0), b1 = min(e == t ? rb1 : tl.cl_ptr[e / MC + 1], r1);
                 double v = pass == 0 ? 0.0 : Rs[e];
@@ -671,7 +676,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         __syncthreads();
         PCT(3)
-        constexpr int KPW = (MC + kCgWaves - 1) / kCgWaves, LPL = (kCoarseMax + 63) / 64;
+        constexpr int KPW = (MC + kPcWaves - 1) / kPcWaves, LPL = (kCoarseMax + 63) / 64;
         double sy[KPW];
 #pragma unroll
         for (int kk = 0; kk < KPW; ++kk) sy[kk] = 0.0;
@@ -682,14 +687,14 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
                 const double rl = Rs[l];
 #pragma unroll
                 for (int kk = 0; kk < KPW; ++kk) {
-                    const int k = wv + kk * kCgWaves;
+                    const int k = wv + kk * kPcWaves;
                     if (k < MC) sy[kk] += EL[(size_t)k * m + l] * rl;
                 }
             }
         }
 #pragma unroll
         for (int kk = 0; kk < KPW; ++kk) {
-            const int k = wv + kk * kCgWaves;
+            const int k = wv + kk * kPcWaves;
             const double v = wave_sum(sy[kk]);
             if (lane == 0 && k < MC) y[k] = v;
         }
@@ -697,7 +702,7 @@ __global__ __launch_bounds__(kCgThreads) void k_tl_pc(int it, int C, int maxit, 
     }
     PCT(4)
     double* dst = setup ? tl.u : cg.s[1];
-    for (int e = t; e < ne * D; e += kCgThreads) {
+    for (int e = t; e < ne * D; e += kPcThreads) {
         const bool first = e == t;
         const size_t idx = first ? pidx : (size_t)tl.cl_cams[e0 + e / D] * D + e % D;
         double v = first ? vp : tl.vc[(size_t)e0 * D + e];
