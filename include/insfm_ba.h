@@ -93,9 +93,10 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
 
 /* One LM step (bae.optim.LM.step semantics).  cam_params [C, 7+n_intr] ([t, q_xyzw, intrinsics without pp]) and
  * points [P,3] are DEVICE pointers, read at the start and updated in place at the end (on a multi-rank run each
- * rank updates only its shard's points).  `stats` may be NULL.  Blocks for one 64-byte device->host copy per trial;
- * the in-place update is the last work enqueued on the handle's stream (stream-ordered: work queued after the call on
- * that stream sees it; other streams or host reads synchronize with the stream first). */
+ * rank updates only its shard's points).  `stats` may be NULL.  Blocks for one 64-byte device->host copy per trial.
+ * The buffers are read in place as the step's linearization point (they must not be written by other work while the
+ * step runs); an accepted trial is copied into them as the last work enqueued on the handle's stream (stream-ordered:
+ * work queued after the call on that stream sees it; other streams or host reads synchronize with the stream first). */
 int insfm_ba_step(insfm_ba* h, double* cam_params, double* points, insfm_ba_stats* stats);
 
 /* Enable (1) / disable (0, default) the per-phase hipEvent timing reported in insfm_ba_stats.time_ms. */

@@ -1254,6 +1254,7 @@ struct insfm_ba {
     CgBufs cg{};
     int cg_nwg = 0;
     double *cams_cur = nullptr, *cams_new = nullptr, *pts_cur = nullptr, *pts_new = nullptr;
+    bool ext_cur = false;  // during insfm_ba_step: cams_cur / pts_cur are the caller's buffers
     double *part_cost = nullptr, *part_gp = nullptr, *part_gc = nullptr;
     int n_cost = 0, n_gp = 0, n_gc = 0;
     int n_gp_grp = 0;  // global positioning: k_gp_backsub blocks (kGPG lanes per track)
@@ -1934,8 +1935,16 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
             h->loss = last;
             continue;
         }
-        std::swap(h->cams_cur, h->cams_new);
-        std::swap(h->pts_cur, h->pts_new);
+        if (h->ext_cur) {  // the current parameters live in the caller's buffers: copy the accepted trial there
+            HIPCHK(hipMemcpyAsync(h->cams_cur, h->cams_new, sizeof(double) * (size_t)h->C * h->stride,
+                                  hipMemcpyDeviceToDevice, h->stream));
+            if (h->Pl)
+                HIPCHK(hipMemcpyAsync(h->pts_cur, h->pts_new, sizeof(double) * (size_t)h->Pl * 3, hipMemcpyDeviceToDevice,
+                                      h->stream));
+        } else {
+            std::swap(h->cams_cur, h->cams_new);
+            std::swap(h->pts_cur, h->pts_new);
+        }
         std::swap(h->scl_cur, h->scl_new);
         h->loss = loss_new;
         break;
@@ -2581,16 +2590,19 @@ int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* lo
 
 int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_stats* st) {
     if (!h || !cams_user || !pts_user || h->kind != 0) return INSFM_BA_EINVAL;
-    const size_t cam_bytes = sizeof(double) * (size_t)h->C * h->stride;
-    const size_t pt_bytes = sizeof(double) * (size_t)h->Pl * 3;
-    HIPCHK(hipMemcpyAsync(h->cams_cur, cams_user, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
-    if (pt_bytes) HIPCHK(hipMemcpyAsync(h->pts_cur, pts_user + 3 * (size_t)h->p0, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
-    int rc = lm_step(h, st);
-    if (rc) return rc;
-    // stream-ordered write-back (no host wait: the step's loss is already on the host)
-    HIPCHK(hipMemcpyAsync(cams_user, h->cams_cur, cam_bytes, hipMemcpyDeviceToDevice, h->stream));
-    if (pt_bytes) HIPCHK(hipMemcpyAsync(pts_user + 3 * (size_t)h->p0, h->pts_cur, pt_bytes, hipMemcpyDeviceToDevice, h->stream));
-    return INSFM_BA_OK;
+    // The caller's buffers are the linearization point of this step (read in place, no copy-in); trials go to the
+    // internal cams_new / pts_new, and an accepted trial is copied back into the caller's buffers (stream-ordered, no
+    // host wait: the step's loss is already on the host).
+    double* const ic = h->cams_cur;
+    double* const ip = h->pts_cur;
+    h->cams_cur = cams_user;
+    h->pts_cur = pts_user + 3 * (size_t)h->p0;
+    h->ext_cur = true;
+    const int rc = lm_step(h, st);
+    h->cams_cur = ic;
+    h->pts_cur = ip;
+    h->ext_cur = false;
+    return rc;
 }
 
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts) {

@@ -581,7 +581,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
         cg.status[2] = okv;  // reported as insfm_ba_stats.coarse_used
         if (cg.prog) __hip_atomic_store(cg.prog + 3, okv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    const bool pon = t < ne * D;
     const int tp = min(t, ne * D - 1);
     // the cluster's rows are contiguous in the cluster-ordered copies
     const size_t ci = (size_t)e0 * D + tp;
