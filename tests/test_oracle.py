@@ -36,7 +36,10 @@ def test_c_oracle_projection_matches_reference(golden, model):
 def test_fov_and_thin_prism_raise_in_reference(golden):
     assert int(golden["m7_raises"]) == 1 and int(golden["m10_raises"]) == 1
     with pytest.raises(NotImplementedError):
-        reproject(7, np.zeros((1, 3)), np.zeros((1, 12)), np.zeros((1, 2)))
+        # identity pose (q_w = 1), point in front of the camera: no 0/0 before the dispatch raises
+        cam = np.zeros((1, 12))
+        cam[0, 6] = 1.0
+        reproject(7, np.array([[0.0, 0.0, 1.0]]), cam, np.zeros((1, 2)))
     assert O.n_intr(7) == -1 and O.n_intr(10) == -1
 
 
