@@ -79,7 +79,9 @@ def normal_from_fisheye(uv):
     """Camera.normal_from_fisheye (defs.py:252-255), in the array's own dtype."""
     theta = np.linalg.norm(uv, axis=-1, keepdims=True)
     theta_cos_theta = theta * np.cos(theta)
-    return uv * np.sin(theta) / theta_cos_theta
+    # the reference divides unguarded: uv = 0 gives 0/0 = NaN there too (the kernel matches it)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        return uv * np.sin(theta) / theta_cos_theta
 
 
 def img2cam(model, params, xy):
