@@ -539,7 +539,12 @@ def main():
     eng.reset()
     ci, pi = cams0.clone(), pts0.clone()
     eng.set_timing(True)
-    istats = [eng.step(ci, pi)[1] for _ in range(args.steps)]
+    istats = []
+    rmse_conv = None  # RMSE where the reference stop rule fires: like-for-like with the CPU run's final RMSE
+    for k in range(args.steps):
+        istats.append(eng.step(ci, pi)[1])
+        if conv_step is not None and k + 1 == conv_step:
+            rmse_conv = eng.cost(ci, pi)[1]
     eng.set_timing(False)
     tl = args.precond == 1
     us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
@@ -592,8 +597,9 @@ def main():
                    "cams": C, "points": P, "obs": N, "camera_block_dim": D, "schur_blocks": nnzb,
                    "parallelism": f"track-shard x{world}" if world > 1 else "single GPU"},
         "final_loss": final_loss,
-        "final_rmse_px": rmse,
+        "final_rmse_px": rmse_conv,
         "converged_at_step": conv_step,
+        "rmse_after_timed_steps_px": rmse,
         "pcg_iters": [s["pcg_iters"] for s in stats],
         "trials": trials,
         "phase_ms_per_step": {k: round(float(v) / args.steps, 3) for k, v in

@@ -33,6 +33,7 @@
 #include "ba_common.h"
 #include "ba_twolevel.h"
 #include "ba_gp.h"
+#include "cg_poll.h"
 
 using namespace insfm;
 
@@ -1375,7 +1376,8 @@ int launch_err(insfm_ba* h, const char* what) {
 }
 
 int allreduce(insfm_ba* h, double* buf, int64_t n) {
-    if (h->d.world_size <= 1) return 0;
+    // a single rank skips the exchange unless a callback is installed (tests drive the RCCL path with one rank)
+    if (h->d.world_size <= 1 && !h->d.allreduce) return 0;
     if (!h->d.allreduce) { h->err = "world_size > 1 needs an allreduce callback"; return INSFM_BA_ECOMM; }
     int rc = h->d.allreduce(h->d.allreduce_ctx, buf, n);
     if (rc) { h->err = "allreduce callback failed (" + std::to_string(rc) + ")"; return INSFM_BA_ECOMM; }
@@ -1720,35 +1722,35 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // the loop below tops up one iteration at a time
             int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
             if ((rc = enqueue(0, enq))) return rc;
-            long spins = 0;
-            for (;;) {
-                if (pg[1] != 0) break;
-                // keep about kCgAhead iterations queued, one at a time: every iteration queued past convergence
-                // costs ~10 us of early-exit launches (chunks of 4 left 5 such iterations per solve)
-                const int reached = pg[0];
-                if (enq < maxit + 2 && reached >= enq - kCgAhead) {
-                    const int to = std::min(enq + 1, maxit + 2);
-                    if ((rc = enqueue(enq, to))) return rc;
-                    enq = to;
-                    continue;
-                }
-                if ((++spins & 255) == 0) {
+            CgPoll poll;
+            poll.enq = enq;
+            static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
+            int erc = 0;
+            const int pr = cg_poll(
+                poll, maxit + 2, kCgAhead, stall_s, [&] { return (int)pg[1]; }, [&] { return (int)pg[0]; }, enqueue,
+                [&] {
                     const hipError_t q = hipStreamQuery(h->stream);
-                    if (q == hipSuccess) {  // drained: everything enqueued has run
-                        std::atomic_thread_fence(std::memory_order_seq_cst);
-                        if (pg[1] != 0) break;
-                        if (enq >= maxit + 2) break;
-                        const int to = std::min(enq + 8, maxit + 2);
-                        if ((rc = enqueue(enq, to))) return rc;
-                        enq = to;
-                    } else if (q != hipErrorNotReady) {
-                        h->err = std::string("PCG: ") + hipGetErrorString(q);
-                        return INSFM_BA_EHIP;
-                    }
-                }
+                    if (q == hipSuccess) { std::atomic_thread_fence(std::memory_order_seq_cst); return 0; }
+                    return q == hipErrorNotReady ? 1 : -1;
+                },
+                wall_seconds,
+                [] {
 #if defined(__x86_64__)
-                __builtin_ia32_pause();
+                    __builtin_ia32_pause();
 #endif
+                },
+                &erc);
+            enq = poll.enq;
+            if (pr == CgPoll::kEnqueueError) return erc;
+            if (pr == CgPoll::kStreamError) {
+                h->err = std::string("PCG: ") + hipGetErrorString(hipStreamQuery(h->stream));
+                return INSFM_BA_EHIP;
+            }
+            if (pr == CgPoll::kStalled) {
+                h->err = "PCG: no progress from the device for " + std::to_string(poll.stalled_s) +
+                         " s (iterations started " + std::to_string(pg[0]) + ", status " + std::to_string(pg[1]) +
+                         ", enqueued " + std::to_string(enq) + "); set INSFM_CG_STALL_S to change the limit";
+                return INSFM_BA_EHIP;
             }
             std::atomic_thread_fence(std::memory_order_seq_cst);
             rec(h, 9);

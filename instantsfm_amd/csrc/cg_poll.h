@@ -1,0 +1,83 @@
+// Host poll policy of the two-level CG (ba_kernels.hip run_solve): no stream sync inside the CG.  The lead workgroup
+// of k_tl_pc publishes {iterations started, status} into host-mapped memory; the host keeps about `ahead` iterations
+// queued, one at a time, and stops when the status word turns non-zero.  Plain C++ (no HIP types) so the policy,
+// including its deadline, is unit-tested on the CPU (tests/test_cg_poll.py builds tests/cpp/cg_poll_test.cpp).
+//
+// Deadline: if neither the progress word nor the status changes for `stall_s` seconds of wall clock, the poll gives up
+// (CgPoll::kStalled) instead of spinning forever on a CG launch that never publishes (a hung kernel, or a fault that
+// does not surface as a stream error).  A live CG iteration takes ~10-20 us, so any stall of seconds is a failure.
+#pragma once
+#include <chrono>
+#include <cstdlib>
+#include <string>
+
+namespace insfm {
+
+struct CgPoll {
+    enum Result { kDone = 0, kDrained = 1, kEnqueueError = -1, kStreamError = -2, kStalled = -3 };
+    int enq = 0;            // iterations enqueued so far
+    int last_reached = 0;   // last progress word seen
+    long spins = 0;
+    double stalled_s = 0.0; // wall-clock seconds without progress when the poll stopped
+};
+
+// Default stall limit (seconds); the environment variable INSFM_CG_STALL_S overrides it.
+inline double cg_stall_limit_s(const char* env_value) {
+    if (env_value && *env_value) {
+        char* end = nullptr;
+        const double v = std::strtod(env_value, &end);
+        if (end != env_value && v > 0.0) return v;
+    }
+    return 10.0;
+}
+
+// status():  the published status word (0 running, non-zero finished)
+// reached(): the published count of iterations started
+// enqueue(from, to) -> int: launch iterations [from, to); non-zero = error (returned as kEnqueueError, code in *rc)
+// query() -> int: 0 = stream drained, 1 = still running, negative = stream error
+// now() -> double seconds (monotonic)
+// pause(): a CPU relax hint
+template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause>
+int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reached reached, Enqueue enqueue,
+            Query query, Now now, Pause pause, int* rc) {
+    double t_progress = now();
+    for (;;) {
+        if (status() != 0) return CgPoll::kDone;
+        const int r = reached();
+        if (r != s.last_reached) {
+            s.last_reached = r;
+            t_progress = now();
+        }
+        if (s.enq < limit && r >= s.enq - ahead) {
+            const int to = s.enq + 1 < limit ? s.enq + 1 : limit;
+            if ((*rc = enqueue(s.enq, to)) != 0) return CgPoll::kEnqueueError;
+            s.enq = to;
+            continue;
+        }
+        if ((++s.spins & 255) == 0) {
+            const int q = query();
+            if (q == 0) {  // drained: everything enqueued has run
+                if (status() != 0) return CgPoll::kDone;
+                if (s.enq >= limit) return CgPoll::kDrained;
+                const int to = s.enq + 8 < limit ? s.enq + 8 : limit;
+                if ((*rc = enqueue(s.enq, to)) != 0) return CgPoll::kEnqueueError;
+                s.enq = to;
+                t_progress = now();
+                continue;
+            }
+            if (q < 0) return CgPoll::kStreamError;
+            const double dt = now() - t_progress;
+            if (dt > stall_s) {
+                s.stalled_s = dt;
+                return CgPoll::kStalled;
+            }
+        }
+        pause();
+    }
+}
+
+inline double wall_seconds() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace insfm

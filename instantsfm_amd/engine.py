@@ -18,7 +18,7 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
                    pcg_max_iter=500, precond=1, cluster_size=32)
 
 
-def make_allreduce_callback(get_buffer, group=None, errors=None):
+def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
     """The C ABI's allreduce callback (insfm_ba_allreduce_fn) over torch.distributed.
 
     The library only ever passes sub-ranges of the exchange tensor returned by ``get_buffer()``; the slice is summed
@@ -29,6 +29,8 @@ def make_allreduce_callback(get_buffer, group=None, errors=None):
 
     def _allreduce(ctx, ptr, count):
         try:
+            if counter is not None:
+                counter[0] += 1
             buf = get_buffer()
             addr = ctypes.cast(ptr, ctypes.c_void_p).value
             off = (addr - buf.data_ptr()) // buf.element_size()
@@ -58,11 +60,35 @@ def _require_gpu(device):
     return dev
 
 
+class _LibraryStream:
+    """Context: library stream current; ordered after the caller's stream on entry, caller's after it on exit."""
+
+    def __init__(self, lib_stream):
+        self.lib = lib_stream
+        self.ctx = None
+        self.caller = None
+
+    def __enter__(self):
+        self.caller = torch.cuda.current_stream(self.lib.device)
+        if self.caller != self.lib:
+            self.lib.wait_stream(self.caller)
+        self.ctx = torch.cuda.stream(self.lib)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self.ctx.__exit__(*exc)
+        if self.caller != self.lib:
+            self.caller.wait_stream(self.lib)
+        return False
+
+
 class BundleAdjuster:
     """One LM problem on one GPU (or one track shard of it)."""
 
     def __init__(self, model, uv, cam_idx, pt_idx, pp, n_cams, n_points, device="cuda:0", optimize_poses=True,
-                 huber_delta=1.0, deterministic=False, world_size=1, rank=0, shard=None, process_group=None, **lm):
+                 huber_delta=1.0, deterministic=False, world_size=1, rank=0, shard=None, process_group=None,
+                 force_exchange=False, **lm):
         self.device = _require_gpu(device)
         L = _capi.load()
         opts = dict(LM_DEFAULTS, **lm)
@@ -83,11 +109,14 @@ class BundleAdjuster:
         self._xbuf = None
         self._cb = None
         self._errors = []
-        if world_size > 1:
-            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors))
+        self.exchange_calls = [0]
+        exchange = world_size > 1 or force_exchange
+        if exchange:
+            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors,
+                                                                  self.exchange_calls))
             d.allreduce = self._cb
-        with torch.cuda.device(self.device):
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._stream = torch.cuda.current_stream(self.device)
+        stream = self._stream.cuda_stream
         h = ctypes.c_void_p()
         rc = L.insfm_ba_create(ctypes.byref(d), uv.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                cam_idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
@@ -102,7 +131,7 @@ class BundleAdjuster:
         self.desc = d
         self.n_cams, self.n_points, self.n_obs = d.n_cams, d.n_points, d.n_obs
         self.D = 6 + {0: 1, 1: 2, 2: 2, 3: 3, 4: 6, 5: 6, 6: 10, 8: 2, 9: 3}[int(model)]
-        if world_size > 1:
+        if exchange:
             n = L.insfm_ba_exchange_count(h)
             self._xbuf = torch.zeros(int(n), dtype=torch.float64, device=self.device)
             _capi.check(h, L.insfm_ba_set_exchange(h, ctypes.c_void_p(self._xbuf.data_ptr()), n))
@@ -126,20 +155,30 @@ class BundleAdjuster:
             raise ValueError(f"expected shape {shape}, got {tuple(t.shape)}")
         return ctypes.c_void_p(t.data_ptr())
 
+    def _on_stream(self):
+        """The library launches on the stream captured at create.  Callers may be inside another torch stream context:
+        order the library stream after the caller's current stream, and make the library stream current while the
+        library runs, so the all-reduce callback (RCCL on the current stream, or gloo's device->host copy) is ordered
+        with the library's kernels.  The caller's stream is ordered after the library's on exit."""
+        return _LibraryStream(self._stream)
+
     def step(self, cam_params, points):
         """One LM step; updates ``cam_params`` [C, 7+ni] and ``points`` [P, 3] in place.  Returns (loss, stats)."""
         st = _capi.Stats()
         L = _capi.load()
-        rc = L.insfm_ba_step(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)), self._ptr(points, (self.n_points, 3)),
-                             ctypes.byref(st))
+        with self._on_stream():
+            rc = L.insfm_ba_step(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)),
+                                 self._ptr(points, (self.n_points, 3)), ctypes.byref(st))
         _capi.check(self._h, rc)
         return st.loss, st.as_dict()
 
     def cost(self, cam_params, points):
         loss, rmse = ctypes.c_double(), ctypes.c_double()
         L = _capi.load()
-        _capi.check(self._h, L.insfm_ba_cost(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)),
-                                             self._ptr(points, (self.n_points, 3)), ctypes.byref(loss), ctypes.byref(rmse)))
+        with self._on_stream():
+            rc = L.insfm_ba_cost(self._h, self._ptr(cam_params, (self.n_cams, self.D + 1)),
+                                 self._ptr(points, (self.n_points, 3)), ctypes.byref(loss), ctypes.byref(rmse))
+        _capi.check(self._h, rc)
         return loss.value, rmse.value
 
     def set_timing(self, on):
@@ -215,11 +254,13 @@ class GlobalPositioner(BundleAdjuster):
         self._xbuf = None
         self._cb = None
         self._errors = []
+        self.exchange_calls = [0]
         if world_size > 1:
-            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors))
+            self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors,
+                                                                  self.exchange_calls))
             d.allreduce = self._cb
-        with torch.cuda.device(self.device):
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._stream = torch.cuda.current_stream(self.device)
+        stream = self._stream.cuda_stream
         h = ctypes.c_void_p()
         dp, ip = ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)
         rc = L.insfm_gp_create(ctypes.byref(d), trans.ctypes.data_as(dp), cam_idx.ctypes.data_as(ip),
@@ -246,13 +287,17 @@ class GlobalPositioner(BundleAdjuster):
     def step(self, positions, points, scales):
         """One LM step; updates ``positions`` [C,3], ``points`` [P,3], ``scales`` [N] in place.  Returns (loss, stats)."""
         st = _capi.Stats()
-        _capi.check(self._h, _capi.load().insfm_gp_step(self._h, *self._args(positions, points, scales), ctypes.byref(st)))
+        with self._on_stream():
+            rc = _capi.load().insfm_gp_step(self._h, *self._args(positions, points, scales), ctypes.byref(st))
+        _capi.check(self._h, rc)
         return st.loss, st.as_dict()
 
     def cost(self, positions, points, scales):
         loss, rmse = ctypes.c_double(), ctypes.c_double()
-        _capi.check(self._h, _capi.load().insfm_gp_cost(self._h, *self._args(positions, points, scales), ctypes.byref(loss),
-                                                        ctypes.byref(rmse)))
+        with self._on_stream():
+            rc = _capi.load().insfm_gp_cost(self._h, *self._args(positions, points, scales), ctypes.byref(loss),
+                                            ctypes.byref(rmse))
+        _capi.check(self._h, rc)
         return loss.value, rmse.value
 
     def debug_linearize(self, positions, points, scales):

@@ -22,19 +22,49 @@ def _port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"], ["--gp", "--steps", "6"]])
-def test_two_ranks_match_single_gpu(extra):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "tools", "dist_check.py"), "--backend", "gloo",
+def _run(nproc, backend, extra, timeout=600):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc), "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "tools", "dist_check.py"), "--backend", backend,
            "--same-device", *extra]
     env = dict(os.environ, OMP_NUM_THREADS="4")
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=REPO)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
-    out = json.loads(line)
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"], ["--gp", "--steps", "6"]])
+def test_two_ranks_match_single_gpu(extra):
+    out = _run(2, "gloo", extra)
     assert out["loss_rel"] < 1e-9, out
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
     assert out["cams_equal_across_ranks"], out
     assert abs(out["rmse"] - out["ref_rmse"]) < 1e-6, out
     if "scales_rel" in out:
         assert out["scales_rel"] < 1e-7, out
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_config4_sharded_config3_scene(nproc):
+    """BASELINE config 4: the full config-3 scene (1000 cams / 200k points / 2M obs) track-sharded over 2 and 4 ranks
+    (gloo, ranks sharing the one MI355X of the test box) vs the single-GPU LM: loss 1e-9, parameters 1e-7, every rank
+    holds bitwise-equal cameras (the replicated CG computed the same dc), RMSE |delta| <= 1e-4 px."""
+    out = _run(nproc, "gloo", ["--config", "3", "--steps", "3"], timeout=850)
+    assert out["world"] == nproc and len(out["shards"]) == nproc
+    assert out["loss_rel"] < 1e-9, out
+    assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
+    assert out["cams_equal_across_ranks"], out
+    assert abs(out["rmse"] - out["ref_rmse"]) <= 1e-4, out
+    assert out["exchange_calls"] > 0, out
+
+
+@pytest.mark.timeout(300)
+def test_rccl_exchange_one_rank():
+    """The RCCL ("nccl") branch of the exchange callback (engine.make_allreduce_callback) on a device tensor, ordered
+    on the library's stream: one rank with the callback forced on, so every all-reduce of the camera system runs
+    through RCCL; the result must equal the plain single-GPU run (a 1-rank sum is the identity)."""
+    out = _run(1, "nccl", ["--small", "--steps", "4", "--force-exchange"], timeout=280)
+    assert out["backend"] == "nccl" and out["world"] == 1
+    assert out["exchange_calls"] >= 4 * 3, out  # per step: [U|g_c], [S|b] per trial, the 5 result scalars
+    assert out["loss_rel"] < 1e-12 and out["cams_rel"] < 1e-12 and out["points_rel"] < 1e-12, out

@@ -259,3 +259,78 @@ def test_repeated_solves_lagged_coarse_inverse(model):
             lagged = relin and k > 0
             assert err < (1e-6 if lagged else 1e-8), (rep, k, err)
         eng.close()
+
+
+def _reject_scene(seed, frac):
+    """A config-1-sized scene whose LM takes rejected trials: a fraction of the initial points moved by N(0, 10^2)
+    (the oracle's reject counts for these seeds: seed 21 / 5 % -> steps 5 and 6 reject 2 and 1 trials; seed 23 / 20 %
+    -> rejects spread over steps 4-15)."""
+    prob = make_problem(24, 600, seed=seed)
+    rng = np.random.default_rng(seed)
+    p0 = prob.points_init.copy()
+    idx = rng.random(p0.shape[0]) < frac
+    p0[idx] += rng.normal(0, 10.0, (int(idx.sum()), 3))
+    return prob, p0
+
+
+@pytest.mark.parametrize("seed,frac,tr_factor", [(21, 0.05, 0.5), (21, 0.05, 0.25), (23, 0.2, 0.5)])
+def test_reject_path_parity(seed, frac, tr_factor):
+    """BA steps that reject trials (LM reject loop, bundle_adjustment.py:119 reject=30), step by step vs the oracle:
+    trials, rejects, damping, loss and the in-place-updated caller buffers (the step reads them as the linearization
+    point, retries from them unchanged after a reject and copies the accepted trial back) to 1e-9.  tr_factor (the
+    TrustRegion down-multiplier's shrink per consecutive failure) is passed through to both."""
+    prob, p0 = _reject_scene(seed, frac)
+    eng, _ = engines(prob, tr_factor=tr_factor)
+    ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
+                     tr_factor=tr_factor)
+    cg, pg = dev(prob.cams_init), dev(p0)
+    co, po = prob.cams_init.copy(), p0.copy()
+    total_rej, multi = 0, 0
+    for s in range(15):
+        lg, st = eng.step(cg, pg)
+        lo = ora.step(co, po)
+        so = ora.stats()
+        assert (st["trials"], st["rejects"], st["failed"]) == (so["trials"], so["rejects"], so["failed"]), (s, st, so)
+        assert abs(st["damping"] - so["damping"]) <= 1e-9 * so["damping"], (s, st, so)
+        assert abs(lg - lo) <= 1e-9 * lo, (s, lg, lo)
+        assert rel(cg.cpu().numpy(), co) < 1e-9, s
+        assert rel(pg.cpu().numpy(), po) < 1e-9, s
+        total_rej += st["rejects"]
+        multi += st["rejects"] > 0
+    assert total_rej > 0 and multi > 0
+
+
+def test_reject_path_tr_factor_changes_damping():
+    """The tr_factor knob is live: with two consecutive rejects (seed 21, step 5), 0.5 and 0.25 give different damping
+    sequences (oracle and GPU alike, see test_reject_path_parity)."""
+    prob, p0 = _reject_scene(21, 0.05)
+    damp = {}
+    for trf in (0.5, 0.25):
+        ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
+                         tr_factor=trf)
+        c, p = prob.cams_init.copy(), p0.copy()
+        damp[trf] = []
+        for _ in range(15):
+            ora.step(c, p)
+            damp[trf].append(ora.stats()["damping"])
+    assert damp[0.5] != damp[0.25]
+
+
+def test_solver_failure_leaves_caller_buffers_unchanged():
+    """A trial whose damped point blocks are not positive definite (forced here with an out-of-range diagonal clamp,
+    clamp_min = clamp_max = -1) fails the step: the LM reports solver_failed, returns the previous loss and leaves the
+    caller's parameter buffers bit-for-bit unchanged -- like the oracle (and the LM's "Linear solver failed. Breaking
+    optimization step...")."""
+    prob = make_problem(20, 400, seed=2)
+    eng, _ = engines(prob, clamp_min=-1.0, clamp_max=-1.0)
+    ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
+                     clamp_min=-1.0, clamp_max=-1.0)
+    cg, pg = dev(prob.cams_init), dev(prob.points_init)
+    l0, _ = eng.cost(cg, pg)
+    lg, st = eng.step(cg, pg)
+    assert st["failed"] == 1 and lg == l0, st
+    assert np.array_equal(cg.cpu().numpy(), prob.cams_init) and np.array_equal(pg.cpu().numpy(), prob.points_init)
+    co, po = prob.cams_init.copy(), prob.points_init.copy()
+    lo = ora.step(co, po)
+    assert ora.stats()["failed"] == 1 and abs(lo - l0) <= 1e-12 * l0
+    assert np.array_equal(co, prob.cams_init) and np.array_equal(po, prob.points_init)

@@ -80,12 +80,17 @@ def main():
     ap.add_argument("--steps", type=int, default=6)
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0")
     ap.add_argument("--gp", action="store_true", help="global positioning (insfm_gp) instead of BA")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="install the all-reduce callback even with one rank (drives the RCCL branch on one GPU)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
-    dist.init_process_group(args.backend)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group(args.backend)
     if args.gp:
         run_gp(args, rank, world, dev)
         dist.destroy_process_group()
@@ -93,7 +98,8 @@ def main():
     prob = make_problem(24, 900, seed=9) if args.small else make_config(args.config)
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
-                         world_size=world, rank=rank, shard=shards[rank], deterministic=True)
+                         world_size=world, rank=rank, shard=shards[rank], deterministic=True,
+                         force_exchange=args.force_exchange)
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
     pts = torch.from_numpy(prob.points_init.copy()).to(dev)
     losses = []
@@ -112,8 +118,13 @@ def main():
     else:
         dist.all_reduce(full)
         full = full.cpu()
-    cams_all = [torch.zeros_like(cams).cpu() for _ in range(world)]
-    dist.all_gather(cams_all, cams.cpu()) if args.backend == "gloo" else None
+    if args.backend == "gloo":
+        cams_all = [torch.zeros_like(cams).cpu() for _ in range(world)]
+        dist.all_gather(cams_all, cams.cpu())
+    else:
+        cams_all = [torch.zeros_like(cams) for _ in range(world)]
+        dist.all_gather(cams_all, cams)
+        cams_all = [c.cpu() for c in cams_all]
     if rank == 0:
         ref = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                              device=dev, deterministic=True)
@@ -125,7 +136,7 @@ def main():
         out = dict(world=world, backend=args.backend, shards=shards,
                    loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
                    cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
-                   rmse=rmse, ref_rmse=ref_rmse,
+                   rmse=rmse, ref_rmse=ref_rmse, exchange_calls=eng.exchange_calls[0], n_obs=int(prob.n_obs),
                    cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all) if cams_all else None)
         print(json.dumps(out), flush=True)
         ok = out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7
