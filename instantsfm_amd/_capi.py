@@ -33,7 +33,7 @@ class Desc(ctypes.Structure):
         ("world_size", ctypes.c_int32), ("rank", ctypes.c_int32),
         ("shard_point_begin", ctypes.c_int32), ("shard_point_end", ctypes.c_int32),
         ("allreduce", ALLREDUCE_FN), ("allreduce_ctx", ctypes.c_void_p),
-        ("precond", ctypes.c_int32), ("cluster_size", ctypes.c_int32),
+        ("precond", ctypes.c_int32), ("cluster_size", ctypes.c_int32), ("schur_variant", ctypes.c_int32),
     ]
 
 

@@ -34,6 +34,8 @@
 #include "ba_twolevel.h"
 #include "ba_gp.h"
 #include "cg_poll.h"
+#include "ba_schur_rc.h"
+#include "ba_schur_mf.h"
 
 using namespace insfm;
 
@@ -53,6 +55,9 @@ constexpr int kCostThreads = 256;  // k_cost workgroup size (64 / 128 / 512: sam
 #endif
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
+#endif
+#ifndef SCHUR_RC_WAVES
+#define SCHUR_RC_WAVES 4  // waves per k_schur_rc workgroup
 #endif
 
 // ------------------------------------------------------------------------------------------------------------
@@ -108,13 +113,15 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // as one contiguous segment in k_schur); each track reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~.
 constexpr int kLinThreads = 128;  // k_lin_points workgroup (LDS: W staging + V/g terms of its observations)
 
-template <int M>
+template <int M, bool STORE_W = true>
 __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
                                                          const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
                                                          double delta, double* __restrict__ W, double* __restrict__ V,
-                                                         double* __restrict__ gp) {
+                                                         double* __restrict__ gp, double2* __restrict__ obrec) {
+    // STORE_W = false (the re-deriving Schur, ba_schur_rc.h): no W records; each observation's {sqrt(w), camera}
+    // goes to obrec instead (16 B, coalesced).
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
     // is longer), one thread per observation: coalesced uv / cam / point loads and 192-B W records written by
     // consecutive lanes (16 B per lane).  Each observation's V / g_p terms go to LDS and one thread per track adds them
@@ -141,16 +148,19 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             double r[2], Jc[2][D], Jp[2][3];
             eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
             const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+            if (obrec) obrec[o] = make_double2(sw, (double)c);
             r[0] *= sw; r[1] *= sw;
 #pragma unroll
             for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
 #pragma unroll
             for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
-            double* Wo = wst + (size_t)t * WRP;
+            if constexpr (STORE_W) {
+                double* Wo = wst + (size_t)t * WRP;
 #pragma unroll
-            for (int a = 0; a < D; ++a)
+                for (int a = 0; a < D; ++a)
 #pragma unroll
-                for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+                    for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+            }
             cv[0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
             cv[1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
             cv[2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
@@ -160,9 +170,10 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
 #pragma unroll
             for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
         }
-        __syncthreads();
         const int n = min(kLinThreads, oe - base);
-        if constexpr ((WR & 1) == 0) {
+        if constexpr (!STORE_W) {
+        } else if constexpr ((WR & 1) == 0) {
+            __syncthreads();
             // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive
             // 16-B pairs (WR even: a pair never crosses a record, and every record starts 16-B aligned)
             double2* dst = reinterpret_cast<double2*>(W + (size_t)base * WR);
@@ -172,6 +183,7 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
                 dst[k2] = make_double2(src[0], src[1]);
             }
         } else {
+            __syncthreads();
             double* dst = W + (size_t)base * WR;
             for (int k = t; k < n * WR; k += kLinThreads) dst[k] = wst[(k / WR) * WRP + k % WR];
         }
@@ -377,7 +389,9 @@ __global__ __launch_bounds__(NT) void k_lin_cams_reg(const int* __restrict__ cam
 __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* __restrict__ V, const double* __restrict__ gp,
                                                          double f, double cmin, double cmax, double* __restrict__ Vinv,
                                                          double* __restrict__ y, int* __restrict__ flags,
-                                                         int* __restrict__ status) {
+                                                         int* __restrict__ status, const double* __restrict__ pts,
+                                                         double* __restrict__ ptrec) {
+    // ptrec (the re-deriving Schur): per point {V^-1 (6), y (3), X (3)} in one 96-B record
     const int p = blockIdx.x * kThreads + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0;  // the CG status word of this solve
     if (p >= Pl) return;
@@ -396,9 +410,21 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 #pragma unroll
     for (int k = 0; k < 6; ++k) Vinv[6 * (size_t)p + k] = o[k];
     const double g0 = gp[3 * (size_t)p], g1 = gp[3 * (size_t)p + 1], g2 = gp[3 * (size_t)p + 2];
-    y[3 * (size_t)p + 0] = o[0] * g0 + o[1] * g1 + o[2] * g2;
-    y[3 * (size_t)p + 1] = o[1] * g0 + o[3] * g1 + o[4] * g2;
-    y[3 * (size_t)p + 2] = o[2] * g0 + o[4] * g1 + o[5] * g2;
+    const double y0 = o[0] * g0 + o[1] * g1 + o[2] * g2;
+    const double y1 = o[1] * g0 + o[3] * g1 + o[4] * g2;
+    const double y2 = o[2] * g0 + o[4] * g1 + o[5] * g2;
+    y[3 * (size_t)p + 0] = y0;
+    y[3 * (size_t)p + 1] = y1;
+    y[3 * (size_t)p + 2] = y2;
+    if (ptrec) {
+        double2* r = reinterpret_cast<double2*>(ptrec + 12 * (size_t)p);
+        r[0] = make_double2(o[0], o[1]);
+        r[1] = make_double2(o[2], o[3]);
+        r[2] = make_double2(o[4], o[5]);
+        r[3] = make_double2(y0, y1);
+        r[4] = make_double2(y2, pts[3 * (size_t)p]);
+        r[5] = make_double2(pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1245,6 +1271,23 @@ struct insfm_ba {
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
+    // re-deriving Schur (ba_schur_rc.h; BA, non-deterministic): its own row chunks, per-observation {sqrt(w), camera},
+    // per-point {V^-1, y, X}; W is then never formed
+    bool schur_rc = false;
+    int4* work_rc = nullptr;
+    int nwork_rc = 0;
+    size_t schur_rc_lds = 0;
+    double2* obrec = nullptr;
+    double* ptrec = nullptr;
+    const double* cams_lin = nullptr;  // camera rows of the last linearization (caller's or internal buffer)
+    // MFMA-accumulating variant (ba_schur_mf.h, D <= 8): work items, batch-ordered own descriptors, staging positions
+    bool schur_mf = false;
+    MfWork* mf_work = nullptr;
+    int n_mf_work = 0, mf_pcap = 0;
+    int4* mf_sd = nullptr;
+    unsigned short* mf_ppos = nullptr;
+    int* mf_boff = nullptr;
+    size_t schur_mf_lds = 0;
     // numeric (device)
     double *W = nullptr, *V = nullptr, *gp = nullptr, *Vinv = nullptr, *y = nullptr, *dp = nullptr;
     double *xbuf = nullptr;  // [S | b | U | gc | scal]
@@ -1493,6 +1536,7 @@ int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
 // ---- phases --------------------------------------------------------------------------------------------------
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     h->tl_fresh = true;
+    h->cams_lin = cams;  // the re-deriving Schur evaluates the camera Jacobians at this linearization point
     if (h->kind == 1) {
         if (h->Nl > 0)
             k_gp_lin<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, h->sfree,
@@ -1505,9 +1549,16 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
-        if (h->Pl > 0)
-            k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
-                                                                 pts_local, h->d.huber_delta, h->W, h->V, h->gp);
+        if (h->Pl > 0) {
+            if (h->schur_rc)
+                k_lin_points<M, false><<<h->n_lin, kLinThreads, 0, h->stream>>>(
+                    h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, pts_local, h->d.huber_delta, nullptr, h->V,
+                    h->gp, h->obrec);
+            else
+                k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
+                                                                     cams, pts_local, h->d.huber_delta, h->W, h->V, h->gp,
+                                                                     nullptr);
+        }
         static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
         if constexpr (D <= 9) {
             if (!batch_form) {
@@ -1632,6 +1683,28 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
                 h->probe);
         return launch_err(h, "k_schur");
     }
+    if (h->schur_mf) {
+        return with_model(h->model, [&](auto mc) -> int {
+            constexpr int M = decltype(mc)::value;
+            if constexpr (kD<M> <= 8) {
+                k_schur_mf<M><<<h->n_mf_work, 256, h->schur_mf_lds, h->stream>>>(
+                    h->mf_work, h->row_ptr, h->col, h->C, h->mf_sd, h->mf_ppos, h->mf_boff, h->mf_pcap, h->obrec, h->ptrec,
+                    h->cams_lin, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+                return launch_err(h, "k_schur_mf");
+            } else {
+                return INSFM_BA_EINVAL;
+            }
+        });
+    }
+    if (h->schur_rc) {
+        return with_model(h->model, [&](auto mc) -> int {
+            constexpr int M = decltype(mc)::value;
+            k_schur_rc<M, SCHUR_RC_WAVES><<<h->nwork_rc, SCHUR_RC_WAVES * 64, h->schur_rc_lds, h->stream>>>(
+                h->work_rc, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->obrec, h->ptrec, h->cams_lin, Uin, gcin, sf,
+                smin, smax, sdiag, h->S, h->b);
+            return launch_err(h, "k_schur_rc");
+        });
+    }
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (det)
@@ -1675,7 +1748,8 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                                                                      h->gpc);
     } else if (h->Pl > 0)
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
-                                                                       h->Vinv, h->y, h->flags, h->cg.status);
+                                                                       h->Vinv, h->y, h->flags, h->cg.status, pts_local,
+                                                                       h->schur_rc ? h->ptrec : nullptr);
     int iters = 0;
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
@@ -1819,7 +1893,8 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (rc) return rc;
         return iters;
     }
-    static const bool backsub_w = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
+    static const bool backsub_w_env = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
+    const bool backsub_w = backsub_w_env && h->W != nullptr;
     int rc = backsub_w ? with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (h->Pl > 0)
@@ -2216,6 +2291,107 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->max_chunk = maxc;
     h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
+    // Schur variant (INSFM_SCHUR): "w" (default) reads the stored W records (k_schur); "rc" re-derives the camera-point
+    // blocks per pair and adds them with LDS atomics (ba_schur_rc.h); "mf" re-derives them and accumulates in MFMA
+    // registers (ba_schur_mf.h, D <= 8).  Measured on config 3: w 0.51 ms, rc 0.68-0.70 ms
+    // (LDS-atomic bound), mf 1.2-1.6 ms (latency / barrier bound); rc / mf save the 384-MB W write of k_lin_points.
+    static const char* schur_env = std::getenv("INSFM_SCHUR");
+    const std::string schur_kind = schur_env ? std::string(schur_env)
+                                             : (desc->schur_variant == 1 ? "rc" : (desc->schur_variant == 2 ? "mf" : "w"));
+    h->schur_rc = kind == 0 && !desc->deterministic && desc->optimize_poses && (schur_kind == "rc" || schur_kind == "mf");
+    std::vector<int4> work_rc;
+    if (h->schur_rc) {
+        // chunks sized for its LDS layout (block + camera-table entry per slot)
+        int rc_cap = 0;
+        with_model(h->model, [&](auto mc) -> int {
+            constexpr int M = decltype(mc)::value;
+            const size_t fixed = schur_rc_lds_bytes<M>(0, C);
+            const size_t per = sizeof(double) * (schur_rc_bs(D) + kCamTab<M>);
+            rc_cap = fixed + per > (size_t)kLdsBudget ? 0 : (int)((kLdsBudget - fixed) / per);
+            return 0;
+        });
+        if (rc_cap < 1) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
+        int maxrc = 1;
+        for (int i = 0; i < C; ++i) {
+            for (int kb = rptr[i]; kb < rptr[i + 1]; kb += rc_cap) {
+                const int ke = std::min(kb + rc_cap, rptr[i + 1]);
+                work_rc.push_back(make_int4(i, kb, ke, 0));
+                maxrc = std::max(maxrc, ke - kb);
+            }
+        }
+        h->nwork_rc = (int)work_rc.size();
+        with_model(h->model, [&](auto mc) -> int {
+            h->schur_rc_lds = schur_rc_lds_bytes<decltype(mc)::value>(maxrc, C);
+            return 0;
+        });
+    }
+    // MFMA-accumulating variant for D <= 8 (ba_schur_mf.h): rows in chunks of <= 64 blocks; each chunk's own
+    // observations in batches of 64 taken round-robin from the camera's list (sorted by partner count), so every batch
+    // carries about the average number of pairs; every pair's staging position groups the batch's pairs by
+    // destination block (own order, then partner order, inside a block).
+    const bool no_mf = schur_kind != "mf";
+    std::vector<MfWork> mfw;
+    std::vector<int4> mfsd;
+    std::vector<unsigned short> mfpp;
+    std::vector<int> mfbo;
+    if (h->schur_rc && D <= 8 && !no_mf) {
+        std::vector<int> slotmap(C, -1), cnt(kMfSlots + 1), run(kMfSlots + 1);
+        int pcap = 0;
+        bool ok = true;
+        for (int i = 0; i < C && ok; ++i) {
+            const int n_own = cptr[i + 1] - cptr[i];
+            for (int kb = rptr[i]; kb < rptr[i + 1]; kb += kMfSlots) {
+                const int ke = std::min(kb + kMfSlots, rptr[i + 1]);
+                for (int e = kb; e < ke; ++e) slotmap[cols[e]] = e - kb;
+                const int nbat = (n_own + kMfOwn - 1) / kMfOwn;
+                MfWork w{i, kb, ke, nbat, (int)(mfbo.size() / kMfBR), 0, 0, 0};
+                for (int bt = 0; bt < nbat; ++bt) {
+                    std::fill(cnt.begin(), cnt.end(), 0);
+                    std::vector<int> members;
+                    for (int k = bt; k < n_own; k += nbat) members.push_back(cptr[i] + k);
+                    if ((int)members.size() > kMfOwn) { ok = false; break; }
+                    for (int e : members) {
+                        const int4 d = sdesc[e];
+                        for (int q = d.z; q < d.w; ++q) {
+                            const int sl = slotmap[lcam[q]];
+                            if (sl >= 0) cnt[sl]++;
+                        }
+                    }
+                    std::vector<int> bo(kMfSlots + 1, 0);
+                    for (int sl = 0; sl < kMfSlots; ++sl) bo[sl + 1] = bo[sl] + cnt[sl];
+                    pcap = std::max(pcap, bo[kMfSlots]);
+                    for (int sl = 0; sl <= kMfSlots; ++sl) mfbo.push_back(bo[sl]);
+                    mfbo.push_back((int)mfsd.size());
+                    mfbo.push_back((int)members.size());
+                    std::copy(bo.begin(), bo.end(), run.begin());
+                    for (int e : members) {
+                        const int4 d = sdesc[e];
+                        const int n = d.w - d.z, ofs = d.x - d.z;
+                        if (n >= 0x10000 || ofs >= 0x10000) { ok = false; break; }
+                        mfsd.push_back(make_int4(d.y, d.z, n | (ofs << 16), (int)mfpp.size()));
+                        for (int q = d.z; q < d.w; ++q) {
+                            const int sl = slotmap[lcam[q]];
+                            mfpp.push_back(sl >= 0 ? (unsigned short)run[sl]++ : (unsigned short)0xffff);
+                        }
+                    }
+                    if (bo[kMfSlots] >= 0xffff) ok = false;
+                }
+                for (int e = kb; e < ke; ++e) slotmap[cols[e]] = -1;
+                mfw.push_back(w);
+            }
+        }
+        size_t lds = 0;
+        with_model(h->model, [&](auto mc) -> int {
+            lds = schur_mf_lds_bytes<decltype(mc)::value>(std::max(pcap, 16), C);
+            return 0;
+        });
+        if (ok && lds <= (size_t)kLdsBudget) {
+            h->schur_mf = true;
+            h->mf_pcap = std::max(pcap, 16);  // >= 16: the slot-0 quarters are summed in the staging area
+            h->schur_mf_lds = lds;
+            h->n_mf_work = (int)mfw.size();
+        }
+    }
 
     int rc;
     if (kind == 1) {
@@ -2289,7 +2465,22 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     }
     if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
     auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
-    if ((rc = dd(&h->W, (size_t)Nl * D * 3))) return fail(rc, "");
+    if (h->schur_mf) {
+        if (mfsd.empty()) mfsd.push_back(make_int4(0, 0, 0, 0));
+        if (mfbo.empty()) mfbo.assign(kMfBR, 0);
+        if ((rc = upload(h, &h->mf_work, mfw.data(), mfw.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->mf_sd, mfsd.data(), mfsd.size()))) return fail(rc, "");
+        if (mfpp.empty()) mfpp.push_back(0xffff);
+        if ((rc = upload(h, &h->mf_ppos, mfpp.data(), mfpp.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->mf_boff, mfbo.data(), mfbo.size()))) return fail(rc, "");
+    }
+    if (h->schur_rc) {  // W is never formed
+        if ((rc = upload(h, &h->work_rc, work_rc.data(), work_rc.size()))) return fail(rc, "");
+        if ((rc = dalloc(h, (void**)&h->obrec, sizeof(double2) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dd(&h->ptrec, (size_t)std::max(Pl, 1) * 12))) return fail(rc, "");
+    } else if ((rc = dd(&h->W, (size_t)Nl * D * 3))) {
+        return fail(rc, "");
+    }
     if ((rc = dd(&h->V, (size_t)Pl * 6))) return fail(rc, "");
     if ((rc = dd(&h->gp, (size_t)Pl * 3))) return fail(rc, "");
     if ((rc = dd(&h->Vinv, (size_t)Pl * 6))) return fail(rc, "");
@@ -2352,6 +2543,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("init: ") + hipGetErrorString(e));
     }
     // the Schur kernels may need more than the default dynamic-LDS limit
+    if (h->schur_rc)
+        with_model(h->model, [&](auto mc) -> int {
+            constexpr int M = decltype(mc)::value;
+            (void)hipFuncSetAttribute((const void*)k_schur_rc<M, SCHUR_RC_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->schur_rc_lds);
+            if constexpr (kD<M> <= 8)
+                if (h->schur_mf)
+                    (void)hipFuncSetAttribute((const void*)k_schur_mf<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)h->schur_mf_lds);
+            return 0;
+        });
     with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
@@ -2688,7 +2890,9 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     const double* src = nullptr;
     size_t n = 0;
     switch (which) {
-        case 0: src = h->W; n = Nl * D * 3; break;
+        case 0:
+            if (!h->W) { h->err = "W is not formed by the re-deriving Schur (use deterministic = 1 or INSFM_SCHUR_W=1)"; return INSFM_BA_EINVAL; }
+            src = h->W; n = Nl * D * 3; break;
         case 1: src = h->V; n = Pl * 6; break;
         case 2: src = h->gp; n = Pl * 3; break;
         case 3: src = h->U; n = C * D * D; break;

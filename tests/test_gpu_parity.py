@@ -339,3 +339,41 @@ def test_solver_failure_leaves_caller_buffers_unchanged():
     lo = ora.step(co, po)
     assert ora.stats()["failed"] == 1 and abs(lo - l0) <= 1e-12 * l0
     assert np.array_equal(co, prob.cams_init) and np.array_equal(po, prob.points_init)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("model", (0, 2, 4, 9))
+def test_schur_variant_solve_parity(model, variant):
+    """The re-deriving Schur builds (desc.schur_variant 1: LDS-atomic rows, 2: MFMA register accumulation for D <= 8;
+    D > 8 falls back to 1) against the oracle: b, S~, dc, dp at equal PCG iterations, same tolerances as
+    test_solve_parity.  They never form W, so the camera-point blocks are checked through S~."""
+    prob = make_problem(30, 800, seed=5, model=model)
+    eng, ora = engines(prob, schur_variant=variant)
+    eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
+    ora.linearize(prob.cams_init, prob.points_init)
+    f = 1.0 + 1e-4
+    assert eng.debug_solve(f) == ora.solve(f)
+    C, P, D = prob.n_cams, prob.n_points, eng.D
+    nb = eng.nnzb()
+    assert rel(eng.debug_get(6, (C, D)), ora.get(O.B)) < 1e-10
+    assert rel(eng.debug_get(5, (nb, D, D)), ora.get(O.S)) < 1e-9
+    assert rel(eng.debug_get(7, (C, D)), ora.get(O.DC)) < 1e-8
+    assert rel(eng.debug_get(8, (P, 3)), ora.get(O.DP)) < 1e-8
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_schur_variant_step_parity(variant):
+    """Config 2 LM steps with the re-deriving Schur builds: same trials / PCG iterations as the oracle, parameters
+    1e-9 (long rows: more than 64 upper blocks split into several work items)."""
+    prob = make_config(2)
+    eng, ora = engines(prob, schur_variant=variant)
+    cg, pg = dev(prob.cams_init), dev(prob.points_init)
+    co, po = prob.cams_init.copy(), prob.points_init.copy()
+    for s in range(2):
+        lg, st = eng.step(cg, pg)
+        lo = ora.step(co, po)
+        so = ora.stats()
+        assert st["pcg_iters"] == so["pcg_iters"] and st["trials"] == so["trials"], (s, st, so)
+        assert abs(lg - lo) / lo < 1e-10, (s, lg, lo)
+        assert rel(cg.cpu().numpy(), co) < 1e-9
+        assert rel(pg.cpu().numpy(), po) < 1e-9
