@@ -9,6 +9,7 @@ TrustRegion accept/reject) over the whole scene.  Inputs are resident in HBM bef
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL all-reduce of the camera system)
     python bench.py --path gp ...   global positioning (TorchGP.Optimize's LM) on the same scene geometry
+    python bench.py --path tracks|passes|mapper   track establishment, the between-round passes, the config-5 mapper
 
 
 Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) is the build's C/OpenMP restatement of the same LM
@@ -445,6 +446,162 @@ def cpu_baseline_passes(seed):
                       f"scene of the same generator, {dt:.2f} s; CPU: {_cpu_model()}"}
 
 
+def solve_end_to_end(prob, dev):
+    """TorchBA.Solve (bundle_adjustment.py:44-154) on the scene objects of the same problem (cameras, images, a
+    dict of Track; built untimed): the wall-time split of one converged Solve -- host packing, engine creation
+    (H2D copies + insfm_ba_create's host sort / pattern / clustering), the LM steps to the reference stop rule, the
+    write-back -- as the reference's callers see it (global_mapper.py:114-116)."""
+    from instantsfm_amd.config.colmap import BUNDLE_ADJUSTER_OPTIONS
+    from instantsfm_amd.processors.bundle_adjustment import TorchBA
+    from instantsfm_amd.synth import to_scene
+    cams, ims, tracks = to_scene(prob)
+    ba = TorchBA(device=str(dev))
+    ba.Solve(cams, ims, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
+    t = ba.timings
+    host = t["pack_s"] + t["create_s"] + t["update_s"]
+    return {"solve_total_s": round(t["total_s"], 4), "pack_s": round(t["pack_s"], 4),
+            "create_s": round(t["create_s"], 4), "steps_s": round(t["steps_s"], 4),
+            "update_s": round(t["update_s"], 4), "steps": t["steps"], "host_frac": round(host / t["total_s"], 4),
+            "final_rmse_px": t.get("final_rmse")}
+
+
+def _run_mapper_once(db_path, scene, device, seed):
+    import contextlib
+    import io
+    import numpy as np
+    from instantsfm_amd.controllers.data_reader import ReadColmapDatabase
+    from instantsfm_amd.controllers.config import Config
+    from instantsfm_amd.controllers.global_mapper import SolveGlobalMapper
+    from instantsfm_amd.synth import stand_in_rotation_averaging
+    T = {}
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        vg, cams, ims, fn = ReadColmapDatabase(db_path)
+    T['read_database_s'] = time.perf_counter() - t0
+    stand_in_rotation_averaging(vg, ims, scene, seed=seed)
+    np.random.seed(seed)
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        SolveGlobalMapper(vg, cams, ims, Config.for_ba_half(fn), device=device, timings=T)
+    T['mapper_s'] = time.perf_counter() - t0
+    return T, ims
+
+
+def run_mapper(args):
+    """Config 5: COLMAP database.db -> ReadColmapDatabase -> SolveGlobalMapper from track establishment on
+    (global_mapper.py:80-146: TrackEngine, GP, 3 x [BA, undistort, filter], filters, normalize, RetriangulateTracks,
+    BA, filters) on a seeded ~500-image database (synth.write_mapper_database).  The stages before track
+    establishment are out of scope; their outputs come from synth.stand_in_rotation_averaging.  One "step" = one
+    whole mapper run; the value is the wall time of the run (host + device), per-stage times beside it.
+    N GPUs: independent replicas (the mapper itself does not shard)."""
+    import tempfile
+    import numpy as np
+    import torch
+    from instantsfm_amd.synth import write_mapper_database
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    tmp = tempfile.mkdtemp(prefix="insfm_mapper_")
+    db = os.path.join(tmp, f"database_{rank}.db")
+    t0 = time.perf_counter()
+    scene = write_mapper_database(db, n_images=args.mapper_images, n_points=args.mapper_points, seed=args.seed)
+    gen_s = time.perf_counter() - t0
+    if args.warmup:
+        small = os.path.join(tmp, f"warm_{rank}.db")
+        sc = write_mapper_database(small, n_images=40, n_points=3000, track_len=6, window=6, reach=2,
+                                   images_per_camera=10, distractors=50, seed=args.seed)
+        _run_mapper_once(small, sc, dev, args.seed)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    runs = []
+    t0 = time.perf_counter()
+    for _ in range(args.mapper_runs):
+        T, ims = _run_mapper_once(db, scene, dev, args.seed)
+        runs.append(T)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    T = runs[-1]
+    C = np.array([im.center() for im in ims])
+    G = scene.centers_gt
+    mc, mg = C.mean(0), G.mean(0)
+    U, sv, Vt = np.linalg.svd((G - mg).T @ (C - mc))
+    sc_ = sv.sum() / np.sum((C - mc) ** 2)
+    center_err = float(np.linalg.norm(sc_ * (C - mc) @ (U @ Vt).T + mg - G, axis=1).max())
+    r3 = lambda x: round(float(x), 4)  # noqa: E731
+    stages = {k: r3(T[k]) for k in ('read_database_s', 'track_establishment_s', 'global_positioning_s',
+                                    'bundle_adjustment_s', 'retriangulation_s') if k in T}
+    ba = [{k: (r3(v) if isinstance(v, float) else v) for k, v in b.items()} for b in T['ba']]
+    ba_host = sum(b['pack_s'] + b['create_s'] + b['update_s'] for b in T['ba'])
+    ba_total = sum(b['total_s'] for b in T['ba'])
+    per_run = dt / args.mapper_runs
+    out = {
+        "metric": "config-5 mapper (BA half: tracks -> GP -> 3x BA + filters -> retriangulation -> BA) wall time",
+        "value": round(per_run, 3), "unit": "s per mapper run", "n_gpus": world, "steps": args.mapper_runs,
+        "warmup": args.warmup, "ms_per_step": round(per_run * 1e3, 1), "higher_is_better": False,
+        "scaling": "weak" if world > 1 else "strong", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic COLMAP database.db (instantsfm_amd/synth.py write_mapper_database), rotations = GT + "
+                "0.1 deg (stand-in for the out-of-scope rotation averaging)",
+        "config": {"workload": f"config 5: {scene.n_images} images / {scene.n_points} points / {scene.n_pairs} pairs / "
+                               f"{scene.n_matches} matches -> {T.get('tracks_problem')} tracks",
+                   "images": scene.n_images, "matches": scene.n_matches, "pairs": scene.n_pairs,
+                   "parallelism": f"replicas x{world}" if world > 1 else "single GPU"},
+        "stages_s": stages, "gp": {k: (r3(v) if isinstance(v, float) else v) for k, v in T['gp'].items()},
+        "ba_solves": ba, "ba_host_s": r3(ba_host), "ba_total_s": r3(ba_total),
+        "ba_host_frac": r3(ba_host / ba_total) if ba_total else None,
+        "trace": [[t[0], t[1], t[2], None if t[3] is None else float(t[3])] for t in T['trace']],
+        "camera_center_err_max": round(center_err, 5), "db_generation_s": round(gen_s, 2),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_mapper(args, tmp, dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline_mapper(args, tmp, dev):
+    """The oracle-stage pipeline (oracle/mapper.py: the reference's union-find and passes restated in numpy / Python,
+    the C/OpenMP LM restatement for GP and BA) on a 100-image / 20k-point database of the same generator, beside the
+    GPU mapper on the same sample."""
+    import contextlib
+    import io
+    import numpy as np
+    from instantsfm_amd.controllers.data_reader import ReadColmapDatabase
+    from instantsfm_amd.controllers.config import Config
+    from instantsfm_amd.synth import stand_in_rotation_averaging, write_mapper_database
+    from oracle import mapper as OM
+    path = os.path.join(tmp, "cpu_sample.db")
+    scene = write_mapper_database(path, n_images=100, n_points=20000, seed=args.seed)
+    Tg, _ = _run_mapper_once(path, scene, dev, args.seed)
+    with contextlib.redirect_stdout(io.StringIO()):
+        vg, cams, ims, fn = ReadColmapDatabase(path)
+    stand_in_rotation_averaging(vg, ims, scene, seed=args.seed)
+    np.random.seed(args.seed)
+    t0 = time.perf_counter()
+    with contextlib.redirect_stdout(io.StringIO()):
+        OM.solve_global_mapper(vg, cams, ims, Config.for_ba_half(fn))
+    dt = time.perf_counter() - t0
+    return {"value": round(dt, 2), "unit": "s per mapper run", "cores": int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0)), "kind": "port",
+            "sample": f"oracle/mapper.py on a 100-image / 20000-point / {scene.n_matches}-match database of the same "
+                      f"generator: {dt:.2f} s; the GPU mapper on the same sample: {Tg['mapper_s']:.2f} s; "
+                      f"CPU: {_cpu_model()}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -453,10 +610,14 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-solve", action="store_true", help="skip the end-to-end TorchBA.Solve split")
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
-    ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes"), default="ba")
+    ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes", "mapper"), default="ba")
+    ap.add_argument("--mapper-images", type=int, default=500, help="--path mapper: images in the database")
+    ap.add_argument("--mapper-points", type=int, default=100_000, help="--path mapper: scene points")
+    ap.add_argument("--mapper-runs", type=int, default=1, help="--path mapper: timed mapper runs")
     ap.add_argument("--cpu-edges", type=int, default=1_500_000, help="--path tracks: matches in the CPU sample")
     args = ap.parse_args()
     if args.path == "gp":
@@ -465,6 +626,8 @@ def main():
         return run_tracks(args)
     if args.path == "passes":
         return run_passes(args)
+    if args.path == "mapper":
+        return run_mapper(args)
 
     import numpy as np
     import torch
@@ -611,6 +774,8 @@ def main():
         "preconditioner": "two-level (block-Jacobi + camera-cluster similarity coarse space)" if tl else "block-Jacobi",
         "roofline": roof,
     }
+    if rank == 0 and world == 1 and not args.no_solve:
+        out["solve_end_to_end"] = solve_end_to_end(prob, dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb = cpu_baseline(prob, args.cpu_max_steps)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}

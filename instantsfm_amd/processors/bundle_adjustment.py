@@ -4,6 +4,8 @@ Same constructor and ``Solve(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)``
 stop rule and in-place write-back; the LM engine underneath is the MI355X HIP library (``engine.BundleAdjuster``)
 instead of bae/pypose.  Packing (reference :66-113, a Python double loop over tracks x observations) is vectorized.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -12,10 +14,10 @@ from ..scene.defs import CameraModelId, IMPLEMENTED_MODELS, get_camera_model_inf
 
 
 def _quat_xyzw_from_matrix(R):
-    """pp.mat2SE3 rotation part: rotation matrix -> quaternion [x, y, z, w] (sign: w >= 0)."""
+    """pp.mat2SE3 rotation part: rotation matrix (or a batch) -> quaternion [x, y, z, w] (sign: w >= 0)."""
     from scipy.spatial.transform import Rotation
     q = Rotation.from_matrix(np.asarray(R, dtype=np.float64)).as_quat()
-    return -q if q[3] < 0 else q
+    return np.where(q[..., 3:4] < 0, -q, q)
 
 
 def _pose_matrices(cam_rows):
@@ -50,10 +52,26 @@ def _as_torch_like_params(params):
     return arr
 
 
-def _rotate_quat(points, pose):
-    t, qv, w = pose[:, 0:3], pose[:, 3:6], pose[:, 6:7]
-    uv = np.cross(qv, points)
-    return points + 2.0 * (w * uv + np.cross(qv, uv)) + t
+def _rotated_z(points, pt, pose, cam):
+    """z of bae's rotate_quat(points[pt], pose[cam]) = p + 2(w (q x p) + q x (q x p)) + t, the same products and
+    sums as the vector form (numpy's cross), computed only for the z row; the per-observation operands are gathered
+    column by column from contiguous per-point / per-camera columns."""
+    P = np.ascontiguousarray(points.T)
+    Q = np.ascontiguousarray(pose[:, :7].T)
+    px, py, pz = P[0][pt], P[1][pt], P[2][pt]
+    qx, qy, qz, w = Q[3][cam], Q[4][cam], Q[5][cam], Q[6][cam]
+    uvx = qy * pz - qz * py
+    uvy = qz * px - qx * pz
+    uvz = qx * py - qy * px
+    return pz + 2.0 * (w * uvz + (qx * uvy - qy * uvx)) + Q[2][cam]
+
+
+def _compact(ids, n):
+    """np.unique(ids, return_inverse=True) for ids in [0, n): bincount instead of a sort."""
+    present = np.bincount(ids, minlength=n) > 0
+    uniq = np.flatnonzero(present)
+    remap = np.cumsum(present) - 1
+    return uniq, remap[ids]
 
 
 class PackedProblem:
@@ -82,46 +100,65 @@ def pack(cameras, images, tracks, options):
     if model.value not in IMPLEMENTED_MODELS:
         raise NotImplementedError("Unsupported camera model")
     track_keys = list(tracks.keys())
-    lengths = np.array([len(tracks[k].observations) for k in track_keys], dtype=np.int64)
+    track_vals = list(tracks.values())
+    obs_all = [t.observations for t in track_vals]
+    lengths = np.fromiter(map(len, obs_all), dtype=np.int64, count=len(obs_all))
     is_valid = lengths >= options['min_num_view_per_track']                                   # :66-68
     registered = np.array([img.is_registered for img in images], dtype=bool)                  # :70
-    rows = []
-    for img in images:                                                                        # :71-73
-        if img.is_registered:
-            w2c = np.asarray(img.world2cam, dtype=np.float64)
-            se3 = np.concatenate([w2c[:3, 3], _quat_xyzw_from_matrix(w2c[:3, :3])])
-        else:
-            se3 = np.array([0, 0, 0, 0, 0, 0, 1.0])
-        rows.append(np.concatenate([se3, _as_torch_like_params(cameras[img.cam_id].params)]))
-    camera_params = np.stack(rows).astype(np.float64)
+    # :71-73, one batched matrix -> quaternion conversion; unregistered images get the identity row
+    se3 = np.tile(np.array([0, 0, 0, 0, 0, 0, 1.0]), (len(images), 1))
+    reg = np.flatnonzero(registered)
+    if reg.size:
+        w2c = np.array([np.asarray(images[i].world2cam, dtype=np.float64) for i in reg.tolist()]).reshape(-1, 4, 4)
+        se3[reg, :3] = w2c[:, :3, 3]
+        se3[reg, 3:] = _quat_xyzw_from_matrix(w2c[:, :3, :3])
+    intr = {}
+    for img in images:
+        if img.cam_id not in intr:
+            intr[img.cam_id] = _as_torch_like_params(cameras[img.cam_id].params)
+    camera_params = np.concatenate([se3, np.array([intr[img.cam_id] for img in images])], axis=1).astype(np.float64)
     pp_indices = np.asarray(info['pp']) + 7                                                   # :75-80
     remaining = np.array([i for i in range(camera_params.shape[1]) if i not in pp_indices])
     camera_pps = camera_params[:, pp_indices]
     camera_params = camera_params[:, remaining]
-    points_3d = np.stack([np.asarray(tracks[k].xyz, dtype=np.float64) for k in track_keys])   # :82-83
+    xyz = [t.xyz for t in track_vals]                                                         # :82-83
+    try:
+        points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
+        if points_3d.shape[0] != len(xyz):
+            raise ValueError
+    except ValueError:
+        points_3d = np.stack([np.asarray(x, dtype=np.float64).reshape(3) for x in xyz])
 
-    valid_ids = np.nonzero(is_valid)[0]                                                       # :85-96
+    valid_ids = np.flatnonzero(is_valid)                                                      # :85-96
     if valid_ids.size:
-        obs = [np.asarray(tracks[track_keys[t]].observations).reshape(-1, 2) for t in valid_ids]
-        counts = np.array([o.shape[0] for o in obs])
-        obs = np.concatenate(obs).astype(np.int64)
-        tid = np.repeat(valid_ids, counts)
+        sel = [obs_all[t] for t in valid_ids.tolist()]
+        try:
+            obs = np.concatenate(sel)
+            if obs.ndim != 2 or obs.shape[1] != 2:
+                raise ValueError
+        except ValueError:
+            obs = np.concatenate([np.asarray(o).reshape(-1, 2) for o in sel])
+        obs = obs.astype(np.int64, copy=False)
+        tid = np.repeat(valid_ids, lengths[valid_ids])
     else:
         obs = np.zeros((0, 2), np.int64)
         tid = np.zeros(0, np.int64)
     img_id, feat_id = obs[:, 0], obs[:, 1]
     keep = registered[img_id]
-    img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
-    feats = [np.asarray(im.features, dtype=np.float64).reshape(-1, 2) for im in images]
-    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])])
-    feat_all = np.concatenate(feats) if feats else np.zeros((0, 2))
-    points_2d = feat_all[foff[img_id] + feat_id]
+    if not keep.all():
+        img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
+    feats = [np.asarray(im.features).reshape(-1, 2) for im in images]
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])]).astype(np.int64)
+    feat_all = np.ascontiguousarray(np.concatenate(feats), dtype=np.float64) if feats else np.zeros((0, 2))
+    # one 16-byte gather per observation (a row of feat_all viewed as one complex128)
+    points_2d = feat_all.view(np.complex128).reshape(-1)[foff[img_id] + feat_id].view(np.float64).reshape(-1, 2)
 
-    z = _rotate_quat(points_3d[tid], camera_params[img_id][:, :7])[:, 2]                      # :102-107
+    z = _rotated_z(points_3d, tid, camera_params, img_id)                                    # :102-107
     ok = z > 0.1
-    points_2d, img_id, tid = points_2d[ok], img_id[ok], tid[ok]
-    unique_cameras, cam_inv = np.unique(img_id, return_inverse=True)                          # :108-113
-    unique_points, pt_inv = np.unique(tid, return_inverse=True)
+    if not ok.all():
+        points_2d, img_id, tid = points_2d[ok], img_id[ok], tid[ok]
+    unique_cameras, cam_inv = _compact(img_id, len(images))                                   # :108-113
+    unique_points, pt_inv = _compact(tid, len(track_vals))
     return PackedProblem(model, np.ascontiguousarray(points_2d), cam_inv.astype(np.int64), pt_inv.astype(np.int64),
                          np.ascontiguousarray(camera_pps[unique_cameras]),
                          np.ascontiguousarray(camera_params[unique_cameras]),
@@ -137,12 +174,16 @@ def update(cameras, images, tracks, packed, camera_params, points_3d):
     full[:, packed.remaining_indices] = cp
     full[:, packed.pp_indices] = packed.camera_pps
     mats = _pose_matrices(full[:, :7])
-    for i, orig in enumerate(packed.unique_points.tolist()):
-        tracks[packed.track_keys[orig]].xyz = pts[i]
+    keys = packed.track_keys
+    for orig, xyz in zip(packed.unique_points.tolist(), pts):
+        tracks[keys[orig]].xyz = xyz
+    last = {}
     for i, image_id in enumerate(packed.unique_cameras.tolist()):
         image = images[image_id]
         image.world2cam = mats[i]
-        cameras[image.cam_id].set_params(full[i, 7:])
+        last[image.cam_id] = i            # :33-36 set_params per image: the last image of a camera wins
+    for cam_id, i in last.items():
+        cameras[cam_id].set_params(full[i, 7:])
 
 
 class TorchBA:
@@ -153,10 +194,18 @@ class TorchBA:
         self.visualizer = visualizer
         self.loss_history = []
         self.last_stats = None
+        self.timings = {}
 
     def Solve(self, cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=True):
+        """bundle_adjustment.py:44-154.  ``self.timings`` gets the wall-time split of the call (pack, create,
+        steps, write-back) and the step count."""
         opts = BUNDLE_ADJUSTER_OPTIONS
+        t0 = time.perf_counter()
         packed = pack(cameras, images, tracks, opts)
+        t1 = time.perf_counter()
+        self.timings = dict(pack_s=t1 - t0, create_s=0.0, steps_s=0.0, update_s=0.0, total_s=t1 - t0, steps=0,
+                            n_cams=int(packed.camera_params.shape[0]), n_points=int(packed.points_3d.shape[0]),
+                            n_obs=int(packed.points_2d.shape[0]))
         if packed.points_2d.shape[0] == 0:
             return
         # the engine wants track-major observations: point_indices from np.unique are already nondecreasing because
@@ -169,6 +218,7 @@ class TorchBA:
         dev = torch.device(self.device)
         cams_t = torch.from_numpy(packed.camera_params).to(dev).contiguous()
         pts_t = torch.from_numpy(packed.points_3d).to(dev).contiguous()
+        t2 = time.perf_counter()
         window_size = 4                                                                       # :128-150
         loss_history = []
         it = range(opts['max_num_iterations'])
@@ -200,6 +250,10 @@ class TorchBA:
         if bar is not None:
             bar.close()
         self.loss_history = loss_history
+        t3 = time.perf_counter()
         self.final_loss, self.final_rmse = eng.cost(cams_t, pts_t)
         update(cameras, images, tracks, packed, cams_t, pts_t)
         eng.close()
+        t4 = time.perf_counter()
+        self.timings.update(create_s=t2 - t1, steps_s=t3 - t2, update_s=t4 - t3, total_s=t4 - t0,
+                            steps=len(loss_history), final_rmse=self.final_rmse)

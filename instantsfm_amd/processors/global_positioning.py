@@ -6,6 +6,8 @@ GLOBAL_POSITIONER_OPTIONS, depth_only=False)``: same track / image filters (they
 the MI355X HIP library (``engine.GlobalPositioner``, include/insfm_gp.h) instead of bae/pypose; the packing loop
 (reference :114-152, Python over tracks x observations) is vectorized.
 """
+import time
+
 import numpy as np
 import torch
 
@@ -22,14 +24,15 @@ class PackedGP:
 def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     """Vectorized restatement of global_positioning.py:85-152.  Mutates ``tracks`` (drops short tracks) and
     ``images[*].is_registered`` (images left without tracks) exactly like the reference."""
-    for track_id in list(tracks.keys()):                                                        # :86-89
-        if tracks[track_id].observations.shape[0] < options['min_num_view_per_track']:
-            del tracks[track_id]
+    short = [k for k, t in tracks.items() if t.observations.shape[0] < options['min_num_view_per_track']]
+    for track_id in short:                                                                      # :86-89
+        del tracks[track_id]
+    track_list = list(tracks.values())
+    obs = [np.asarray(t.observations, dtype=np.int64).reshape(-1, 2) for t in track_list]
+    counts = np.fromiter(map(len, obs), dtype=np.int64, count=len(obs))
+    obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
     image_used = np.zeros(len(images), dtype=bool)                                              # :91-99
-    for track in tracks.values():
-        image_used[np.unique(np.asarray(track.observations)[:, 0])] = True
-        if all(image_used):
-            break
+    image_used[obs[:, 0]] = True  # the union over all tracks (the reference's early exit does not change it)
     for image_id, image in enumerate(images):
         if not image_used[image_id]:
             image.is_registered = False
@@ -38,18 +41,21 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     image_idx2id = np.nonzero(registered)[0]
     image_id2idx = -np.ones(len(images), dtype=np.int64)
     image_id2idx[image_idx2id] = np.arange(image_idx2id.size)
-    camera_translations = np.stack([np.asarray(images[i].world2cam, dtype=np.float64)[:3, 3]    # :108-109
-                                    for i in image_idx2id])
-    track_list = list(tracks.values())
-    points_3d = np.stack([np.asarray(t.xyz, dtype=np.float64) for t in track_list])             # :110-111
+    w2c = np.array([np.asarray(im.world2cam, dtype=np.float64) for im in images]).reshape(-1, 4, 4)
+    camera_translations = np.ascontiguousarray(w2c[image_idx2id, :3, 3])                        # :108-109
+    xyz = [t.xyz for t in track_list]                                                           # :110-111
+    try:
+        points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
+        if points_3d.shape[0] != len(xyz):
+            raise ValueError
+    except ValueError:
+        points_3d = np.stack([np.asarray(x, dtype=np.float64).reshape(3) for x in xyz])
 
-    obs = [np.asarray(t.observations, dtype=np.int64).reshape(-1, 2) for t in track_list]       # :120-138
-    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
-    obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
-    tid = np.repeat(np.arange(len(track_list)), counts)
+    tid = np.repeat(np.arange(len(track_list)), counts)                                         # :120-138
     img_id, feat_id = obs[:, 0], obs[:, 1]
     keep = registered[img_id]
-    img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
+    if not keep.all():
+        img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
     if depths is not None:
         dep = np.array([float(images[i].depths[f]) for i, f in zip(img_id.tolist(), feat_id.tolist())], dtype=np.float64)
         if depth_only:                                                                          # :129-130
@@ -60,10 +66,10 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     else:
         available = np.zeros(img_id.size, dtype=bool)
         scales = np.ones(img_id.size)                                                           # :146-147
-    rot = np.stack([np.asarray(images[i].world2cam, dtype=np.float64)[:3, :3] for i in range(len(images))])
+    rot = w2c[:, :3, :3]
     fu_list = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) if len(im.features_undist) else
                np.zeros((0, 3)) for im in images]
-    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu_list])])
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu_list])]).astype(np.int64)
     fu_all = np.concatenate(fu_list) if fu_list else np.zeros((0, 3))
     fu = fu_all[foff[img_id] + feat_id]
     translations = np.einsum('nki,nk->ni', rot[img_id], fu)                                     # :135  R^T f
@@ -86,6 +92,7 @@ class TorchGP:
         self.visualizer = visualizer
         self.loss_history = []
         self.last_stats = None
+        self.timings = {}
 
     def InitializeRandomPositions(self, cameras, images, tracks, depths=None):
         """global_positioning.py:23-39 (same draws from numpy's global RNG, in the same order)."""
@@ -112,7 +119,9 @@ class TorchGP:
         if depth_only and depths is None:                                                       # :46-48
             print("Warning: No depth maps provided, skip depth-only optimization.")
             return
+        t0 = time.perf_counter()
         pk = pack_gp(cameras, images, tracks, depths, opts, depth_only)
+        t1 = time.perf_counter()
         C, P = pk.camera_translations.shape[0], pk.points_3d.shape[0]
         eng = GlobalPositioner(pk.translations, pk.camera_indices, pk.point_indices,
                                np.where(pk.is_calibrated, 1.0, 0.5), pk.scale_free, C, P, device=self.device,
@@ -122,6 +131,7 @@ class TorchGP:
         pos_t = torch.from_numpy(pk.camera_translations).to(dev).contiguous()
         pts_t = torch.from_numpy(pk.points_3d).to(dev).contiguous()
         scl_t = torch.from_numpy(pk.scales).to(dev).contiguous()
+        t2 = time.perf_counter()
         window_size = 4                                                                         # :172-186
         loss_history = []
         it = range(opts['max_num_iterations'])
@@ -152,17 +162,21 @@ class TorchGP:
         if bar is not None:
             bar.close()
         self.loss_history = loss_history
+        t3 = time.perf_counter()
         self.final_loss, self.final_rmse = eng.cost(pos_t, pts_t, scl_t)
         self.scales = scl_t.cpu().numpy()
         self._write_back(images, pk, pos_t, pts_t)                                              # :199-206
         self.ConvertResults(images)
         eng.close()
+        t4 = time.perf_counter()
+        self.timings = dict(pack_s=t1 - t0, create_s=t2 - t1, steps_s=t3 - t2, update_s=t4 - t3, total_s=t4 - t0,
+                            steps=len(loss_history), n_cams=C, n_points=P, n_obs=int(pk.translations.shape[0]))
 
     @staticmethod
     def _write_back(images, pk, pos_t, pts_t):
         pts = pts_t.detach().cpu().numpy()
         pos = pos_t.detach().cpu().numpy()
-        for k, track in enumerate(pk.track_list):
-            track.xyz = pts[k]
+        for track, xyz in zip(pk.track_list, pts):
+            track.xyz = xyz
         for idx, image_id in enumerate(pk.image_idx2id.tolist()):
             images[image_id].world2cam[:3, 3] = pos[idx]

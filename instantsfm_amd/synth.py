@@ -519,3 +519,119 @@ def make_match_graph(n_images=500, n_points=600_000, track_len=8, window=12, rea
     images = [Image(id=c, cam_id=0, features=rng.uniform([0, 0], [2000, 1500], (nfeat[c], 2)).astype(np.float32))
               for c in range(C)]
     return vg, images
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Config-5 mapper scenes: a COLMAP database.db with geometrically consistent tracks (global_mapper.py:80-146)
+# ------------------------------------------------------------------------------------------------------------
+@dataclass
+class MapperScene:
+    """What write_mapper_database wrote, plus the ground truth the stand-in for rotation averaging draws from."""
+    path: str
+    n_images: int
+    n_points: int
+    n_matches: int
+    n_pairs: int
+    rot_gt: np.ndarray       # [C, 3, 3] world-to-camera rotations, DB image order (= reader's list order)
+    centers_gt: np.ndarray   # [C, 3]
+    points_gt: np.ndarray    # [P, 3]
+
+
+def write_mapper_database(path, n_images=500, n_points=100_000, track_len=8, window=12, reach=3, seed=0,
+                          images_per_camera=50, distractors=200, wrong_frac=0.01, min_matches=15,
+                          focal_sigma=0.01):
+    """Write a seeded COLMAP database.db (utils/database.py schema) for the mapper's BA half (config 5).
+
+    Geometry is make_problem's ring (SIMPLE_RADIAL, GT f = 1000, k = -0.02, 0.5 px noise, 1 % outliers): each point
+    is seen by ``track_len`` distinct images of a window of 2*window+1 consecutive ones.  Keypoints are those
+    observations (float32, COLMAP's type) plus ``distractors`` random ones per image, shuffled.  Matches are the
+    sequential-matching subset of every track (observations at most ``reach`` apart in camera order) plus
+    ``wrong_frac`` random wrong matches; a pair with fewer than ``min_matches`` matches is not stored.  Each stored
+    pair gets a matches row and a two_view_geometries row holding the same matches (config CALIBRATED, a few
+    UNCALIBRATED).  Cameras are shared by ``images_per_camera`` images; their stored focal is the GT one times
+    1 + N(0, focal_sigma^2) and their distortion 0 (BA recovers both).  Vectorized: a 500-image database in seconds."""
+    from .utils.database import COLMAPDatabase
+    rng = np.random.default_rng([seed, 5])
+    prob = make_problem(n_images, n_points, track_len=track_len, seed=seed, window=window)
+    C, P, L = prob.n_cams, prob.n_points, int(track_len)
+    cam_idx = prob.cam_idx.astype(np.int64)
+    n_obs = cam_idx.size
+    n_obs_img = np.bincount(cam_idx, minlength=C)
+    nfeat = n_obs_img + distractors
+    # feature slot of every observation: a random permutation of its image's keypoints
+    order = np.argsort(cam_idx, kind="stable")
+    start = np.concatenate([[0], np.cumsum(n_obs_img)])
+    rank = np.empty(n_obs, np.int64)
+    rank[order] = np.arange(n_obs) - start[cam_idx[order]]
+    slot_off = np.concatenate([[0], np.cumsum(nfeat)])
+    slots = np.concatenate([rng.permutation(int(n)) for n in nfeat])
+    feat = slots[slot_off[cam_idx] + rank]
+    kps = []
+    for c in range(C):
+        kp = np.empty((int(nfeat[c]), 2), np.float32)
+        kp[:] = rng.uniform([0, 0], [2000, 1500], (int(nfeat[c]), 2))
+        sel = order[start[c]:start[c + 1]]
+        kp[feat[sel]] = prob.uv[sel]
+        kps.append(kp)
+    # sequential matches inside each track
+    img = cam_idx.reshape(P, L)
+    ft = feat.reshape(P, L)
+    ai, af, bi, bf = [], [], [], []
+    for d in range(1, min(reach, L - 1) + 1):
+        ai.append(img[:, :-d].ravel()); af.append(ft[:, :-d].ravel())
+        bi.append(img[:, d:].ravel()); bf.append(ft[:, d:].ravel())
+    ai, af, bi, bf = (np.concatenate(x) for x in (ai, af, bi, bf))
+    n_wrong = int(wrong_frac * ai.size)
+    w = rng.integers(0, ai.size, n_wrong)                # wrong partner feature on an existing pair
+    ai = np.concatenate([ai, ai[w]]); bi = np.concatenate([bi, bi[w]]); af = np.concatenate([af, af[w]])
+    bf = np.concatenate([bf, (rng.uniform(size=n_wrong) * nfeat[bi[ai.size - n_wrong:]]).astype(np.int64)])
+    swap = ai > bi
+    ai[swap], bi[swap] = bi[swap], ai[swap].copy()
+    af[swap], bf[swap] = bf[swap], af[swap].copy()
+    key = ai * C + bi
+    o = np.lexsort((rng.uniform(size=key.size), key))
+    key, af, bf = key[o], af[o], bf[o]
+    ukey, first, cnt = np.unique(key, return_index=True, return_counts=True)
+
+    db = COLMAPDatabase.connect(path)
+    db.create_tables()
+    n_cam_rows = (C + images_per_camera - 1) // images_per_camera
+    f0 = 1000.0 * (1 + rng.normal(0, focal_sigma, n_cam_rows))
+    cam_ids = [db.add_camera(2, 2000, 1500, [f0[k], 1000.0, 750.0, 0.0], prior_focal_length=(k % 2 == 0))
+               for k in range(n_cam_rows)]
+    for c in range(C):
+        db.add_image(f"img_{c:04d}.jpg", cam_ids[c // images_per_camera], image_id=c + 1)
+        db.add_keypoints(c + 1, kps[c])
+    n_pairs = n_matches = 0
+    for k in range(ukey.size):
+        if cnt[k] < min_matches:
+            continue
+        i, j = divmod(int(ukey[k]), C)
+        m = np.stack([af[first[k]:first[k] + cnt[k]], bf[first[k]:first[k] + cnt[k]]], 1)
+        db.add_matches(i + 1, j + 1, m)
+        db.add_two_view_geometry(i + 1, j + 1, m, config=2 if rng.uniform() < 0.95 else 3)
+        n_pairs += 1
+        n_matches += int(cnt[k])
+    db.add_feature_name("colmap")
+    db.commit()
+    db.close()
+    Rgt = quat_to_matrix(prob.cams_gt[:, 3:7])
+    centers = -np.einsum('cji,cj->ci', Rgt, prob.cams_gt[:, :3])
+    return MapperScene(path, C, P, n_matches, n_pairs, Rgt, centers, prob.points_gt)
+
+
+def stand_in_rotation_averaging(view_graph, images, scene: MapperScene, rot_sigma_deg=0.1, seed=0):
+    """What the mapper's stages before track establishment leave behind (global_mapper.py:22-78, out of scope here):
+    every pair's inlier set (relpose estimation, image_pair_inliers.py) = the geometrically verified matches the
+    database's two_view_geometries rows hold, and every image registered with a world-to-camera rotation = ground
+    truth composed with a N(0, rot_sigma_deg^2) rotation (rotation averaging's output)."""
+    rng = np.random.default_rng([seed, 7])
+    for pair in view_graph.image_pairs.values():
+        pair.inliers = np.arange(len(pair.matches))
+    C = len(images)
+    dq = _quat_from_rotvec(rng.normal(0, np.deg2rad(rot_sigma_deg), (C, 3)))
+    R = np.einsum('cij,cjk->cik', quat_to_matrix(dq), scene.rot_gt)
+    for i, im in enumerate(images):
+        im.world2cam = np.eye(4)
+        im.world2cam[:3, :3] = R[i]
+        im.is_registered = True
