@@ -10,8 +10,8 @@ databases).  With a switch left off the mapper raises NotImplementedError instea
 
 ``timings`` (optional dict) receives the wall time of every stage and, per TorchGP / TorchBA call, its
 pack / create / steps / write-back split (``TorchGP.timings`` / ``TorchBA.timings``); ``timings['trace']`` lists
-(stage, tracks, observations, final LM loss or RMSE) after every stage -- what the oracle pipeline
-(oracle/mapper.py) records too, so the two can be compared stage by stage.
+(stage, tracks, observations, final LM loss or RMSE) after every stage -- what the tests' CPU restatement of the
+pipeline records too, so the two can be compared stage by stage.
 """
 import time
 
