@@ -54,14 +54,15 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
     raise ValueError(kernel)
 
 
-def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8):
+def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=16):
     """The oracle's LM to convergence on the same scene, repeated until >= min_seconds of CPU work (a bounded sample)."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
     dt, steps, runs = 0.0, 0, 0
     while runs < max_runs and (runs == 0 or dt < min_seconds):
         t0 = time.perf_counter()
-        cams, pts, hist, rmse = O.solve_to_convergence(prob, max_iters=max_steps, threads=threads)
+        cams, pts, hist, rmse = O.solve_to_convergence(prob, max_iters=max_steps, threads=threads,
+                                                       cluster_size=cluster_size)
         dt += time.perf_counter() - t0
         steps += len(hist)
         runs += 1
@@ -614,6 +615,7 @@ def main():
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
     ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
+    ap.add_argument("--cluster-size", type=int, default=16, help="two-level: target cameras per coarse cluster")
     ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes", "mapper"), default="ba")
     ap.add_argument("--mapper-images", type=int, default=500, help="--path mapper: images in the database")
     ap.add_argument("--mapper-points", type=int, default=100_000, help="--path mapper: scene points")
@@ -658,7 +660,7 @@ def main():
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
                          deterministic=args.deterministic, world_size=world, rank=rank, shard=shards[rank],
-                         precond=args.precond)
+                         precond=args.precond, cluster_size=args.cluster_size)
     cams0 = torch.from_numpy(prob.cams_init).to(dev)
     pts0 = torch.from_numpy(prob.points_init).to(dev)
     cams, pts = cams0.clone(), pts0.clone()
@@ -777,7 +779,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_solve:
         out["solve_end_to_end"] = solve_end_to_end(prob, dev)
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(prob, args.cpu_max_steps)
+        cb = cpu_baseline(prob, args.cpu_max_steps, cluster_size=args.cluster_size)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["cpu_final_rmse_px"] = cb["final_rmse_px"]
         out["cpu_steps_to_converge"] = cb["steps"]

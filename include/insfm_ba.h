@@ -60,7 +60,7 @@ typedef struct {
     int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
                               plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
                               Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
-    int32_t cluster_size;  /* target cameras per coarse cluster (default 32; doubled until nclust*(D+1) <= 288) */
+    int32_t cluster_size;  /* target cameras per coarse cluster (default 16; doubled until nclust*(D+1) <= 768) */
     int32_t schur_variant; /* reduced-system build (BA, deterministic = 0): 0 (default) reads the stored camera-point
                               blocks W; 1 re-derives them per pair, LDS-atomic row accumulation; 2 re-derives them,
                               MFMA register accumulation (D <= 8, else 1).  1 and 2 never form W (no 192 B/obs write).
@@ -138,6 +138,12 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
 int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);
 /* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */
 int64_t insfm_ba_nnzb(const insfm_ba* h);
+/* E^-1 of a dense SPD matrix (DEVICE pointers, row-major m x m, 1 <= m <= 4096) by the two-level preconditioner's
+ * blocked Gauss-Jordan kernels (k_gj_pivot / k_gj_update), on `stream` (NULL: the default stream); blocks until done.
+ * Returns 1 when E is positive definite, 0 when a pivot was not positive (Einv is then meaningless), or a negative
+ * code.  If us_per_inverse is non-NULL, the inversion is repeated `reps` times and the mean device time stored. */
+int insfm_ba_debug_spd_inverse(int32_t m, const double* E, double* Einv, void* stream, int32_t reps,
+                               double* us_per_inverse);
 
 #ifdef __cplusplus
 }

@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
 SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
-           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters",
+           "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters", "insfm_ba_debug_spd_inverse",
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
            "insfm_gp_debug_get_ds",
            "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
@@ -116,6 +116,8 @@ def load(path=None):
     L.insfm_ba_set_timing.restype = ctypes.c_int
     L.insfm_ba_debug_clusters.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
     L.insfm_ba_debug_clusters.restype = ctypes.c_int32
+    L.insfm_ba_debug_spd_inverse.argtypes = [ctypes.c_int32, vp, vp, vp, ctypes.c_int32, dp]
+    L.insfm_ba_debug_spd_inverse.restype = ctypes.c_int
     ip = ctypes.POINTER(ctypes.c_int32)
     L.insfm_gp_default_desc.argtypes = [ctypes.POINTER(Desc)]
     L.insfm_gp_default_desc.restype = None

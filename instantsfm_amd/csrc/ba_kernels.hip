@@ -1321,13 +1321,18 @@ struct insfm_ba {
     bool tlon = false;
     TlBufs tl{};
     std::vector<int> clab_host;
-    size_t chol_lds = 0, trinv_lds = 0, erow_lds = 0, pc_lds = 0;
+    size_t erow_lds = 0, pc_lds = 0;
     int pc_rows = 0;  // k_tl_pc rows per restriction pass
     // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
-    double *Ebuf[2]{}, *Dinvbuf[2]{}, *Linvbuf[2]{}, *Einvbuf[2]{};
+    double *Ebuf[2]{}, *Einvbuf[2]{};
+    double* gjW = nullptr;  // Gauss-Jordan ping-pong buffer [ldE][ldE]
+    double* gjP = nullptr;  // Gauss-Jordan pivot-block inverses [2][64][64]
     int* okbuf = nullptr;  // [2]
     hipStream_t side = nullptr;
     hipEvent_t ev_E = nullptr, ev_built = nullptr, ev_fact[2]{};
+    // the side-stream chain of a solve still to be issued (slot, next unit): issued a launch at a time from the CG's
+    // host poll loop, where the host otherwise only spins
+    int side_slot = -1, side_next = 0;
     bool built_pending = false;
     long long tl_solves = 0;
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
@@ -1606,16 +1611,11 @@ int run_tl_build(insfm_ba* h, int slot, hipStream_t stream) {
     });
 }
 
-// Two-level setup, part 2: Cholesky of E[slot], diagonal-block inverses, L^-1, E^-1 = L^-T L^-1 on `stream`.
-int run_tl_factor(insfm_ba* h, int slot, hipStream_t stream) {
-    const int m = h->tl.m;
-    const int nB = (m + kNB - 1) / kNB;
-    int* ok = h->okbuf + slot;
-    k_tl_chol<<<1, 1024, h->chol_lds, stream>>>(m, h->Ebuf[slot], ok);
-    k_tl_dinv<<<nB, 64, 0, stream>>>(m, h->Ebuf[slot], h->Dinvbuf[slot], ok);
-    k_tl_trinv<<<nB, 256, h->trinv_lds, stream>>>(m, h->Ebuf[slot], h->Dinvbuf[slot], h->Linvbuf[slot], ok);
-    k_tl_gram<<<nB * nB, 256, 0, stream>>>(m, h->Linvbuf[slot], h->Einvbuf[slot], ok);
-    return launch_err(h, "two-level factorization");
+// Two-level setup, part 2: unit u of E_slot's Gauss-Jordan inversion on `stream` (launch_gj_unit; the last writes
+// Einvbuf[slot]).
+int run_tl_gj_unit(insfm_ba* h, int slot, int u, hipStream_t stream) {
+    launch_gj_unit(u, h->tl.m, h->Ebuf[slot], h->gjW, h->gjP, h->tl.Ed, h->Einvbuf[slot], h->okbuf + slot, stream);
+    return launch_err(h, "k_gj_pinv0/k_gj_step");
 }
 
 // Per solve (after k_cg_factor / k_cg_scale on the main stream): the basis Z~ on the main stream, then E_n's build
@@ -1631,20 +1631,51 @@ int run_tl_factor(insfm_ba* h, int slot, hipStream_t stream) {
 #endif
 constexpr int kCgAhead = CG_AHEAD;  // CG iterations the host keeps queued ahead of the device (pipelined two-level PCG)
 
-int run_tl_setup(insfm_ba* h, const double* cams) {
-    const int slot = (int)(h->tl_solves & 1);
+// The side-stream chain of a solve, in issue units: 0 = wait for the basis (ev_E), E build (k_tl_erow, k_tl_ereduce),
+// ev_built; 1 .. nB + 1 = the Gauss-Jordan launches, the last followed by ev_fact[slot].  Each unit is one or two
+// kernel launches (~5-10 us of host time each), so the chain can be issued piecemeal while the host waits on the CG.
+int side_units(const insfm_ba* h) { return 2 + gj_steps(h->tl.m); }
+
+int side_issue(insfm_ba* h) {
+    if (h->side_slot < 0) return 0;
+    const int slot = h->side_slot, u = h->side_next;
     hipStream_t fs = h->tl_sync ? h->stream : h->side;
-    int rc = run_tl_basis(h, cams, h->stream);
+    int rc = 0;
+    if (u == 0) {
+        HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
+        if ((rc = run_tl_build(h, slot, fs))) return rc;
+        HIPCHK(hipEventRecord(h->ev_built, fs));
+        h->built_pending = true;
+    } else if ((rc = run_tl_gj_unit(h, slot, u - 1, fs))) {
+        return rc;
+    }
+    if (++h->side_next == side_units(h)) {
+        HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
+        h->side_slot = -1;
+    }
+    return 0;
+}
+
+int side_drain(insfm_ba* h) {
+    int rc = 0;
+    while (h->side_slot >= 0 && !(rc = side_issue(h))) {}
+    return rc;
+}
+
+// Per-solve setup on the main stream: the basis, then this solve's side chain is queued (side_slot).  Under the lag
+// rule the CG runs with the previous solve's E^-1 and the chain is issued piecemeal from the CG's poll loop (the
+// host time of issuing it does not hold back the CG); a solve that needs its own E^-1 issues it here and waits.
+int run_tl_setup(insfm_ba* h, const double* cams) {
+    int rc = side_drain(h);  // (never pending here: every solve drains its chain before it returns)
     if (rc) return rc;
+    const int slot = (int)(h->tl_solves & 1);
+    if ((rc = run_tl_basis(h, cams, h->stream))) return rc;
     HIPCHK(hipEventRecord(h->ev_E, h->stream));
-    HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
-    if ((rc = run_tl_build(h, slot, fs))) return rc;
-    HIPCHK(hipEventRecord(h->ev_built, fs));
-    h->built_pending = true;
-    if ((rc = run_tl_factor(h, slot, fs))) return rc;
-    HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
+    h->side_slot = slot;
+    h->side_next = 0;
+    if (use == slot && (rc = side_drain(h))) return rc;
     HIPCHK(hipStreamWaitEvent(h->stream, h->ev_fact[use], 0));
     h->tl.Einv = h->Einvbuf[use];
     h->tl.ok = h->okbuf + use;
@@ -1808,12 +1839,20 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                     return q == hipErrorNotReady ? 1 : -1;
                 },
                 wall_seconds,
-                [] {
+                [&] {
+                    // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax
+                    if (h->side_slot >= 0) {
+                        const int r = side_issue(h);
+                        if (r && !erc) erc = r;
+                        return;
+                    }
 #if defined(__x86_64__)
                     __builtin_ia32_pause();
 #endif
                 },
                 &erc);
+            if (!erc) erc = side_drain(h);  // whatever the CG left unissued
+            if (erc) return erc;
             enq = poll.enq;
             if (pr == CgPoll::kEnqueueError) return erc;
             if (pr == CgPoll::kStreamError) {
@@ -1857,6 +1896,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 return launch_err(h, "k_cg_iter");
             });
             if (rc) return rc;
+            if ((rc = side_drain(h))) return rc;
             rec(h, 9);
             it = stop;
             HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
@@ -2065,7 +2105,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->world_size = 1; d->rank = 0;
     d->shard_point_begin = 0; d->shard_point_end = -1;
     d->precond = 1;
-    d->cluster_size = 32;
+    d->cluster_size = 16;
 }
 
 const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() : "null handle"; }
@@ -2574,7 +2614,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         // ---- two-level preconditioner: clusters, source lists of E, buffers ----
         const int MC = D + 1;
         CovisGraph g = covis_graph(C, gcptr, gcobs, gptr, cam_idx, pt_idx);
-        int K = desc->cluster_size > 0 ? desc->cluster_size : 32;
+        int K = desc->cluster_size > 0 ? desc->cluster_size : 16;
         std::vector<int>& lab = h->clab_host;
         int nc = aggregate(g, C, K, lab);
         while (nc * MC > kCoarseMax) {
@@ -2644,7 +2684,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         tl.nc = nc;
         tl.m = m;
         tl.maxmem = maxmem;
-        const int nB = (m + kNB - 1) / kNB;
+        const int ldE = gj_steps(m) * kGB;
+        tl.ldE = ldE;
         int* ip = nullptr;
         if ((rc = upload(h, &ip, clp.data(), clp.size()))) return fail(rc, "");
         tl.cl_ptr = ip;
@@ -2680,19 +2721,27 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
         if ((rc = dd(&tl.rowR, (size_t)C * MC + 2))) return fail(rc, "");  // +2: k_tl_pc reads it in 16-B pairs
         if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
-        for (int sl = 0; sl < 2; ++sl) {
-            if ((rc = dd(&h->Ebuf[sl], (size_t)m * m))) return fail(rc, "");
-            if ((rc = dd(&h->Linvbuf[sl], (size_t)m * m))) return fail(rc, "");
-            if ((rc = dd(&h->Einvbuf[sl], (size_t)m * m))) return fail(rc, "");
-            if ((rc = dd(&h->Dinvbuf[sl], (size_t)nB * kNB * kNB))) return fail(rc, "");
+        {
+            // E is kept padded to whole blocks; the pad is the identity (k_tl_ereduce writes only the m x m part and
+            // the Gauss-Jordan steps keep the pad an identity)
+            std::vector<double> eye((size_t)ldE * ldE, 0.0);
+            for (int q = m; q < ldE; ++q) eye[(size_t)q * ldE + q] = 1.0;
+            for (int sl = 0; sl < 2; ++sl) {
+                if ((rc = upload(h, &h->Ebuf[sl], eye.data(), eye.size()))) return fail(rc, "");
+                if ((rc = dd(&h->Einvbuf[sl], (size_t)m * m))) return fail(rc, "");
+            }
+        }
+        if ((rc = dd(&h->gjW, (size_t)ldE * ldE))) return fail(rc, "");
+        if ((rc = dd(&h->gjP, (size_t)2 * kGB * kGB))) return fail(rc, "");
+        {
+            std::vector<double> ones(ldE, 1.0);   // equilibration of the pad (k_tl_ereduce writes the first m)
+            if ((rc = upload(h, &tl.Ed, ones.data(), ones.size()))) return fail(rc, "");
         }
         if ((rc = dalloc(h, (void**)&h->okbuf, sizeof(int) * 2))) return fail(rc, "");
         tl.E = h->Ebuf[0];
         tl.Einv = h->Einvbuf[0];
         tl.ok = h->okbuf;
-        hipError_t e = hipMemsetAsync(h->Linvbuf[0], 0, sizeof(double) * (size_t)m * m, h->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(h->Linvbuf[1], 0, sizeof(double) * (size_t)m * m, h->stream);
-        if (e == hipSuccess) e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
+        hipError_t e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
         // The side stream (E build + factorization, off the critical path) runs at the lowest priority, so its
         // workgroups do not take CUs from the CG iterations that overlap it.  INSFM_SIDE_PRIO overrides (experiments).
         int prio_lo = 0, prio_hi = 0;
@@ -2705,8 +2754,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
-        h->chol_lds = sizeof(double) * (size_t)m * kCPS;
-        h->trinv_lds = sizeof(double) * ((size_t)m * kPS + (size_t)kNB * (m + 1));
         const int DPd = D + (D & 1), CH = D <= 9 ? 32 : 16;
         h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
                                         (size_t)maxseg * MC * MC);
@@ -2717,8 +2764,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
         if (h->erow_lds > 160 * 1024 || h->pc_lds > 150 * 1024)
             return fail(INSFM_BA_EINVAL, "two-level preconditioner: scene too connected for the LDS budget (use precond 0)");
-        (void)hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->chol_lds);
-        (void)hipFuncSetAttribute((const void*)k_tl_trinv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->trinv_lds);
         with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             (void)hipFuncSetAttribute((const void*)k_tl_erow<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2831,6 +2876,54 @@ int insfm_ba_debug_solve(insfm_ba* h, double f) {
     return it;
 }
 
+int insfm_ba_debug_spd_inverse(int32_t m, const double* E, double* Einv, void* stream, int32_t reps,
+                               double* us_per_inverse) {
+    if (m < 1 || m > 4096 || !E || !Einv) return INSFM_BA_EINVAL;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const int nB = gj_steps(m), ld = nB * kGB;
+    const int n = reps > 0 && us_per_inverse ? reps : 1;
+    // the padded, identity-extended copy and the equilibration d = 1 / sqrt(diag E) are built on the host
+    std::vector<double> Eh((size_t)m * m), Ep((size_t)ld * ld, 0.0), dh(ld, 1.0);
+    if (hipMemcpy(Eh.data(), E, sizeof(double) * Eh.size(), hipMemcpyDeviceToHost) != hipSuccess) return INSFM_BA_EHIP;
+    for (int r = 0; r < ld; ++r)
+        for (int c = 0; c < ld; ++c)
+            Ep[(size_t)r * ld + c] = (r < m && c < m) ? Eh[(size_t)r * m + c] : (r == c ? 1.0 : 0.0);
+    for (int r = 0; r < m; ++r) dh[r] = 1.0 / std::sqrt(Eh[(size_t)r * m + r]);
+    double *Ew = nullptr, *Ww = nullptr, *dd = nullptr, *Pw = nullptr;
+    int* ok = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int okh = 0;
+    float ms = 0.f;
+    hipError_t e = hipMalloc(&Ew, sizeof(double) * (size_t)ld * ld);
+    if (e == hipSuccess) e = hipMalloc(&Ww, sizeof(double) * (size_t)ld * ld);
+    if (e == hipSuccess) e = hipMalloc(&dd, sizeof(double) * ld);
+    if (e == hipSuccess) e = hipMalloc(&Pw, sizeof(double) * 2 * kGB * kGB);
+    if (e == hipSuccess) e = hipMalloc(&ok, sizeof(int));
+    if (e == hipSuccess) e = hipMemcpy(dd, dh.data(), sizeof(double) * ld, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    for (int r = 0; r < n && e == hipSuccess; ++r) {
+        e = hipMemcpyAsync(Ew, Ep.data(), sizeof(double) * Ep.size(), hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(e0, st);
+        for (int u = 0; u <= nB && e == hipSuccess; ++u) {
+            launch_gj_unit(u, m, Ew, Ww, Pw, dd, Einv, ok, st);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(e1, st);
+        if (e == hipSuccess) e = hipEventSynchronize(e1);
+        float t = 0.f;
+        if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+        ms += t;
+    }
+    if (e == hipSuccess) e = hipMemcpy(&okh, ok, sizeof(int), hipMemcpyDeviceToHost);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(Ew); (void)hipFree(Ww); (void)hipFree(dd); (void)hipFree(Pw); (void)hipFree(ok);
+    if (e != hipSuccess) return INSFM_BA_EHIP;
+    if (us_per_inverse) *us_per_inverse = 1e3 * ms / n;
+    return okh ? 1 : 0;
+}
+
 int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch) {
     if (!h || reps <= 0 || !us_per_launch || !h->d.optimize_poses) return INSFM_BA_EINVAL;
     // re-run one kernel `reps` times back to back on the data of the last solve; the CG state it overwrites is
@@ -2851,7 +2944,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 4) {
                 int rc2 = run_tl_basis(h, h->cams_cur, h->stream);
                 if (!rc2) rc2 = run_tl_build(h, 0, h->stream);
-                if (!rc2) rc2 = run_tl_factor(h, 0, h->stream);
+                for (int u = 0; u <= gj_steps(h->tl.m) && !rc2; ++u) rc2 = run_tl_gj_unit(h, 0, u, h->stream);
                 if (rc2) return rc2;
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
@@ -2910,10 +3003,8 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 13: src = h->Einvbuf[1]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 14: src = h->tl.gd; n = h->tlon ? 2 * C : 0; break;
         case 15: src = h->cg.r[0]; n = C * D; break;
-        // 16/17 factor (E slot 0/1, lower = L), 18/19 Dinv slot 0/1 [nB*32*32], 20/21 L^-1 slot 0/1
-        case 16: case 17: src = h->Ebuf[which - 16]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
-        case 18: case 19: src = h->Dinvbuf[which - 18]; n = h->tlon ? (size_t)((h->tl.m + kNB - 1) / kNB) * kNB * kNB : 0; break;
-        case 20: case 21: src = h->Linvbuf[which - 20]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
+        // 16/17 E slot 0/1 padded to whole blocks [ldE][ldE] (E^-1 once the slot's inversion has run)
+        case 16: case 17: src = h->Ebuf[which - 16]; n = h->tlon ? (size_t)h->tl.ldE * h->tl.ldE : 0; break;
         default: return INSFM_BA_EINVAL;
     }
     if (h->side) HIPCHK(hipStreamSynchronize(h->side));

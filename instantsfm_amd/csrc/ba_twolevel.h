@@ -11,23 +11,24 @@
 //   k_tl_basis   : Z~ per (camera, coarse column)
 //   k_tl_erow    : per camera row and neighbour cluster, sum of Z~_i^T S~_ij Z~_j (+ Z~_i^T Z~_i), LDS-staged
 //   k_tl_ereduce : E[(c',k),(c,l)] = fixed-order sum of the row segments of cluster pair (c', c)
-//   k_tl_chol    : one workgroup, blocked right-looking Cholesky of E (diag block in registers, panel in LDS)
-//   k_tl_dinv    : inverses of the factor's diagonal blocks
-//   k_tl_trinv   : L^-1 by column blocks (block forward substitution, diag-block inverses as GEMMs)
-//   k_tl_gram    : E^-1 = L^-T L^-1 (dense tiles)
+//   k_gj_step    : E^-1 by blocked Gauss-Jordan inversion, one launch per 64-wide block step (f64 MFMA)
 // Per CG iteration (pipelined PCG, same stopping rule as block-Jacobi; see the section below):
 //   k_tl_pc      : per cluster: recurrence scalars from the row partials, restriction, y = E^-1 R (its MC rows),
 //                  m_i = w_i + Z~_i y_c
 //   k_tl_pspmv   : n = S~ m (row-contiguous Sn stream), the row's vector updates, its partials for the next iteration
 #pragma once
+#include <algorithm>
+
 #include "ba_common.h"
+
+#ifndef COARSE_MAX_DIM
+#define COARSE_MAX_DIM 768
+#endif
 #include "ba_device.h"
 
 namespace insfm {
 
-constexpr int kCoarseMax = 288;  // nclust * (D + 1) cap: L^-1's column block + an L strip (2 x 288 x 33 f64) fit LDS
-constexpr int kNB = 32;          // block size of the dense coarse factorization
-constexpr int kPS = kNB + 1;     // padded LDS row stride (odd: conflict-free column walks)
+constexpr int kCoarseMax = COARSE_MAX_DIM;  // nclust * (D + 1) cap (k_tl_pc keeps a cluster's E^-1 rows in registers)
 
 struct TlBufs {
     double* u;           // [C*D]  preconditioned residual
@@ -38,10 +39,9 @@ struct TlBufs {
     double* gd;          // [3C]  row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2  (k_tl_pspmv)
     double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
     double* Oseg;        // [nseg][MC][MC] per (row, neighbour cluster) sums of Z~_i^T S~_ij Z~_j
-    double* E;           // [m][m] coarse matrix, Cholesky factor (lower) in place
-    double* Dinv;        // [nB][kNB][kNB] inverses of the diagonal blocks of the factor
-    double* Linv;        // [m][m] (lower)
-    double* Einv;        // [m][m]
+    double* E;           // [ldE][ldE] coarse matrix padded to whole kGB blocks (pad: identity), inverted in place
+    double* Einv;        // [m][m] compact E^-1 (k_tl_pc reads its cluster's rows)
+    double* Ed;          // [ldE] 1 / sqrt(E_kk) (pad: 1): E is inverted as diag(Ed) E diag(Ed) (symmetric equilibration)
     int* ok;             // coarse correction usable (E positive definite)
     const int* cl_ptr;   // [nc+1]
     const int* cl_cams;  // cluster members, ascending camera id
@@ -52,7 +52,7 @@ struct TlBufs {
     const int* rseg_ptr; // [C+1] segments of each row
     const int* ered_ptr; // [nc*nc+1]
     const int* ered_seg; // segment ids of each cluster pair, rows ascending
-    int nc, m, maxmem;
+    int nc, m, maxmem, ldE;
 };
 
 // ---- setup ---------------------------------------------------------------------------------------------------
@@ -227,7 +227,8 @@ __global__ __launch_bounds__(kThreads) void k_tl_ereduce(TlBufs tl) {
     }
     for (; e < s1; ++e) acc += O[(size_t)tl.ered_seg[e] * MM];
     if (r == q && acc == 0.0) acc = 1.0;
-    tl.E[g] = acc;
+    tl.E[(size_t)r * tl.ldE + q] = acc;
+    if (r == q) tl.Ed[r] = 1.0 / sqrt(acc);  // equilibration (k_gj_equil); NaN for a non-positive diagonal
 }
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -236,249 +237,163 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __hiloint2double(hi, lo);
 }
 
-constexpr int kCB = 16;          // block size of the Cholesky factorization
-constexpr int kCPS = kCB + 1;    // LDS row stride of the Cholesky panel
+// ---- E^-1 by blocked Gauss-Jordan inversion (multi-workgroup, f64 MFMA) -------------------------------------------
+// E (m x m, SPD) is held padded to ld = nB * kGB (pad: identity), symmetrically equilibrated on the fly
+// (d = 1 / sqrt(diag E), from k_tl_ereduce; the pad's d is 1) and inverted by block Gauss-Jordan steps k = 0..nB-1
+// with pivot block P = X_kk (no pivoting: every pivot block of an SPD matrix is SPD):
+//   Y_kk = P^-1,  Y_kj = P^-1 X_kj,  Y_ik = -X_ik P^-1,  Y_ij = X_ij - X_ik (P^-1 X_kj)      (i, j != k)
+// One launch per step (k_gj_step: nB x nB workgroups, one 32 x 32 tile each, v_mfma_f64_16x16x4f64), ping-ponging
+// between two buffers so that no workgroup reads a tile another one writes in the same launch.  P^-1 is looked
+// ahead: the workgroup that forms the next pivot block Y_{k+1,k+1} inverts it right away (k_gj_pinv0 does P_0) by
+// scalar in-place Gauss-Jordan in one wave's registers (lane r = row r, pivot rows broadcast by readlane), so the
+// other workgroups only load it.  The last step writes diag(d) Y diag(d) compactly (row stride m) for k_tl_pc.
+// 2 m^3 flops in nB + 1 launches; the oracle (ba_oracle.c gj_inverse) runs the same steps, pivots and fused
+// multiply-adds.
+constexpr int kGB = 32;        // block size
+constexpr int kGS = kGB + 1;   // LDS row stride (odd: the A-fragment column reads are conflict-free)
+typedef double gj_acc_t __attribute__((ext_vector_type(4)));
 
-// One 1024-thread workgroup: blocked right-looking Cholesky of E (m <= kCoarseMax) in place (lower triangle).
-// Per block column of kCB:
-//   diagonal block : wave 0, lane r holds row r in registers; each pivot column goes through LDS once and is read
-//                    back as one batch of independent loads;
-//   panel          : one thread per row below, column-oriented forward substitution against the block (LDS);
-//   trailing SYRK  : 4x4 register tiles with rows/columns strided by ceil(n/4) (the 64 lanes of a wave read 64
-//                    consecutive panel rows: conflict-free LDS; update consecutive columns: coalesced RMW); only the
-//                    entries of the lower triangle are computed.
-// ok[0] = 0 when a pivot is not positive (the solve then runs without the coarse correction).  `prof` (debug only)
-// receives clock64() stamps per block column and phase.
-__global__ __launch_bounds__(1024) void k_tl_chol(int m, double* __restrict__ A, int* __restrict__ ok,
-                                                  long long* __restrict__ prof = nullptr) {
-    extern __shared__ double lds[];
-    double* Pn = lds;  // [m][kCPS]; rows [kb, kb+nb) double as the diagonal block of the current step
-    __shared__ double colb[2][64];
-    __shared__ int bad;
-    const int t = threadIdx.x;
-    if (t == 0) bad = 0;
-    if (prof && t == 0) prof[63] = clock64();
-    __syncthreads();
-    int step = 0;
-    for (int kb = 0; kb < m; kb += kCB, ++step) {
-        const int nb = min(kCB, m - kb);
-        double* Dg = Pn + (size_t)kb * kCPS;
-        if (t < 64) {
-            const int r = t;
-            double a[kCB];
+// acc += sgn * As[R .. R+15][:] * Bs[:][Cc .. Cc+15] over K = 32 for wave w's subtile (R, Cc) = (16 (w >> 1),
+// 16 (w & 1)) (v_mfma_f64_16x16x4f64: A fragment lane l = A[row l & 15][k l >> 4], B fragment = B[k l >> 4]
+// [col l & 15], result reg q = D[row (l >> 4) + 4 q][col l & 15]; cdna_hip_programming.md, f64 MFMA layout).
+__device__ __forceinline__ gj_acc_t gj_tile_mfma(const double (*As)[kGS], const double (*Bs)[kGS], gj_acc_t acc, double sgn,
+                                                 int lane, int w) {
+    const int R = (w >> 1) * 16, Cc = (w & 1) * 16, lr = lane & 15, lk = lane >> 4;
 #pragma unroll
-            for (int c = 0; c < kCB; ++c) a[c] = (r < nb && c <= r && c < nb) ? A[(size_t)(kb + r) * m + kb + c] : 0.0;
-            int isbad = 0;
-#pragma unroll
-            for (int j = 0; j < kCB; ++j) {
-                if (j < nb) {
-                    colb[j & 1][r] = a[j];
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    double d = colb[j & 1][j];
-                    if (!(d > 0.0)) { isbad = 1; d = 1.0; }
-                    const double inv = 1.0 / sqrt(d);
-                    // column j of L: lanes >= j (lane j: sqrt(d))
-                    double lc[kCB];
-#pragma unroll
-                    for (int c = 0; c < kCB; ++c) lc[c] = colb[j & 1][c] * inv;
-                    const double l = (r > j) ? a[j] * inv : (r == j ? d * inv : 0.0);
-                    a[j] = (r >= j) ? l : 0.0;
-#pragma unroll
-                    for (int c = j + 1; c < kCB; ++c) a[c] -= l * lc[c];
-                }
-            }
-            if (r == 0 && isbad) bad = 1;
-            if (r < nb) {
-#pragma unroll
-                for (int c = 0; c < kCB; ++c) {
-                    if (c < nb) {
-                        const double v = (c <= r) ? a[c] : 0.0;
-                        Dg[r * kCPS + c] = v;
-                        if (c <= r) A[(size_t)(kb + r) * m + kb + c] = v;
-                    }
-                }
-                Dg[r * kCPS + kCB] = 1.0 / a[r];   // reciprocal pivot in the pad column
-            }
-        }
-        __syncthreads();
-        if (prof && t == 0 && step < 20) prof[3 * step] = clock64();
-        // panel: row i solves x L_kk^T = a, column by column
-        const int i = kb + nb + t;
-        if (i < m) {
-            double x[kCB];
-#pragma unroll
-            for (int c = 0; c < kCB; ++c) x[c] = (c < nb) ? A[(size_t)i * m + kb + c] : 0.0;
-#pragma unroll
-            for (int q = 0; q < kCB; ++q) {
-                if (q < nb) {
-                    double lq[kCB];
-#pragma unroll
-                    for (int c = q + 1; c < kCB; ++c) lq[c] = Dg[c * kCPS + q];
-                    x[q] *= Dg[q * kCPS + kCB];
-#pragma unroll
-                    for (int c = q + 1; c < kCB; ++c) x[c] -= x[q] * lq[c];
-                }
-            }
-#pragma unroll
-            for (int c = 0; c < kCB; ++c)
-                if (c < nb) {
-                    A[(size_t)i * m + kb + c] = x[c];
-                    Pn[(size_t)i * kCPS + c] = x[c];
-                }
-        }
-        __syncthreads();
-        if (prof && t == 0 && step < 20) prof[3 * step + 1] = clock64();
-        // trailing update: strided 4x4 tiles, entries (u, v) with v <= u (the others are above the diagonal)
-        const int base = kb + nb, n = m - base;
-        if (n > 0) {
-            const int nt = (n + 3) / 4;
-            for (int tt = t; tt < nt * nt; tt += 1024) {
-                const int I = tt / nt, J = tt - (tt / nt) * nt;
-                int rr[4], cc[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) { rr[u] = base + I + nt * u; cc[u] = base + J + nt * u; }
-                double acc[10];
-#pragma unroll
-                for (int e = 0; e < 10; ++e) acc[e] = 0.0;
-                for (int k = 0; k < nb; ++k) {
-                    double av[4], bq[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) av[u] = (rr[u] < m) ? Pn[(size_t)rr[u] * kCPS + k] : 0.0;
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) bq[v] = (cc[v] < m) ? Pn[(size_t)cc[v] * kCPS + k] : 0.0;
-                    int e = 0;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int v = 0; v <= u; ++v) acc[e++] += av[u] * bq[v];
-                }
-                int e = 0;
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int v = 0; v <= u; ++v, ++e)
-                        if (rr[u] < m && cc[v] <= rr[u]) A[(size_t)rr[u] * m + cc[v]] -= acc[e];
-            }
-        }
-        __threadfence_block();
-        __syncthreads();
-        if (prof && t == 0 && step < 20) prof[3 * step + 2] = clock64();
-    }
-    if (t == 0) ok[0] = !bad;
+    for (int s = 0; s < kGB / 4; ++s)
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(sgn * As[R + lr][4 * s + lk], Bs[4 * s + lk][Cc + lr], acc, 0, 0, 0);
+    return acc;
 }
 
-// One wave per diagonal block R of the factor: Dinv_R = L_RR^-1, lane c owns column c (forward substitution).
-__global__ __launch_bounds__(64) void k_tl_dinv(int m, const double* __restrict__ Lc, double* __restrict__ Dinv,
-                                                const int* __restrict__ ok) {
-    __shared__ double Lb[kNB][kPS];
-    if (!ok[0]) return;
-    const int R = blockIdx.x, c = threadIdx.x;
-    const int r0 = R * kNB, nb = min(kNB, m - r0);
-    for (int e = c; e < kNB * kNB; e += 64) {
-        const int rr = e / kNB, q = e % kNB;
-        Lb[rr][q] = (rr < nb && q <= rr) ? Lc[(size_t)(r0 + rr) * m + r0 + q] : (rr == q ? 1.0 : 0.0);
+// tile (r0, c0) of X (row stride ld) -> LDS, optionally equilibrated ((x d_r) d_c, the oracle's order)
+__device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __restrict__ X, int ld, size_t r0, size_t c0,
+                                         const double* __restrict__ d) {
+    for (int e = threadIdx.x; e < kGB * kGB; e += 256) {
+        const int r = e / kGB, c = e % kGB;
+        double v = X[(r0 + r) * ld + c0 + c];
+        if (d) v = v * d[r0 + r] * d[c0 + c];
+        dst[r][c] = v;
+    }
+}
+
+// In-place scalar Gauss-Jordan inversion of the SPD block in M (LDS) by wave 0 (lane r & 31 = row r; the pivot row is
+// broadcast by readlane), result back into M; every thread of the workgroup must call it.  Returns (in wave 0)
+// whether a pivot was not positive.
+__device__ bool gj_invert_block(double (*M)[kGS]) {
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x, r = lane & 31;
+        double a[kGB];
+#pragma unroll
+        for (int c = 0; c < kGB; ++c) a[c] = M[r][c];
+#pragma unroll
+        for (int p = 0; p < kGB; ++p) {
+            double piv = readlane_d(a[p], p);
+            if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+            const double inv = 1.0 / piv;
+            const double aip = a[p];
+#pragma unroll
+            for (int c = 0; c < kGB; ++c) {
+                if (c == p) continue;
+                const double rpc = readlane_d(a[c], p) * inv;
+                a[c] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[c]);
+            }
+            a[p] = (r == p) ? inv : -aip * inv;
+        }
+        if (lane < kGB) {
+#pragma unroll
+            for (int c = 0; c < kGB; ++c) M[lane][c] = a[c];
+        }
     }
     __syncthreads();
-    if (c >= kNB) return;
-    double x[kNB];
-#pragma unroll
-    for (int rr = 0; rr < kNB; ++rr) {
-        double s = (rr == c) ? 1.0 : 0.0;
-#pragma unroll
-        for (int q = 0; q < rr; ++q) s -= Lb[rr][q] * x[q];
-        x[rr] = (rr >= c) ? s / Lb[rr][rr] : 0.0;
-    }
-    double* Dv = Dinv + (size_t)R * kNB * kNB;
-#pragma unroll
-    for (int rr = 0; rr < kNB; ++rr) Dv[rr * kNB + c] = x[rr];
+    return bad;
 }
 
-// Workgroup J computes columns [J*kNB, J*kNB + kNB) of L^-1 by block forward substitution:
-//   X_R = Dinv_R (I_RJ - sum_{J<=K<R} L_RK X_K), the column block kept in LDS.  The strip L_R[J*kNB, R*kNB) is staged
-//   through LDS with coalesced loads; 256 threads, thread (q, c) owns rows q, q+8, q+16, q+24 of column c, so every LDS
-//   load of X feeds four FMAs (the strip loads are broadcasts).  Rows past the end of the matrix are never touched.
-__global__ __launch_bounds__(256) void k_tl_trinv(int m, const double* __restrict__ Lc, const double* __restrict__ Dinv,
-                                                  double* __restrict__ Linv, const int* __restrict__ ok) {
-    extern __shared__ double lds[];
-    double* X = lds;                          // [m][kPS]
-    double* St = lds + (size_t)m * kPS;       // [kNB][m + 1] strip of L (row stride m + 1)
-    __shared__ double Tb[kNB][kPS];
-    if (!ok[0]) return;
-    const int J = blockIdx.x;
-    const int t = threadIdx.x, q0 = t / kNB, c = t % kNB;   // q0 in [0, 8)
-    const int j0 = J * kNB;
-    const int nB = (m + kNB - 1) / kNB;
-    const int ls = m + 1;
-    for (int R = J; R < nB; ++R) {
-        const int r0 = R * kNB, nr = min(kNB, m - r0);
-        const int w = r0 - j0;                // strip width
-        for (int e = t; e < nr * w; e += 256) {
-            const int q = e / w, k = e - q * w;
-            St[q * ls + k] = Lc[(size_t)(r0 + q) * m + j0 + k];
-        }
-        __syncthreads();
-        double v[4];
+// P_0^-1 (one workgroup): the equilibrated first pivot block.
+__global__ __launch_bounds__(256) void k_gj_pinv0(int ld, const double* __restrict__ X, const double* __restrict__ d,
+                                                  double* __restrict__ Pout, int* __restrict__ ok) {
+    __shared__ double M[kGB][kGS];
+    gj_stage(M, X, ld, 0, 0, d);
+    const bool bad = gj_invert_block(M);
+    for (int e = threadIdx.x; e < kGB * kGB; e += 256) Pout[e] = M[e / kGB][e % kGB];
+    if (threadIdx.x == 0) ok[0] = !bad;
+}
+
+__global__ __launch_bounds__(256) void k_gj_step(int k, int nB, int ld, int m, const double* __restrict__ X,
+                                                 double* __restrict__ Y, const double* __restrict__ d, int first,
+                                                 const double* __restrict__ Pin, double* __restrict__ Pnext,
+                                                 double* __restrict__ Eout, int* __restrict__ ok) {
+    __shared__ double Ps[kGB][kGS];   // P^-1
+    __shared__ double Bk[kGB][kGS];   // X_kj, then P^-1 X_kj
+    __shared__ double Ci[kGB][kGS];   // X_ik
+    const int i = blockIdx.x / nB, j = blockIdx.x % nB, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const size_t k0 = (size_t)k * kGB, i0 = (size_t)i * kGB, j0 = (size_t)j * kGB;
+    const int R = (w >> 1) * 16, Cc = (w & 1) * 16;
+    const double* ds = first ? d : nullptr;   // equilibrate while reading E (step 0)
+    for (int e = t; e < kGB * kGB; e += 256) Ps[e / kGB][e % kGB] = Pin[e];
+    if (j != k) gj_stage(Bk, X, ld, k0, j0, ds);
+    if (i != k) gj_stage(Ci, X, ld, i0, k0, ds);
+    __syncthreads();
+    gj_acc_t acc = {0.0, 0.0, 0.0, 0.0};
+    if (i == k && j == k) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int rr = q0 + 8 * u;
-            double a = (R == J && rr == c) ? 1.0 : 0.0;
-            if (rr < nr) {
-                const double* Sr = St + rr * ls;
-                for (int k = 0; k < w; ++k) a -= Sr[k] * X[(size_t)(j0 + k) * kPS + c];
-            }
-            v[u] = a;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) Tb[q0 + 8 * u][c] = v[u];
+        for (int q = 0; q < 4; ++q) acc[q] = Ps[R + (lane >> 4) + 4 * q][Cc + (lane & 15)];
+    } else if (i == k) {
+        acc = gj_tile_mfma(Ps, Bk, acc, 1.0, lane, w);                // Y_kj = P^-1 X_kj
+    } else if (j == k) {
+        acc = gj_tile_mfma(Ci, Ps, acc, -1.0, lane, w);               // Y_ik = -X_ik P^-1
+    } else {
+        acc = gj_tile_mfma(Ps, Bk, acc, 1.0, lane, w);                // P^-1 X_kj ...
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int rr = q0 + 8 * u;
-            if (rr < nr) {
-                const double* Dv = Dinv + (size_t)R * kNB * kNB + rr * kNB;
-                double x = 0.0;
-                for (int q = 0; q <= rr; ++q) x += Dv[q] * Tb[q][c];
-                X[(size_t)(r0 + rr) * kPS + c] = x;
-                if (j0 + c < m) Linv[(size_t)(r0 + rr) * m + j0 + c] = x;
-            }
-        }
+        for (int q = 0; q < 4; ++q) Bk[R + (lane >> 4) + 4 * q][Cc + (lane & 15)] = acc[q];
         __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const size_t r = i0 + R + (lane >> 4) + 4 * q, cc = j0 + Cc + (lane & 15);
+            double v = X[r * ld + cc];
+            if (ds) v = v * ds[r] * ds[cc];
+            acc[q] = v;
+        }
+        acc = gj_tile_mfma(Ci, Bk, acc, -1.0, lane, w);               // ... Y_ij = X_ij - X_ik (P^-1 X_kj)
+    }
+    const bool last = k == nB - 1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const size_t r = i0 + R + (lane >> 4) + 4 * q, cc = j0 + Cc + (lane & 15);
+        Y[r * ld + cc] = acc[q];
+        if (last && r < (size_t)m && cc < (size_t)m) Eout[r * m + cc] = acc[q] * d[r] * d[cc];
+    }
+    if (i == k + 1 && j == k + 1) {
+        // look-ahead: this tile is the next step's pivot block; invert it now
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ps[R + (lane >> 4) + 4 * q][Cc + (lane & 15)] = acc[q];
+        const bool bad = gj_invert_block(Ps);
+        for (int e = t; e < kGB * kGB; e += 256) Pnext[e] = Ps[e / kGB][e % kGB];
+        if (t == 0 && bad) ok[0] = 0;
     }
 }
 
-// E^-1 = L^-T L^-1 : one 32x32 tile per 256-thread workgroup (4 outputs per thread), rows of L^-1 staged through LDS.
-__global__ __launch_bounds__(256) void k_tl_gram(int m, const double* __restrict__ Linv, double* __restrict__ Einv,
-                                                 const int* __restrict__ ok) {
-    __shared__ double A[kNB][kPS];
-    __shared__ double B[kNB][kPS];
-    if (!ok[0]) return;
-    const int nB = (m + kNB - 1) / kNB;
-    const int tk = blockIdx.x / nB, tlb = blockIdx.x % nB;
-    const int t = threadIdx.x, k0q = t / kNB, ll = t % kNB;
-    const int k0 = tk * kNB, l0 = tlb * kNB;
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int r0 = max(k0, l0); r0 < m; r0 += kNB) {
-        for (int e = t; e < kNB * kNB; e += 256) {
-            const int rr = e / kNB, cc = e % kNB, r = r0 + rr;
-            A[rr][cc] = (r < m && k0 + cc < m) ? Linv[(size_t)r * m + k0 + cc] : 0.0;
-            B[rr][cc] = (r < m && l0 + cc < m) ? Linv[(size_t)r * m + l0 + cc] : 0.0;
-        }
-        __syncthreads();
-#pragma unroll 8
-        for (int q = 0; q < kNB; ++q) {
-            const double bq = B[q][ll];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) acc[u] += A[q][k0q + 8 * u] * bq;
-        }
-        __syncthreads();
+inline int gj_steps(int m) { return (m + kGB - 1) / kGB; }
+
+// Launch unit u of the inversion of E (padded [ld][ld], equilibration d [ld], pad entries 1), u = 0 .. gj_steps(m):
+// 0 = P_0^-1, u >= 1 = step u - 1.  E and W are the ping-pong buffers, P [2][kGB][kGB] the pivot inverses; the last
+// step writes the compact E^-1 into Eout [m][m]; ok[0] = 0 when E is not positive definite.  Units run in order on
+// one stream.
+inline void launch_gj_unit(int u, int m, double* E, double* W, double* P, const double* d, double* Eout, int* ok,
+                           hipStream_t st) {
+    const int nB = gj_steps(m), ld = nB * kGB;
+    if (u == 0) {
+        k_gj_pinv0<<<1, 256, 0, st>>>(ld, E, d, P, ok);
+        return;
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int kk = k0q + 8 * u;
-        if (k0 + kk < m && l0 + ll < m) Einv[(size_t)(k0 + kk) * m + l0 + ll] = acc[u];
-    }
+    const int k = u - 1;
+    const double* X = (k & 1) ? W : E;
+    double* Y = (k & 1) ? E : W;
+    k_gj_step<<<nB * nB, 256, 0, st>>>(k, nB, ld, m, X, Y, d, k == 0, P + (size_t)(k & 1) * kGB * kGB,
+                                       P + (size_t)((k + 1) & 1) * kGB * kGB, Eout, ok);
 }
 
 // ---- per iteration: pipelined PCG (oracle/ba_oracle.c ora_pcg, two-level path) -----------------------------------

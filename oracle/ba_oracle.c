@@ -343,9 +343,10 @@ static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *
  * K/2 are then dissolved: each member joins the aggregate of size >= K/2 it is most connected to (ties: smallest
  * aggregate id).  Labels are renumbered in order of first appearance by camera id. */
 static int ora_aggregate(ora_t* h, int K);
-/* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU factorizes E in one workgroup's LDS):
- * while the aggregation yields more clusters, it is redone with twice the target size. */
-#define COARSE_MAX 288
+/* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU's k_tl_pc keeps a cluster's rows of E^-1
+ * in registers; csrc/ba_twolevel.h COARSE_MAX_DIM): while the aggregation yields more clusters, it is redone with
+ * twice the target size. */
+#define COARSE_MAX 768
 static void ora_cluster_cameras(ora_t* h) {
     int K = h->cluster_size;
     while (ora_aggregate(h, K) * (h->D + 1) > COARSE_MAX) K *= 2;
@@ -504,7 +505,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     h->down0 = dopt[5]; h->factor = dopt[6]; h->high = dopt[7]; h->low = dopt[8]; h->cmin = dopt[9];
     h->cmax = dopt[10]; h->pcg_tol = dopt[11];
     h->max_rejects = iopt[0]; h->pcg_max_iter = iopt[1]; h->optimize_poses = iopt[2];
-    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 32;
+    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 16;
 #ifdef _OPENMP
     if (iopt[3] > 0) omp_set_num_threads(iopt[3]);
 #endif
@@ -841,13 +842,86 @@ static void tri_inv(int n, const double* L, double* Li) {
     }
 }
 
+/* E^-1 in place by blocked Gauss-Jordan inversion, 32-wide blocks (the last one partial), the GPU's algorithm
+ * (csrc/ba_twolevel.h k_gj_pinv0 / k_gj_step) with its fused multiply-adds -- the pivot update a - aip * rpc as
+ * fma(-aip, rpc, a), every tile product as one fma chain in k order (v_mfma_f64_16x16x4f64 accumulates like that) --
+ * so the two round alike: per block step k with pivot block P = A_kk
+ *   P^-1 by scalar in-place Gauss-Jordan (pivots in order), A_kj <- P^-1 A_kj, A_ij <- A_ij - A_ik A_kj (new A_kj),
+ *   A_ik <- -A_ik P^-1, A_kk <- P^-1.
+ * Same pivot order and blocking as the GPU, so the two round alike (an ill-conditioned E amplifies the rounding of
+ * a different inversion algorithm far beyond the PCG parity tolerance).  Returns -1 if a pivot is not positive. */
+#define GJB 32
+static int gj_inverse(int m, double* A) {
+    double* P = (double*)malloc(sizeof(double) * GJB * GJB);
+    double* Cc = (double*)malloc(sizeof(double) * (size_t)m * GJB);
+    int bad = 0;
+    for (int k0 = 0; k0 < m; k0 += GJB) {
+        const int nk = (m - k0) < GJB ? (m - k0) : GJB;
+        for (int r = 0; r < nk; ++r)
+            for (int c = 0; c < nk; ++c) P[r * GJB + c] = A[(size_t)(k0 + r) * m + k0 + c];
+        for (int p = 0; p < nk; ++p) {
+            double piv = P[p * GJB + p];
+            if (!(piv > 0.0)) { bad = 1; piv = 1.0; }
+            const double inv = 1.0 / piv;
+            double rp[GJB];
+            for (int c = 0; c < nk; ++c) rp[c] = P[p * GJB + c] * inv;
+            for (int r = 0; r < nk; ++r) {
+                if (r == p) continue;
+                const double aip = P[r * GJB + p];
+                for (int c = 0; c < nk; ++c)
+                    if (c != p) P[r * GJB + c] = fma(-aip, rp[c], P[r * GJB + c]);
+                P[r * GJB + p] = -aip * inv;
+            }
+            for (int c = 0; c < nk; ++c)
+                if (c != p) P[p * GJB + c] = rp[c];
+            P[p * GJB + p] = inv;
+        }
+        /* old column tiles */
+        for (int i = 0; i < m; ++i)
+            for (int c = 0; c < nk; ++c) Cc[(size_t)i * GJB + c] = A[(size_t)i * m + k0 + c];
+        /* row k: A_kj <- P^-1 A_kj */
+        #pragma omp parallel for schedule(static)
+        for (int j = 0; j < m; ++j) {
+            if (j >= k0 && j < k0 + nk) continue;
+            double col[GJB];
+            for (int q = 0; q < nk; ++q) col[q] = A[(size_t)(k0 + q) * m + j];
+            for (int r = 0; r < nk; ++r) {
+                double s = 0.0;
+                for (int q = 0; q < nk; ++q) s = fma(P[r * GJB + q], col[q], s);
+                A[(size_t)(k0 + r) * m + j] = s;
+            }
+        }
+        /* rows i outside block k */
+        #pragma omp parallel for schedule(static)
+        for (int i = 0; i < m; ++i) {
+            if (i >= k0 && i < k0 + nk) continue;
+            const double* ci = Cc + (size_t)i * GJB;
+            double* Ai = A + (size_t)i * m;
+            for (int j = 0; j < m; ++j) {
+                if (j >= k0 && j < k0 + nk) continue;
+                double s = Ai[j];
+                for (int q = 0; q < nk; ++q) s = fma(-ci[q], A[(size_t)(k0 + q) * m + j], s);
+                Ai[j] = s;
+            }
+            for (int c = 0; c < nk; ++c) {
+                double s = 0.0;
+                for (int q = 0; q < nk; ++q) s = fma(-ci[q], P[q * GJB + c], s);
+                Ai[k0 + c] = s;
+            }
+        }
+        for (int r = 0; r < nk; ++r)
+            for (int c = 0; c < nk; ++c) A[(size_t)(k0 + r) * m + k0 + c] = P[r * GJB + c];
+    }
+    free(P); free(Cc);
+    return bad ? -1 : 0;
+}
 
 /* Coarse operator of the two-level preconditioner (scaled space).  Z~_i = L_i^T G_i (D x MC) with G_i the coarse
  * basis of camera i at the linearization point; E = Z~^T S~ Z~ (m x m, m = nclust * MC), accumulated per camera row
  * in increasing row order: diagonal term Z~_i^T Z~_i, then for every upper block (i,j>i) Z~_i^T S~_ij Z~_j into
  * (c_i,c_j) and its transpose into (c_j,c_i).  A zero diagonal entry (unused column of a single-camera cluster)
- * becomes 1.  E^-1 is formed explicitly from its Cholesky factor.  Returns 0 when E is not positive definite (the
- * solve then runs with plain block-Jacobi). */
+ * becomes 1.  E^-1 is formed explicitly by blocked Gauss-Jordan inversion (gj_inverse) of the symmetrically
+ * equilibrated E.  Returns 0 when E is not positive definite (the solve then runs with plain block-Jacobi). */
 static int ora_coarse_setup(ora_t* h, const double* Lfac, double* Zt, double* Einv) {
     const int D = h->D, C = h->C, MC = D + 1, nc = h->nclust, m = nc * MC;
     const size_t DD = (size_t)D * D;
@@ -895,20 +969,33 @@ static int ora_coarse_setup(ora_t* h, const double* Lfac, double* Zt, double* Ei
     }
     for (int k = 0; k < m; ++k)
         if (E[(size_t)k * m + k] == 0.0) E[(size_t)k * m + k] = 1.0;
-    double* Lc = (double*)malloc(sizeof(double) * (size_t)m * m);
-    int ok = chol(m, E, Lc) == 0;
-    if (ok) {
-        double* Li = E;                             /* reuse: L^-1 */
-        tri_inv(m, Lc, Li);
-        /* Einv = L^-T L^-1 : Einv_kl = sum_{r >= max(k,l)} Li_rk Li_rl */
-        for (int k = 0; k < m; ++k)
-            for (int l = 0; l < m; ++l) {
-                double s = 0;
-                for (int r = k > l ? k : l; r < m; ++r) s += Li[(size_t)r * m + k] * Li[(size_t)r * m + l];
-                Einv[(size_t)k * m + l] = s;
-            }
-    }
-    free(Lc); free(E);
+    /* symmetric equilibration d = 1 / sqrt(diag E) (the GPU's k_gj_equil; NaN for a non-positive diagonal, which
+     * fails the first pivot test), then E^-1 = diag(d) (diag(d) E diag(d))^-1 diag(d) */
+    double* dq = (double*)malloc(sizeof(double) * (size_t)m);
+    for (int k = 0; k < m; ++k) dq[k] = 1.0 / sqrt(E[(size_t)k * m + k]);
+    for (int r = 0; r < m; ++r)
+        for (int q = 0; q < m; ++q) E[(size_t)r * m + q] = E[(size_t)r * m + q] * dq[r] * dq[q];
+    int ok = gj_inverse(m, E) == 0;
+    if (ok)
+        for (int r = 0; r < m; ++r)
+            for (int q = 0; q < m; ++q) Einv[(size_t)r * m + q] = E[(size_t)r * m + q] * dq[r] * dq[q];
+    free(dq);
+    free(E);
+    return ok;
+}
+
+/* The coarse inverse exactly as ora_coarse_setup forms it (equilibration, gj_inverse, scaling back), exported for
+ * the GPU kernels' bitwise test.  Returns 1 when E is positive definite, 0 when not. */
+int ora_spd_inverse(int m, const double* E, double* Einv) {
+    double* A = (double*)malloc(sizeof(double) * (size_t)m * m);
+    double* dq = (double*)malloc(sizeof(double) * (size_t)m);
+    for (int k = 0; k < m; ++k) dq[k] = 1.0 / sqrt(E[(size_t)k * m + k]);
+    for (int r = 0; r < m; ++r)
+        for (int q = 0; q < m; ++q) A[(size_t)r * m + q] = E[(size_t)r * m + q] * dq[r] * dq[q];
+    const int ok = gj_inverse(m, A) == 0;
+    for (int r = 0; r < m; ++r)
+        for (int q = 0; q < m; ++q) Einv[(size_t)r * m + q] = A[(size_t)r * m + q] * dq[r] * dq[q];
+    free(A); free(dq);
     return ok;
 }
 

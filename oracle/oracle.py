@@ -54,6 +54,8 @@ def lib():
         L.ora_gp_linearize.argtypes = [ctypes.c_void_p, _dp, _dp, _dp]
         L.ora_gp_solve.argtypes = [ctypes.c_void_p, ctypes.c_double]
         L.ora_gp_get_ds.argtypes = [ctypes.c_void_p, _dp]
+        L.ora_spd_inverse.argtypes = [ctypes.c_int, _dp, _dp]
+        L.ora_spd_inverse.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -84,6 +86,15 @@ def evaluate(model, X, cam, pp, uv=None, want_jac=True):
     lib().ora_eval(model, n, _d(X), _d(cam), _d(pp), _d(u) if u is not None else None, _d(r),
                    _d(Jc) if want_jac else None, _d(Jp) if want_jac else None)
     return r, Jc, Jp
+
+
+def spd_inverse(E):
+    """The two-level preconditioner's coarse inverse as the oracle forms it (equilibrated blocked Gauss-Jordan).
+    Returns (E^-1, positive definite?)."""
+    E = np.ascontiguousarray(E, np.float64)
+    X = np.zeros_like(E)
+    ok = lib().ora_spd_inverse(E.shape[0], _d(E), _d(X))
+    return X, bool(ok)
 
 
 def retract_pose(x7, d6):

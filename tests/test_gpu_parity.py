@@ -30,7 +30,7 @@ def engines(prob, **kw):
                          **kw)
     ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                      optimize_poses=int(kw.get("optimize_poses", True)), precond=kw.get("precond", 1),
-                     cluster_size=kw.get("cluster_size", 32))
+                     cluster_size=kw.get("cluster_size", 16))
     return eng, ora
 
 
@@ -254,10 +254,13 @@ def test_repeated_solves_lagged_coarse_inverse(model):
             assert it_g == it_o, (rep, k, it_g, it_o)
             err = rel(eng.debug_get(7, (prob.n_cams, eng.D)), ora.get(O.DC))
             # own-E solves: 1e-8 like every other solve.  Lagged solves run with the previous solve's E^-1, a worse
-            # fit to the current S~, which amplifies the (last-bit) differences of the two E^-1 computations: up to
-            # ~1e-7 seen with D = 16 (cond(E) ~ 4e11); still 100x inside the PCG tolerance (1e-5).
+            # fit to the current S~, which amplifies the rounding differences of the two E^-1 computations (same
+            # blocked Gauss-Jordan algorithm; FMA / MFMA accumulation order differ).  With D = 16 (ten intrinsics,
+            # cond(E) ~ 4e11) E^-1 itself is only determined to ~cond(E) u ~ 4e-5 in its worst direction by any f64
+            # algorithm: up to 4e-6 seen there, 1e-7 for D <= 12.
             lagged = relin and k > 0
-            assert err < (1e-6 if lagged else 1e-8), (rep, k, err)
+            tol_lag = 1e-5 if eng.D == 16 else 1e-6
+            assert err < (tol_lag if lagged else 1e-8), (rep, k, err)
         eng.close()
 
 
@@ -377,3 +380,44 @@ def test_schur_variant_step_parity(variant):
         assert abs(lg - lo) / lo < 1e-10, (s, lg, lo)
         assert rel(cg.cpu().numpy(), co) < 1e-9
         assert rel(pg.cpu().numpy(), po) < 1e-9
+
+
+def _spd(m, seed, cond_exp=4.0):
+    """B B^T + 1e-3 m I with rows / columns scaled over cond_exp decades (the coarse matrix's wide diagonal)."""
+    rng = np.random.default_rng(seed)
+    B = rng.normal(size=(m, m))
+    sc = 10.0 ** (cond_exp * np.arange(m) / max(1, m - 1))
+    return (B @ B.T + 1e-3 * m * np.eye(m)) * sc[:, None] * sc[None, :], sc
+
+
+@pytest.mark.parametrize("m", [1, 5, 32, 33, 279, 567, 747, 768])
+def test_coarse_inverse_matches_numpy(m):
+    """The two-level preconditioner's E^-1 (blocked Gauss-Jordan, f64 MFMA; k_gj_pivot / k_gj_update) vs numpy's
+    inverse, in the scale-free metric max |D^-1 (E X - I) D|, and a non-positive-definite matrix is reported."""
+    import ctypes
+    from instantsfm_amd import _capi
+    L = _capi.load()
+    E, sc = _spd(m, seed=m)
+    Ed = dev(E)
+    Xd = torch.empty_like(Ed)
+    us = ctypes.c_double()
+    rc = L.insfm_ba_debug_spd_inverse(m, ctypes.c_void_p(Ed.data_ptr()), ctypes.c_void_p(Xd.data_ptr()), None, 5,
+                                      ctypes.byref(us))
+    assert rc == 1
+    X = Xd.cpu().numpy()
+    res = (E @ X - np.eye(m)) * sc[None, :] / sc[:, None]
+    assert np.abs(res).max() < 1e-9, np.abs(res).max()
+    ref = np.linalg.inv(E)
+    assert np.abs((X - ref) * sc[:, None] * sc[None, :]).max() < 1e-8
+    # the oracle runs the same steps, pivots and fused multiply-adds
+    Xo, oko = O.spd_inverse(E)
+    assert oko
+    dev_o = np.abs((X - Xo) * sc[:, None] * sc[None, :]).max()
+    print(f"m={m}: {us.value:.1f} us per inverse; vs oracle: bitwise {np.array_equal(X, Xo)}, max scaled diff {dev_o:.2e}")
+    assert dev_o < 1e-12
+    if m > 1:
+        En = E.copy()
+        En[m // 2, m // 2] = -abs(En[m // 2, m // 2])   # not positive definite
+        rc = L.insfm_ba_debug_spd_inverse(m, ctypes.c_void_p(dev(En).data_ptr()), ctypes.c_void_p(Xd.data_ptr()),
+                                          None, 0, None)
+        assert rc == 0

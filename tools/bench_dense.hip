@@ -1,6 +1,6 @@
-// Dense coarse-factorization harness (k_tl_chol / k_tl_dinv / k_tl_trinv / k_tl_gram): random SPD E of size m,
-// checks ||E E^-1 - I||_max and reports per-kernel device time plus the Cholesky's per-phase clocks.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/bench_dense.hip -o tools/bench_dense && tools/bench_dense 279
+// Dense coarse-inverse harness (k_gj_pinv0 + k_gj_step): random SPD E of size m with a wide diagonal scaling,
+// checks max |D^-1 (E Einv - I) D| and reports the device time per inversion.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/bench_dense.hip -o tools/bench_dense && tools/bench_dense 567
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -21,14 +21,11 @@ using namespace insfm;
     } while (0)
 
 int main(int argc, char** argv) {
-    const int m = argc > 1 ? std::atoi(argv[1]) : 279;
+    const int m = argc > 1 ? std::atoi(argv[1]) : 567;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 20;
-    const bool verify_all = argc > 3 && std::atoi(argv[3]) != 0;
-    int nbad = 0;
-    if (m < 1 || m > kCoarseMax) { std::printf("m out of range\n"); return 2; }
+    if (m < 1 || m > 4096) { std::printf("m out of range\n"); return 2; }
     std::mt19937_64 rng(1);
     std::normal_distribution<double> nd;
-    // E = B B^T + m I scaled by a wide diagonal (condition ~1e8, like the coarse matrix)
     std::vector<double> B((size_t)m * m), E((size_t)m * m, 0.0), sc(m);
     for (auto& v : B) v = nd(rng);
     for (int i = 0; i < m; ++i) sc[i] = std::pow(10.0, 4.0 * i / std::max(1, m - 1));
@@ -39,90 +36,49 @@ int main(int argc, char** argv) {
             if (i == j) s += 1e-3 * m;
             E[(size_t)i * m + j] = E[(size_t)j * m + i] = s * sc[i] * sc[j];
         }
-    const int nB = (m + kNB - 1) / kNB;
-    double *dE, *dA, *dDinv, *dLinv, *dEinv;
+    const int nB = gj_steps(m), ld = nB * kGB;
+    std::vector<double> Ep((size_t)ld * ld, 0.0), dh(ld, 1.0);
+    for (int i = 0; i < ld; ++i)
+        for (int j = 0; j < ld; ++j) Ep[(size_t)i * ld + j] = (i < m && j < m) ? E[(size_t)i * m + j] : (i == j ? 1.0 : 0.0);
+    for (int i = 0; i < m; ++i) dh[i] = 1.0 / std::sqrt(E[(size_t)i * m + i]);
+    double *dE, *dA, *dW, *dX, *dd, *dP;
     int* dok;
-    long long* dprof;
-    CK(hipMalloc(&dE, sizeof(double) * m * m));
-    CK(hipMalloc(&dA, sizeof(double) * m * m));
-    CK(hipMalloc(&dDinv, sizeof(double) * nB * kNB * kNB));
-    CK(hipMalloc(&dLinv, sizeof(double) * m * m));
-    CK(hipMalloc(&dEinv, sizeof(double) * m * m));
-    CK(hipMalloc(&dok, sizeof(int) * 4));
-    CK(hipMalloc(&dprof, sizeof(long long) * 64));
-    CK(hipMemset(dLinv, 0, sizeof(double) * m * m));
-    CK(hipMemset(dprof, 0, sizeof(long long) * 64));
-    CK(hipMemcpy(dE, E.data(), sizeof(double) * m * m, hipMemcpyHostToDevice));
-    const size_t chol_lds = sizeof(double) * (size_t)m * kCPS;
-    const size_t trinv_lds = sizeof(double) * ((size_t)m * kPS + (size_t)kNB * (m + 1));
-    CK(hipFuncSetAttribute((const void*)k_tl_chol, hipFuncAttributeMaxDynamicSharedMemorySize, (int)chol_lds));
-    CK(hipFuncSetAttribute((const void*)k_tl_trinv, hipFuncAttributeMaxDynamicSharedMemorySize, (int)trinv_lds));
-    hipStream_t st = nullptr;
-    if (argc > 4 && std::atoi(argv[4]) != 0) CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    hipEvent_t ev[5];
-    for (auto& e : ev) CK(hipEventCreate(&e));
-    float tms[4] = {0, 0, 0, 0};
+    CK(hipMalloc(&dE, sizeof(double) * ld * ld));
+    CK(hipMalloc(&dA, sizeof(double) * ld * ld));
+    CK(hipMalloc(&dW, sizeof(double) * ld * ld));
+    CK(hipMalloc(&dX, sizeof(double) * m * m));
+    CK(hipMalloc(&dd, sizeof(double) * ld));
+    CK(hipMalloc(&dP, sizeof(double) * 2 * kGB * kGB));
+    CK(hipMalloc(&dok, sizeof(int)));
+    CK(hipMemcpy(dE, Ep.data(), sizeof(double) * ld * ld, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dd, dh.data(), sizeof(double) * ld, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float tot = 0.f;
     for (int r = 0; r < reps; ++r) {
-        CK(hipMemcpyAsync(dA, dE, sizeof(double) * m * m, hipMemcpyDeviceToDevice, st));
-        CK(hipEventRecord(ev[0], st));
-        k_tl_chol<<<1, 1024, chol_lds, st>>>(m, dA, dok, r == reps - 1 ? dprof : nullptr);
-        CK(hipEventRecord(ev[1], st));
-        k_tl_dinv<<<nB, 64, 0, st>>>(m, dA, dDinv, dok);
-        CK(hipEventRecord(ev[2], st));
-        k_tl_trinv<<<nB, 256, trinv_lds, st>>>(m, dA, dDinv, dLinv, dok);
-        CK(hipEventRecord(ev[3], st));
-        k_tl_gram<<<nB * nB, 256, 0, st>>>(m, dLinv, dEinv, dok);
-        CK(hipEventRecord(ev[4], st));
-        CK(hipEventSynchronize(ev[4]));
-        if (verify_all) {
-            int okr = 0;
-            CK(hipMemcpy(&okr, dok, sizeof(int), hipMemcpyDeviceToHost));
-            std::vector<double> Er((size_t)m * m);
-            CK(hipMemcpy(Er.data(), dEinv, sizeof(double) * m * m, hipMemcpyDeviceToHost));
-            double e2 = 0.0;
-            for (int j = 0; j < m; j += std::max(1, m / 16))
-                for (int i = 0; i < m; ++i) {
-                    double s = 0.0;
-                    for (int k = 0; k < m; ++k) s += E[(size_t)i * m + k] * Er[(size_t)k * m + j];
-                    s -= (i == j) ? 1.0 : 0.0;
-                    e2 = std::max(e2, std::fabs(s) * sc[j] / sc[i]);
-                }
-            if (!okr || !(e2 < 1e-6)) { ++nbad; std::printf("rep %d: ok=%d err=%.3e\n", r, okr, e2); }
-        }
-        if (r >= 2)
-            for (int k = 0; k < 4; ++k) {
-                float ms;
-                CK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
-                tms[k] += ms;
-            }
+        CK(hipMemcpy(dA, dE, sizeof(double) * ld * ld, hipMemcpyDeviceToDevice));
+        CK(hipEventRecord(e0, nullptr));
+        for (int u = 0; u <= nB; ++u) launch_gj_unit(u, m, dA, dW, dP, dd, dX, dok, nullptr);
+        CK(hipEventRecord(e1, nullptr));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 2) tot += ms;
     }
     int ok = 0;
     CK(hipMemcpy(&ok, dok, sizeof(int), hipMemcpyDeviceToHost));
-    std::vector<double> Ei((size_t)m * m);
-    CK(hipMemcpy(Ei.data(), dEinv, sizeof(double) * m * m, hipMemcpyDeviceToHost));
-    // scaled residual: D^-1 (E Einv - I) D with D = diag(sc) removes the diagonal scaling
+    std::vector<double> X((size_t)m * m);
+    CK(hipMemcpy(X.data(), dX, sizeof(double) * m * m, hipMemcpyDeviceToHost));
     double err = 0.0;
     for (int i = 0; i < m; ++i)
         for (int j = 0; j < m; ++j) {
             double s = 0.0;
-            for (int k = 0; k < m; ++k) s += E[(size_t)i * m + k] * Ei[(size_t)k * m + j];
+            for (int k = 0; k < m; ++k) s += E[(size_t)i * m + k] * X[(size_t)k * m + j];
             s -= (i == j) ? 1.0 : 0.0;
             err = std::max(err, std::fabs(s) * sc[j] / sc[i]);
         }
-    std::vector<long long> pf(64);
-    CK(hipMemcpy(pf.data(), dprof, sizeof(long long) * 64, hipMemcpyDeviceToHost));
-    const int n = reps - 2;
-    std::printf("m=%d ok=%d max|D^-1(E Einv - I)D|=%.3e  us: chol %.1f dinv %.1f trinv %.1f gram %.1f\n", m, ok, err,
-                1e3 * tms[0] / n, 1e3 * tms[1] / n, 1e3 * tms[2] / n, 1e3 * tms[3] / n);
-    long long prev = pf[63];
-    long long tot[3] = {0, 0, 0};
-    const int nsteps = std::min(20, (m + kCB - 1) / kCB);
-    for (int b = 0; b < nsteps; ++b)
-        for (int p = 0; p < 3; ++p) {
-            tot[p] += pf[3 * b + p] - prev;
-            prev = pf[3 * b + p];
-        }
-    std::printf("chol clocks (first %d block steps): diag %lld panel %lld trailing %lld\n", nsteps, tot[0], tot[1], tot[2]);
-    if (verify_all) std::printf("verified %d reps: %d bad\n", reps, nbad);
-    return (ok && err < 1e-6 && nbad == 0) ? 0 : 1;
+    std::printf("m=%d ok=%d max|D^-1(E Einv - I)D|=%.3e  %.1f us per inverse (%d launches)\n", m, ok, err,
+                1e3 * tot / std::max(1, reps - 2), nB + 1);
+    return (ok && err < 1e-6) ? 0 : 1;
 }
