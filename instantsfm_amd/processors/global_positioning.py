@@ -57,12 +57,18 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     if not keep.all():
         img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
     if depths is not None:
-        dep = np.array([float(images[i].depths[f]) for i, f in zip(img_id.tolist(), feat_id.tolist())], dtype=np.float64)
+        # image.depths[feature_id] keeps the depth map's dtype (float32 from data_reader.py:132), and so does the
+        # reference's 1 / depth (:133); the list becomes float64 only in the final np.array
+        dep_img = [np.asarray(im.depths).reshape(-1) for im in images]
+        dep_off = np.concatenate([[0], np.cumsum([d.shape[0] for d in dep_img])]).astype(np.int64)
+        dep_all = np.concatenate(dep_img) if dep_img else np.zeros(0)
+        dep = dep_all[dep_off[img_id] + feat_id]
         if depth_only:                                                                          # :129-130
             m = dep != 0
             img_id, feat_id, tid, dep = img_id[m], feat_id[m], tid[m], dep[m]
         available = dep != 0                                                                    # :131-134
-        scales = 1.0 / np.where(available, dep, 1.0)
+        safe = np.where(available, dep, np.ones(1, dtype=dep.dtype))
+        scales = np.where(available, (1 / safe), 1.0).astype(np.float64)
     else:
         available = np.zeros(img_id.size, dtype=bool)
         scales = np.ones(img_id.size)                                                           # :146-147

@@ -22,7 +22,11 @@ def NormalizeReconstruction(images, tracks, depths=None, fixed_scale=False, exte
         xyz = [np.asarray(t.xyz, dtype=np.float64) for t in tracks.values()]
         counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
         allobs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
-        dep = np.array([float(images[i].depths[f]) for i, f in allobs.tolist()], dtype=np.float64)
+        # depths keep the depth map's dtype: np.log(np.array(depth_gt_list)) is a float32 log for float32 maps
+        dep_img = [np.asarray(im.depths).reshape(-1) for im in images]
+        dep_off = np.concatenate([[0], np.cumsum([d.shape[0] for d in dep_img])]).astype(np.int64)
+        dep_all = np.concatenate(dep_img) if dep_img else np.zeros(0)
+        dep = dep_all[dep_off[allobs[:, 0]] + allobs[:, 1]] if allobs.shape[0] else dep_all[:0]
         m = dep > 0
         if m.any():
             P = np.repeat(np.array(xyz).reshape(-1, 3), counts, axis=0)[m]

@@ -10,7 +10,7 @@ from instantsfm_amd.engine import GP_DEFAULTS
 from instantsfm_amd.scene.defs import Camera, CameraModelId, Image, Track
 
 OPTS = dict(min_num_view_per_track=3, thres_loss_function=1e-1, max_num_iterations=100, function_tolerance=5e-4)
-NAMES = ["gp_packing_plain", "gp_packing_depth", "gp_packing_depth_only", "gp_packing_edge"]
+NAMES = ["gp_packing_plain", "gp_packing_depth", "gp_packing_depth_only", "gp_packing_edge", "gp_packing_depth_f32"]
 
 
 def scene_from_fixture(g):

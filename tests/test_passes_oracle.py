@@ -62,11 +62,15 @@ def test_oracle_filter_tri_angle_matches_reference(golden):
     assert len(removed) == int(golden["tri_counter"])
 
 
-@pytest.mark.parametrize("depths", [None, np.ones(3)])
-def test_normalize_reconstruction_matches_reference(golden, depths):
+@pytest.mark.parametrize("depths,f32", [(None, False), (np.ones(3), False), (np.ones(3), True)])
+def test_normalize_reconstruction_matches_reference(golden, depths, f32):
+    """f32: float32 depth maps (data_reader.py:132) -- the reference's log runs in float32 then."""
     imgs, tracks = load_scene(golden)
+    if f32:
+        for im in imgs:
+            im.depths = np.asarray(im.depths).astype(np.float32)
     NormalizeReconstruction(imgs, tracks, depths)
-    pre = "norm_" if depths is None else "normdepth_"
+    pre = "norm_" if depths is None else ("normdepth32_" if f32 else "normdepth_")
     np.testing.assert_allclose(np.stack([im.world2cam for im in imgs]), golden[pre + "w2c"], rtol=1e-13, atol=1e-12)
     np.testing.assert_allclose(np.stack([t.xyz for t in tracks.values()]), golden[pre + "xyz"], rtol=1e-13, atol=1e-12)
 

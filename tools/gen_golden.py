@@ -281,7 +281,7 @@ def _gp_scene_arrays(cameras, images, tracks):
     keys = list(tracks.keys())
     obs = [np.asarray(tracks[k].observations, dtype=np.int64).reshape(-1, 2) for k in keys]
     fu = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) for im in images]
-    dep = [np.asarray(im.depths, dtype=np.float64).reshape(-1) for im in images]
+    dep = [np.asarray(im.depths).reshape(-1) for im in images]   # kept in their dtype (float32 depth maps)
     return dict(
         cam_prior_focal=np.array([c.has_prior_focal_length for c in cameras]),
         img_cam_id=np.array([im.cam_id for im in images]),
@@ -355,7 +355,7 @@ def gen_gp_packing(out_dir, LM):
     opts = dict(min_num_view_per_track=3, thres_loss_function=1e-1, max_num_iterations=100, function_tolerance=5e-4)
     rng = np.random.default_rng(7)
 
-    def build(prob, with_depth, extra):
+    def build(prob, with_depth, extra, f32=False):
         C = prob.n_cams
         cams = [Camera(id=c, model_id=CameraModelId.SIMPLE_RADIAL, params=[1000.0, 500.0, 400.0, 0.0],
                        has_prior_focal_length=bool(prob.fcam[c] == 1.0)) for c in range(C)]
@@ -377,6 +377,8 @@ def gen_gp_packing(out_dir, LM):
             fu = rays_world @ R.T  # features_undist = R t  so that  R^T fu = t
             dep = np.where(rng.uniform(size=fu.shape[0]) < 0.5, rng.uniform(1, 20, fu.shape[0]), 0.0) if with_depth \
                 else np.zeros(fu.shape[0])
+            if f32:
+                dep = dep.astype(np.float32)   # depth maps are float32 (controllers/data_reader.py:132)
             imgs.append(Image(id=c, cam_id=c, is_registered=True, world2cam=w2c, features=np.zeros((fu.shape[0], 2)),
                               features_undist=fu, depths=dep))
         ptr = np.concatenate([[0], np.cumsum(np.bincount(prob.pt_idx, minlength=prob.n_points))])
@@ -396,10 +398,11 @@ def gen_gp_packing(out_dir, LM):
     cases = [("gp_packing_plain", dict(seed=3), False, False, False),
              ("gp_packing_depth", dict(seed=4), True, False, False),
              ("gp_packing_depth_only", dict(seed=5), True, True, False),
-             ("gp_packing_edge", dict(seed=6), True, False, True)]
+             ("gp_packing_edge", dict(seed=6), True, False, True),
+             ("gp_packing_depth_f32", dict(seed=8), True, False, False)]
     for name, kw, with_depth, depth_only, extra in cases:
         prob = make_gp_problem(8, 40, track_len=4, window=3, init="perturbed", **kw)
-        cams, imgs, trks = build(prob, with_depth, extra)
+        cams, imgs, trks = build(prob, with_depth, extra, f32=name.endswith("_f32"))
         res = _gp_scene_arrays(cams, imgs, trks)
         depths = np.concatenate([np.asarray(im.depths) for im in imgs]) if with_depth else None
         res["has_depths"] = np.array(depths is not None)
@@ -493,8 +496,11 @@ def gen_passes(out_dir):
     cnt = TF.FilterTracksTriangulationAngle(None, ims, trs, 1.5)
     res.update(tracks_out(trs, "tri_"))
     res["tri_counter"] = np.array(cnt)
-    for name, dep in (("norm_", None), ("normdepth_", np.ones(3))):
+    for name, dep in (("norm_", None), ("normdepth_", np.ones(3)), ("normdepth32_", np.ones(3))):
         ims, trs = copy.deepcopy(imgs), copy.deepcopy(tracks)
+        if name == "normdepth32_":
+            for im in ims:
+                im.depths = im.depths.astype(np.float32)   # float32 depth maps (data_reader.py:132)
         NormalizeReconstruction(ims, trs, dep)
         res[name + "w2c"] = np.stack([im.world2cam for im in ims])
         res[name + "xyz"] = np.stack([t.xyz for t in trs.values()])
