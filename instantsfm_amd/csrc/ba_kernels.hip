@@ -1636,6 +1636,13 @@ constexpr int kCgAhead = CG_AHEAD;  // CG iterations the host keeps queued ahead
 // kernel launches (~5-10 us of host time each), so the chain can be issued piecemeal while the host waits on the CG.
 int side_units(const insfm_ba* h) { return 2 + gj_steps(h->tl.m); }
 
+// INSFM_EROW_MAIN=1: the E build runs on the main stream with its full grid right after the basis (experiment:
+// the capped side-stream build overlaps and slows several CG iterations).
+bool erow_on_main() {
+    static const bool v = [] { const char* e = std::getenv("INSFM_EROW_MAIN"); return e && std::atoi(e) != 0; }();
+    return v;
+}
+
 int side_issue(insfm_ba* h) {
     if (h->side_slot < 0) return 0;
     const int slot = h->side_slot, u = h->side_next;
@@ -1643,7 +1650,7 @@ int side_issue(insfm_ba* h) {
     int rc = 0;
     if (u == 0) {
         HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
-        if ((rc = run_tl_build(h, slot, fs))) return rc;
+        if (!(erow_on_main() && !h->tl_sync) && (rc = run_tl_build(h, slot, fs))) return rc;
         HIPCHK(hipEventRecord(h->ev_built, fs));
         h->built_pending = true;
     } else if ((rc = run_tl_gj_unit(h, slot, u - 1, fs))) {
@@ -1670,6 +1677,7 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
     if (rc) return rc;
     const int slot = (int)(h->tl_solves & 1);
     if ((rc = run_tl_basis(h, cams, h->stream))) return rc;
+    if (erow_on_main() && !h->tl_sync && (rc = run_tl_build(h, slot, h->stream))) return rc;
     HIPCHK(hipEventRecord(h->ev_E, h->stream));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
