@@ -2762,7 +2762,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
-        const int DPd = D + (D & 1), CH = D <= 9 ? 32 : 16;
+        const int DPd = D + (D & 1), CH = EROW_CH;
         h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
                                         (size_t)maxseg * MC * MC);
         {

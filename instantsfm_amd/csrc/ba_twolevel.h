@@ -125,11 +125,17 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
     if (k < D) tl.vc[(size_t)tl.cpos[i] * D + k] = r[k];
 }
 
+#ifndef EROW_CH
+#define EROW_CH 16
+#endif
 template <int D>
 struct ErowGeom {
     static constexpr int MC = D + 1;
     static constexpr int DP = D + (D & 1);
-    static constexpr int CH = D <= 9 ? 32 : 16;   // neighbour blocks staged per round
+    // neighbour blocks staged per round: small enough that a k_tl_erow workgroup (side stream) and a k_tl_pc
+    // workgroup (main stream, ~110 KB of LDS) fit one CU together -- with 32 blocks (59 KB) they did not, and the
+    // CG's k_tl_pc waited ~150 us per solve for the E build's workgroups to drain
+    static constexpr int CH = EROW_CH;
 };
 
 // One workgroup per camera row i: per neighbour cluster c, Oseg = [c == c_i] Z~_i^T Z~_i + sum over the row's
