@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -1358,6 +1359,29 @@ namespace {
         }                                                                                         \
     } while (0)
 
+// Host worker threads for create's independent per-camera loops (transient: joined before create returns).
+int host_threads(int work) {
+    static const int hw = [] {
+        const char* e = std::getenv("INSFM_HOST_THREADS");
+        const int v = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+        return std::max(1, std::min(v, 16));
+    }();
+    return std::max(1, std::min(hw, work / 64));
+}
+
+// f(thread, begin, end) over [0, n) split into nth contiguous ranges (thread 0 runs on the caller).
+template <typename F>
+void parallel_ranges(int n, int nth, F&& f) {
+    std::vector<std::thread> ts;
+    const int per = (n + nth - 1) / nth;
+    for (int t = 1; t < nth; ++t) {
+        const int a = t * per, b = std::min(n, a + per);
+        if (a < b) ts.emplace_back([&f, t, a, b] { f(t, a, b); });
+    }
+    f(0, 0, std::min(n, per));
+    for (auto& th : ts) th.join();
+}
+
 int dalloc(insfm_ba* h, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     hipError_t e = hipMalloc(p, bytes);
@@ -1457,23 +1481,37 @@ CovisGraph covis_graph(int C, const std::vector<int>& gcptr, const std::vector<i
                        const int32_t* cam_idx, const int32_t* pt_idx) {
     CovisGraph g;
     g.ptr.assign(C + 1, 0);
-    std::vector<int> mark(C, -1), buf;
-    std::vector<long long> acc(C, 0);
-    for (int i = 0; i < C; ++i) {
-        buf.clear();
-        for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
-            const int o = gcobs[e], p = pt_idx[o];
-            for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
-                if (q == o) continue;
-                const int j = cam_idx[q];
-                if (j == i) continue;
-                if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf.push_back(j); }
-                acc[j] += 1;
+    // rows are independent: camera ranges on transient host threads, concatenated in row order
+    const int nth = host_threads(C);
+    std::vector<std::vector<int>> pnb(nth);
+    std::vector<std::vector<long long>> pw(nth);
+    std::vector<int> rlen(C, 0);
+    parallel_ranges(C, nth, [&](int t, int i0, int i1) {
+        std::vector<int> mark(C, -1), buf;
+        std::vector<long long> acc(C, 0);
+        for (int i = i0; i < i1; ++i) {
+            buf.clear();
+            for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
+                const int o = gcobs[e], p = pt_idx[o];
+                for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
+                    if (q == o) continue;
+                    const int j = cam_idx[q];
+                    if (j == i) continue;
+                    if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf.push_back(j); }
+                    acc[j] += 1;
+                }
             }
+            std::sort(buf.begin(), buf.end());
+            for (int j : buf) { pnb[t].push_back(j); pw[t].push_back(acc[j]); }
+            rlen[i] = (int)buf.size();
         }
-        std::sort(buf.begin(), buf.end());
-        for (int j : buf) { g.nb.push_back(j); g.w.push_back(acc[j]); }
-        g.ptr[i + 1] = (int)g.nb.size();
+    });
+    for (int i = 0; i < C; ++i) g.ptr[i + 1] = g.ptr[i] + rlen[i];
+    g.nb.reserve(g.ptr[C]);
+    g.w.reserve(g.ptr[C]);
+    for (int t = 0; t < nth; ++t) {
+        g.nb.insert(g.nb.end(), pnb[t].begin(), pnb[t].end());
+        g.w.insert(g.w.end(), pw[t].begin(), pw[t].end());
     }
     return g;
 }
@@ -1629,7 +1667,11 @@ int run_tl_gj_unit(insfm_ba* h, int slot, int u, hipStream_t stream) {
 #ifndef CG_INIT_BACK
 #define CG_INIT_BACK 2
 #endif
-constexpr int kCgAhead = CG_AHEAD;  // CG iterations the host keeps queued ahead of the device (pipelined two-level PCG)
+constexpr int kCgAhead = CG_AHEAD;
+#ifndef SIDE_AHEAD
+#define SIDE_AHEAD 2
+#endif
+constexpr int kSideAhead = SIDE_AHEAD;  // extra CG iterations kept queued while side-chain units remain to be issued  // CG iterations the host keeps queued ahead of the device (pipelined two-level PCG)
 
 // The side-stream chain of a solve, in issue units: 0 = wait for the basis (ev_E), E build (k_tl_erow, k_tl_ereduce),
 // ev_built; 1 .. nB + 1 = the Gauss-Jordan launches, the last followed by ev_fact[slot].  Each unit is one or two
@@ -1823,12 +1865,20 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             volatile int* pg = h->prog_host;
             pg[0] = pg[1] = pg[2] = pg[3] = 0;
             std::atomic_thread_fence(std::memory_order_seq_cst);
+            // INSFM_HOST_TRACE=1: per solve, host microseconds spent enqueueing CG iterations / issuing side units, and
+            // the longest single call of each (stderr; diagnostics of host-bound launch gaps)
+            static const bool htrace = [] { const char* e = std::getenv("INSFM_HOST_TRACE"); return e && *e == '1'; }();
+            double t_enq = 0.0, t_side = 0.0, m_enq = 0.0, m_side = 0.0, t_sol0 = htrace ? wall_seconds() : 0.0;
+            int n_enq = 0, n_side = 0;
             auto enqueue = [&](int from, int to) -> int {
-                return with_D(D, [&](auto dc_) -> int {
+                const double t0 = htrace ? wall_seconds() : 0.0;
+                const int r = with_D(D, [&](auto dc_) -> int {
                     constexpr int DV = decltype(dc_)::value;
                     for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
                     return launch_err(h, "k_tl_pc/k_tl_pspmv");
                 });
+                if (htrace) { const double dt = wall_seconds() - t0; t_enq += dt; m_enq = std::max(m_enq, dt / std::max(1, to - from)); n_enq += to - from; }
+                return r;
             };
             rec(h, 8);
             // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step);
@@ -1837,6 +1887,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             if ((rc = enqueue(0, enq))) return rc;
             CgPoll poll;
             poll.enq = enq;
+            poll.extra_ahead = h->side_slot >= 0 ? kSideAhead : 0;
             static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
             int erc = 0;
             const int pr = cg_poll(
@@ -1848,10 +1899,15 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 },
                 wall_seconds,
                 [&] {
-                    // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax
+                    // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax.  While
+                    // side units remain, two more CG iterations are kept queued: a side launch can hold the host
+                    // for longer than two iterations take on the GPU
                     if (h->side_slot >= 0) {
+                        const double t0 = htrace ? wall_seconds() : 0.0;
                         const int r = side_issue(h);
+                        if (htrace) { const double dt = wall_seconds() - t0; t_side += dt; m_side = std::max(m_side, dt); ++n_side; }
                         if (r && !erc) erc = r;
+                        poll.extra_ahead = h->side_slot >= 0 ? kSideAhead : 0;
                         return;
                     }
 #if defined(__x86_64__)
@@ -1859,8 +1915,14 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
 #endif
                 },
                 &erc);
+            const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
             if (!erc) erc = side_drain(h);  // whatever the CG left unissued
             if (erc) return erc;
+            if (htrace)
+                std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
+                             "%d side units in the poll loop in %.1f us (max %.1f), %d left for after the CG\n",
+                             1e6 * (wall_seconds() - t_sol0), n_enq, 1e6 * t_enq, 1e6 * m_enq, n_side, 1e6 * t_side,
+                             1e6 * m_side, left);
             enq = poll.enq;
             if (pr == CgPoll::kEnqueueError) return erc;
             if (pr == CgPoll::kStreamError) {
@@ -2187,6 +2249,12 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->p1 = desc->shard_point_end < 0 ? P : std::min(P, desc->shard_point_end);
     if (h->p1 < h->p0) return fail(INSFM_BA_EINVAL, "bad shard range");
     h->Pl = h->p1 - h->p0;
+    // INSFM_CREATE_TRACE=1: host milliseconds of create's phases (stderr)
+    static const bool ctrace = [] { const char* e = std::getenv("INSFM_CREATE_TRACE"); return e && *e == '1'; }();
+    const double ct0 = wall_seconds();
+    auto tick = [&](const char* what) {
+        if (ctrace) std::fprintf(stderr, "[insfm create] %-28s %8.1f ms\n", what, 1e3 * (wall_seconds() - ct0));
+    };
     // global track pointers
     std::vector<int> gptr(P + 1, 0);
     for (int i = 0; i < N; ++i) gptr[pt_idx[i] + 1]++;
@@ -2212,23 +2280,35 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             lust[o] = u;
         }
     }
+    tick("local track order");
     std::vector<int> cptr(C + 1, 0), cobs(Nl);
     for (int o = 0; o < Nl; ++o) cptr[lcam[o] + 1]++;
     for (int c = 0; c < C; ++c) cptr[c + 1] += cptr[c];
     {
+        // balance the Schur groups: within a camera, observations with more upper partners first (stable) -- one
+        // counting sort on (camera, descending partner count) instead of a comparison sort per camera
+        std::vector<int> key(Nl);
+        int kmax = 0;
+        for (int o = 0; o < Nl; ++o) {
+            key[o] = lptr[lptl[o] + 1] - lust[o];
+            kmax = std::max(kmax, key[o]);
+        }
+        std::vector<int> byk(kmax + 2, 0), order(Nl);
+        for (int o = 0; o < Nl; ++o) byk[kmax - key[o] + 1]++;
+        for (int k = 0; k <= kmax; ++k) byk[k + 1] += byk[k];
+        for (int o = 0; o < Nl; ++o) order[byk[kmax - key[o]]++] = o;   // descending key, stable
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
-        for (int o = 0; o < Nl; ++o) cobs[fill[lcam[o]]++] = o;
-        // balance the Schur groups: within a camera, observations with more upper partners first
-        for (int c = 0; c < C; ++c)
-            std::stable_sort(cobs.begin() + cptr[c], cobs.begin() + cptr[c + 1], [&](int x, int y) {
-                return (lptr[lptl[x] + 1] - lust[x]) > (lptr[lptl[y] + 1] - lust[y]);
-            });
+        for (int t = 0; t < Nl; ++t) {                                     // stable by camera
+            const int o = order[t];
+            cobs[fill[lcam[o]]++] = o;
+        }
     }
     std::vector<int4> sdesc(std::max(Nl, 1));
     for (int e = 0; e < Nl; ++e) {
         const int o = cobs[e], p = lptl[o];
         sdesc[e] = make_int4(o, p, lust[o], lptr[p + 1]);
     }
+    tick("camera-major lists");
     // global upper pattern (identical on every rank)
     std::vector<int> gcptr(C + 1, 0), gcobs(N);
     for (int i = 0; i < N; ++i) gcptr[cam_idx[i] + 1]++;
@@ -2238,24 +2318,33 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int i = 0; i < N; ++i) gcobs[fill[cam_idx[i]]++] = i;
     }
     std::vector<int> rptr(C + 1, 0), cols;
-    cols.reserve((size_t)C * 8);
     {
-        std::vector<int> mark(C, -1), buf;
-        for (int i = 0; i < C; ++i) {
-            buf.clear();
-            buf.push_back(i);
-            mark[i] = i;
-            for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
-                const int p = pt_idx[gcobs[e]];
-                for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
-                    const int j = cam_idx[q];
-                    if (j > i && mark[j] != i) { mark[j] = i; buf.push_back(j); }
+        // rows are independent: camera ranges on a few transient host threads, each with its own marks
+        const int nth = host_threads(C);
+        std::vector<std::vector<int>> part(nth);
+        std::vector<int> rlen(C, 0);
+        parallel_ranges(C, nth, [&](int t, int i0, int i1) {
+            std::vector<int> mark(C, -1), buf;
+            std::vector<int>& out = part[t];
+            for (int i = i0; i < i1; ++i) {
+                buf.clear();
+                buf.push_back(i);
+                mark[i] = i;
+                for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
+                    const int p = pt_idx[gcobs[e]];
+                    for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
+                        const int j = cam_idx[q];
+                        if (j > i && mark[j] != i) { mark[j] = i; buf.push_back(j); }
+                    }
                 }
+                std::sort(buf.begin(), buf.end());
+                out.insert(out.end(), buf.begin(), buf.end());
+                rlen[i] = (int)buf.size();
             }
-            std::sort(buf.begin(), buf.end());
-            cols.insert(cols.end(), buf.begin(), buf.end());
-            rptr[i + 1] = (int)cols.size();
-        }
+        });
+        for (int i = 0; i < C; ++i) rptr[i + 1] = rptr[i] + rlen[i];
+        cols.reserve(rptr[C]);
+        for (auto& v : part) cols.insert(cols.end(), v.begin(), v.end());
     }
     h->nnzb = rptr[C];
     std::vector<int> brow(h->nnzb);
@@ -2275,6 +2364,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 loblk[k] = e;
             }
     }
+    tick("block pattern");
     // flattened CG neighbour list per row: upper blocks then lower (transposed) ones; pos_up/pos_lo give each upper
     // block's two slots in the row-contiguous copy Sn
     std::vector<int> nptr(C + 1, 0), nj, pup(std::max(1, h->nnzb), -1), plo(std::max(1, h->nnzb), -1);
@@ -2315,6 +2405,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->n_nbr = (int64_t)nj.size();
     for (int i = 0; i < C; ++i) { pup[rptr[i]] = 0; plo[rptr[i]] = 0; }  // diagonal blocks: unused slots
     if (nj.empty()) nj.push_back(0);
+    tick("CG neighbour lists");
     // Schur work items: split long rows so a chunk fits the LDS budget
     const size_t wsh_lds = sizeof(double) * kSchurWaves * (64 / D) * schur_ws(D);  // W^ staging, up to kSchurWaves waves
     const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + wsh_lds + 64;
@@ -2617,6 +2708,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
         return 0;
     });
+    tick("uploads + allocations");
     if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
     if (desc->precond == 1 && h->d.optimize_poses) {
         // ---- two-level preconditioner: clusters, source lists of E, buffers ----
@@ -2630,6 +2722,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             nc = aggregate(g, C, K, lab);
         }
         const int m = nc * MC;
+        tick("covisibility + clusters");
         std::vector<int> clp(nc + 1, 0), clc(C), alone(C);
         for (int i = 0; i < C; ++i) clp[lab[i] + 1]++;
         for (int c = 0; c < nc; ++c) clp[c + 1] += clp[c];
@@ -2688,6 +2781,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 }
             }
         }
+        tick("coarse segments");
         TlBufs& tl = h->tl;
         tl.nc = nc;
         tl.m = m;
@@ -2789,6 +2883,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             else { (void)hipHostFree(pm); h->prog_host = nullptr; }
         }
     }
+    tick("two-level setup (end)");
     if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
     if (const char* ts = std::getenv("INSFM_TL_SYNC")) h->tl_sync = std::atoi(ts) != 0;
     h->damping = 1.0 / desc->tr_radius;

@@ -19,6 +19,7 @@ struct CgPoll {
     int last_reached = 0;   // last progress word seen
     long spins = 0;
     double stalled_s = 0.0; // wall-clock seconds without progress when the poll stopped
+    int extra_ahead = 0;    // the caller may raise it (e.g. while it issues other work from pause()) to keep more queued
 };
 
 // Default stall limit (seconds); the environment variable INSFM_CG_STALL_S overrides it.
@@ -48,7 +49,7 @@ int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reac
             s.last_reached = r;
             t_progress = now();
         }
-        if (s.enq < limit && r >= s.enq - ahead) {
+        if (s.enq < limit && r >= s.enq - ahead - s.extra_ahead) {
             const int to = s.enq + 1 < limit ? s.enq + 1 : limit;
             if ((*rc = enqueue(s.enq, to)) != 0) return CgPoll::kEnqueueError;
             s.enq = to;
