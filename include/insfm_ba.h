@@ -39,6 +39,12 @@ typedef struct insfm_ba insfm_ba;
  * has queued on its stream (a torch.distributed all_reduce on the current stream satisfies this). */
 typedef int (*insfm_ba_allreduce_fn)(void* ctx, double* dev_buf, int64_t count);
 
+/* Optional asynchronous form: enqueue the in-place sum of `count` doubles at `dev_buf` on the HIP stream `stream`
+ * (the library's exchange stream, already ordered after the work that produced the range) and return without waiting
+ * for it (an RCCL all_reduce issued on that stream).  With it the library all-reduces the reduced camera system in row
+ * chunks while the Schur complement of the next chunk is still being built (desc.exchange_chunks). */
+typedef int (*insfm_ba_allreduce_async_fn)(void* ctx, double* dev_buf, int64_t count, void* stream);
+
 typedef struct {
     int32_t n_cams;        /* C: rows of camera_params (registered, observed images after compaction) */
     int32_t n_points;      /* P: rows of points_3d */
@@ -65,6 +71,9 @@ typedef struct {
                               blocks W; 1 re-derives them per pair, LDS-atomic row accumulation; 2 re-derives them,
                               MFMA register accumulation (D <= 8, else 1).  1 and 2 never form W (no 192 B/obs write).
                               The environment variable INSFM_SCHUR=w|rc|mf overrides it. */
+    insfm_ba_allreduce_async_fn allreduce_async; /* optional (see above); uses allreduce_ctx */
+    int32_t exchange_chunks;  /* row chunks of the [S | b] exchange overlapped with the Schur build when allreduce_async
+                                 is set (default 4; 1 = one all-reduce after the whole build) */
 } insfm_ba_desc;
 
 typedef struct {

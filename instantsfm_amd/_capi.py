@@ -17,6 +17,8 @@ INSFM_BA_ECOMM = -101
 INSFM_BA_ESOLVER = -102
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
+ALLREDUCE_ASYNC_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_int64,
+                                      ctypes.c_void_p)
 
 
 class Desc(ctypes.Structure):
@@ -34,6 +36,7 @@ class Desc(ctypes.Structure):
         ("shard_point_begin", ctypes.c_int32), ("shard_point_end", ctypes.c_int32),
         ("allreduce", ALLREDUCE_FN), ("allreduce_ctx", ctypes.c_void_p),
         ("precond", ctypes.c_int32), ("cluster_size", ctypes.c_int32), ("schur_variant", ctypes.c_int32),
+        ("allreduce_async", ALLREDUCE_ASYNC_FN), ("exchange_chunks", ctypes.c_int32),
     ]
 
 

@@ -1334,6 +1334,10 @@ struct insfm_ba {
     // the side-stream chain of a solve still to be issued (slot, next unit): issued a launch at a time from the CG's
     // host poll loop, where the host otherwise only spins
     int side_slot = -1, side_next = 0;
+    // chunked [S | b] exchange (desc.allreduce_async): work-item / row boundaries of the chunks, the exchange stream
+    std::vector<int> xw, xr, rptr_host;
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_x = nullptr, ev_xdone = nullptr;
     bool built_pending = false;
     long long tl_solves = 0;
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
@@ -1453,6 +1457,12 @@ int allreduce(insfm_ba* h, double* buf, int64_t n) {
     if (!h->d.allreduce) { h->err = "world_size > 1 needs an allreduce callback"; return INSFM_BA_ECOMM; }
     int rc = h->d.allreduce(h->d.allreduce_ctx, buf, n);
     if (rc) { h->err = "allreduce callback failed (" + std::to_string(rc) + ")"; return INSFM_BA_ECOMM; }
+    return 0;
+}
+
+int allreduce_async(insfm_ba* h, double* buf, int64_t n) {
+    int rc = h->d.allreduce_async(h->d.allreduce_ctx, buf, n, h->xstream);
+    if (rc) { h->err = "allreduce_async callback failed (" + std::to_string(rc) + ")"; return INSFM_BA_ECOMM; }
     return 0;
 }
 
@@ -1750,8 +1760,10 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
 }
 
 // k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
-int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, double smin, double smax, int sdiag) {
+int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, double smin, double smax, int sdiag,
+                 int w0 = 0, int w1 = -1) {
     const bool det = h->d.deterministic != 0;
+    if (w1 < 0) w1 = h->nwork;
     const int nt = det ? 64 : kSchurWaves * 64;
     if (h->kind == 1) {
         if (det)
@@ -1788,14 +1800,15 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
     }
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
+        if (w1 <= w0) return 0;
         if (det)
-            k_schur<DV, 1><<<h->nwork, nt, h->schur_lds, h->stream>>>(
-                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+            k_schur<DV, 1><<<w1 - w0, nt, h->schur_lds, h->stream>>>(
+                h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
+                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
         else
-            k_schur<DV, kSchurWaves><<<h->nwork, nt, h->schur_lds, h->stream>>>(
-                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+            k_schur<DV, kSchurWaves><<<w1 - w0, nt, h->schur_lds, h->stream>>>(
+                h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
+                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
         return launch_err(h, "k_schur");
     });
 }
@@ -1835,11 +1848,29 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
         rec(h, 6);
-        int rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
-        if (rc) return rc;
-        rec(h, 7);
-        rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
-        if (rc) return rc;
+        int rc = 0;
+        if (h->xstream && !h->schur_rc && !h->schur_mf) {
+            // chunked exchange: each row chunk's blocks of S are summed across ranks on the exchange stream while the
+            // next chunk's Schur rows are built; b (filled by every row) after the last chunk
+            const int K = (int)h->xw.size() - 1;
+            for (int c = 0; c < K; ++c) {
+                if ((rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag, h->xw[c], h->xw[c + 1]))) return rc;
+                const int64_t b0 = h->rptr_host[h->xr[c]], b1 = h->rptr_host[h->xr[c + 1]];
+                HIPCHK(hipEventRecord(h->ev_x, h->stream));
+                HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
+                if (b1 > b0 && (rc = allreduce_async(h, h->S + b0 * D * D, (b1 - b0) * D * D))) return rc;
+            }
+            if ((rc = allreduce_async(h, h->b, (int64_t)h->C * D))) return rc;
+            HIPCHK(hipEventRecord(h->ev_xdone, h->xstream));
+            HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
+            rec(h, 7);
+        } else {
+            rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
+            if (rc) return rc;
+            rec(h, 7);
+            rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
+            if (rc) return rc;
+        }
         if (h->built_pending) {  // the side stream's E build of the previous solve still reads S~ / Z~
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_built, 0));
             h->built_pending = false;
@@ -2176,6 +2207,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->shard_point_begin = 0; d->shard_point_end = -1;
     d->precond = 1;
     d->cluster_size = 16;
+    d->exchange_chunks = 4;
 }
 
 const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() : "null handle"; }
@@ -2192,6 +2224,12 @@ void insfm_ba_destroy(insfm_ba* h) {
         (void)hipStreamSynchronize(h->side);
         (void)hipStreamDestroy(h->side);
     }
+    if (h->xstream) {
+        (void)hipStreamSynchronize(h->xstream);
+        (void)hipStreamDestroy(h->xstream);
+    }
+    if (h->ev_x) (void)hipEventDestroy(h->ev_x);
+    if (h->ev_xdone) (void)hipEventDestroy(h->ev_xdone);
     if (h->ev_E) (void)hipEventDestroy(h->ev_E);
     if (h->ev_built) (void)hipEventDestroy(h->ev_built);
     for (auto& e : h->ev_fact)
@@ -2428,6 +2466,29 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     // (651 vs 667 / 688 us on config 3): neighbouring rows launched together share partner W records in L2/MALL.
     h->nwork = (int)work.size();
     h->max_chunk = maxc;
+    if (kind == 0 && desc->allreduce_async && (desc->world_size > 1 || desc->allreduce) && desc->exchange_chunks > 1 &&
+        desc->optimize_poses) {
+        // chunk boundaries at rows with ~equal block counts, and the first work item of each boundary row
+        const int K = std::min(desc->exchange_chunks, C);
+        h->rptr_host = rptr;
+        h->xr.assign(1, 0);
+        h->xw.assign(1, 0);
+        for (int c = 1; c < K; ++c) {
+            const int64_t target = (int64_t)rptr[C] * c / K;
+            const int r = (int)(std::upper_bound(rptr.begin(), rptr.end(), (int)target) - rptr.begin()) - 1;
+            if (r <= h->xr.back() || r >= C) continue;
+            int w = h->xw.back();
+            while (w < (int)work.size() && work[w].x < r) ++w;
+            h->xr.push_back(r);
+            h->xw.push_back(w);
+        }
+        h->xr.push_back(C);
+        h->xw.push_back((int)work.size());
+        hipError_t e = hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_x, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_xdone, hipEventDisableTiming);
+        if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("exchange stream: ") + hipGetErrorString(e));
+    }
     h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
     // Schur variant (INSFM_SCHUR): "w" (default) reads the stored W records (k_schur); "rc" re-derives the camera-point

@@ -15,7 +15,7 @@ from . import _capi
 # TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.
 LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4, tr_factor=0.5,
                    tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, max_rejects=30, pcg_tol=1e-5,
-                   pcg_max_iter=500, precond=1, cluster_size=16)
+                   pcg_max_iter=500, precond=1, cluster_size=16, exchange_chunks=4)
 
 
 def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
@@ -49,6 +49,41 @@ def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
                 errors.append(e)
             return -1
     return _allreduce
+
+
+def make_allreduce_async_callback(get_buffer, group=None, errors=None, counter=None):
+    """The C ABI's asynchronous exchange callback (insfm_ba_allreduce_async_fn): sum the slice in place across ranks,
+    enqueued on the library's exchange stream ``stream`` without waiting for it.  RCCL ("nccl"): the all_reduce is
+    issued with that stream current (the process group's stream waits for it, and it waits for the collective);
+    gloo: the stream is synchronized and the slice reduced through host memory, then copied back on that stream."""
+    import torch.distributed as dist
+
+    def _allreduce_async(ctx, ptr, count, stream):
+        try:
+            if counter is not None:
+                counter[0] += 1
+            buf = get_buffer()
+            addr = ctypes.cast(ptr, ctypes.c_void_p).value
+            off = (addr - buf.data_ptr()) // buf.element_size()
+            if off < 0 or off + count > buf.numel():
+                raise ValueError("allreduce range outside the exchange buffer")
+            view = buf[off:off + count]
+            xs = torch.cuda.ExternalStream(stream, device=buf.device)
+            if dist.get_backend(group) == "gloo":
+                xs.synchronize()
+                host = view.cpu()
+                dist.all_reduce(host, op=dist.ReduceOp.SUM, group=group)
+                with torch.cuda.stream(xs):
+                    view.copy_(host)
+            else:
+                with torch.cuda.stream(xs):
+                    dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
+            return 0
+        except Exception as e:  # surfaced to the caller as INSFM_BA_ECOMM
+            if errors is not None:
+                errors.append(e)
+            return -1
+    return _allreduce_async
 
 
 def _require_gpu(device):
@@ -115,6 +150,11 @@ class BundleAdjuster:
             self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors,
                                                                   self.exchange_calls))
             d.allreduce = self._cb
+            if d.exchange_chunks > 1:
+                # the reduced camera system is summed in row chunks behind the Schur build (exchange stream)
+                self._cb_async = _capi.ALLREDUCE_ASYNC_FN(make_allreduce_async_callback(
+                    lambda: self._xbuf, process_group, self._errors, self.exchange_calls))
+                d.allreduce_async = self._cb_async
         self._stream = torch.cuda.current_stream(self.device)
         stream = self._stream.cuda_stream
         h = ctypes.c_void_p()

@@ -33,8 +33,10 @@ def _run(nproc, backend, extra, timeout=600):
     return json.loads(line)
 
 
-@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"], ["--gp", "--steps", "6"]])
+@pytest.mark.parametrize("extra", [["--small", "--steps", "5"], ["--config", "2", "--steps", "3"],
+                                   ["--config", "2", "--steps", "3", "--exchange-chunks", "1"], ["--gp", "--steps", "6"]])
 def test_two_ranks_match_single_gpu(extra):
+    """[S | b] exchanged in 4 row chunks behind the Schur build (the async callback, default) or in one all-reduce."""
     out = _run(2, "gloo", extra)
     assert out["loss_rel"] < 1e-9, out
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
@@ -60,11 +62,13 @@ def test_config4_sharded_config3_scene(nproc):
 
 
 @pytest.mark.timeout(300)
-def test_rccl_exchange_one_rank():
-    """The RCCL ("nccl") branch of the exchange callback (engine.make_allreduce_callback) on a device tensor, ordered
-    on the library's stream: one rank with the callback forced on, so every all-reduce of the camera system runs
-    through RCCL; the result must equal the plain single-GPU run (a 1-rank sum is the identity)."""
-    out = _run(1, "nccl", ["--small", "--steps", "4", "--force-exchange"], timeout=280)
+@pytest.mark.parametrize("chunks", [4, 1])
+def test_rccl_exchange_one_rank(chunks):
+    """The RCCL ("nccl") branches of the exchange callbacks (engine.make_allreduce_callback and, with chunks > 1, the
+    asynchronous make_allreduce_async_callback on the library's exchange stream) on a device tensor: one rank with the
+    callbacks forced on, so every all-reduce of the camera system runs through RCCL; the result must equal the plain
+    single-GPU run (a 1-rank sum is the identity)."""
+    out = _run(1, "nccl", ["--small", "--steps", "4", "--force-exchange", "--exchange-chunks", str(chunks)], timeout=280)
     assert out["backend"] == "nccl" and out["world"] == 1
     assert out["exchange_calls"] >= 4 * 3, out  # per step: [U|g_c], [S|b] per trial, the 5 result scalars
     assert out["loss_rel"] < 1e-12 and out["cams_rel"] < 1e-12 and out["points_rel"] < 1e-12, out

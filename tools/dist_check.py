@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--gp", action="store_true", help="global positioning (insfm_gp) instead of BA")
     ap.add_argument("--force-exchange", action="store_true",
                     help="install the all-reduce callback even with one rank (drives the RCCL branch on one GPU)")
+    ap.add_argument("--exchange-chunks", type=int, default=4,
+                    help="row chunks of the [S | b] exchange behind the Schur build (1: one all-reduce after it)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -99,7 +101,7 @@ def main():
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
                          world_size=world, rank=rank, shard=shards[rank], deterministic=True,
-                         force_exchange=args.force_exchange)
+                         force_exchange=args.force_exchange, exchange_chunks=args.exchange_chunks)
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
     pts = torch.from_numpy(prob.points_init.copy()).to(dev)
     losses = []
