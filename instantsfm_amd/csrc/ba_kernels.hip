@@ -1239,6 +1239,42 @@ __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) 
     else if (t < 8) status[t - 4] = 0;
 }
 
+// After k_final (and the cross-rank sum): result[0..4] into host-mapped memory for the host's spin-wait, then
+// sequence word `seq` (system-scope release), so the host reads the trial's cost without a stream synchronization or a
+// copy launch.  With `cams_cur` set (insfm_ba_step: the caller's buffers hold the current parameters) the accepted
+// trial is copied there in the same launch; the test is lm_step's accept rule on the same doubles (not SPD -> fail;
+// last < loss with rejects left -> reject; otherwise accept), and the decision is published in pub[5] for the host to
+// check against its own.
+__global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__ result, double* pub, unsigned seq, double last,
+                                                      int can_reject, const double* __restrict__ cams_new,
+                                                      double* __restrict__ cams_cur, long long ncam,
+                                                      const double* __restrict__ pts_new, double* __restrict__ pts_cur,
+                                                      long long npts) {
+    const double loss = result[0];
+    const bool acc = result[4] == 0.0 && !(last < loss && can_reject);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        for (int k = 0; k < 5; ++k) pub[k] = result[k];
+        pub[5] = acc ? 1.0 : 0.0;
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<unsigned*>(pub + 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (!acc || cams_cur == nullptr) return;
+    const long long g = (long long)blockIdx.x * kThreads + threadIdx.x, G = (long long)gridDim.x * kThreads;
+    for (long long k = g; k < ncam; k += G) cams_cur[k] = cams_new[k];
+    // points: 16-byte pieces (both buffers 16-B aligned: allocations and the shard offset are whole points of 24 B,
+    // so the pair path is taken only when both pointers are)
+    const bool al = ((reinterpret_cast<uintptr_t>(pts_new) | reinterpret_cast<uintptr_t>(pts_cur)) & 15) == 0;
+    if (al) {
+        const long long n2 = npts / 2;
+        const double2* s2 = reinterpret_cast<const double2*>(pts_new);
+        double2* d2 = reinterpret_cast<double2*>(pts_cur);
+        for (long long k = g; k < n2; k += G) d2[k] = s2[k];
+        if (g == 0 && (npts & 1)) pts_cur[npts - 1] = pts_new[npts - 1];
+    } else {
+        for (long long k = g; k < npts; k += G) pts_cur[k] = pts_new[k];
+    }
+}
+
 inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace
@@ -1300,6 +1336,7 @@ struct insfm_ba {
     int cg_nwg = 0;
     double *cams_cur = nullptr, *cams_new = nullptr, *pts_cur = nullptr, *pts_new = nullptr;
     bool ext_cur = false;  // during insfm_ba_step: cams_cur / pts_cur are the caller's buffers
+    bool trial_copied = false;  // the last trial cost's k_publish copied the accepted trial into cams_cur / pts_cur
     double *part_cost = nullptr, *part_gp = nullptr, *part_gc = nullptr;
     int n_cost = 0, n_gp = 0, n_gc = 0;
     int n_gp_grp = 0;  // global positioning: k_gp_backsub blocks (kGPG lanes per track)
@@ -1307,6 +1344,9 @@ struct insfm_ba {
     int* flags = nullptr;
     double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
     int* prog_host = nullptr;    // pinned, device-mapped: progress of the two-level CG (CgBufs::prog)
+    double* pub_host = nullptr;  // pinned, device-mapped: k_publish's result[0..4], decision, sequence word (double 8)
+    double* pub_dev = nullptr;
+    unsigned pub_seq = 0;
     std::vector<void*> allocs;
     // LM state
     double damping = 0.0, down = 0.0, loss = 0.0;
@@ -1721,6 +1761,32 @@ int side_drain(insfm_ba* h) {
     return rc;
 }
 
+// Side-chain schedule.  0 (default): a lagged solve's chain is issued from the CG poll loop while the host waits
+// (E build and inversion overlap the CG).  1: the chain is deferred past the CG -- issued while the host waits for
+// the trial cost and, whatever remains, right after the next solve's k_schur is enqueued -- so it overlaps
+// back-substitution, the cost, the next linearization and k_schur instead of the CG.  The lag rule is the same in
+// both (the next solve's k_cg_scale / k_tl_basis wait for the E build; its CG waits for the factorization).
+// Measured on config 3: the CG gets 10 % faster under 1, linearization and k_schur slower by about as much
+// (INSFM_SIDE_SCHED=1 selects it).
+int side_sched() {
+    static const int v = [] { const char* e = std::getenv("INSFM_SIDE_SCHED"); return e ? std::atoi(e) : 0; }();
+    return v;
+}
+
+// Issue side units while the main stream is still busy (the host would otherwise only wait).
+int side_issue_while_busy(insfm_ba* h) {
+    int rc = 0;
+    while (h->side_slot >= 0 && hipStreamQuery(h->stream) == hipErrorNotReady && !(rc = side_issue(h))) {}
+    return rc;
+}
+
+// Everything of the side chain issued and finished (debug getters, kernel timing, destroy).
+int side_flush(insfm_ba* h) {
+    int rc = side_drain(h);
+    if (h->side) HIPCHK(hipStreamSynchronize(h->side));
+    return rc;
+}
+
 // Per-solve setup on the main stream: the basis, then this solve's side chain is queued (side_slot).  Under the lag
 // rule the CG runs with the previous solve's E^-1 and the chain is issued piecemeal from the CG's poll loop (the
 // host time of issuing it does not hold back the CG); a solve that needs its own E^-1 issues it here and waits.
@@ -1860,6 +1926,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
                 if (b1 > b0 && (rc = allreduce_async(h, h->S + b0 * D * D, (b1 - b0) * D * D))) return rc;
             }
+            if ((rc = side_drain(h))) return rc;  // the previous solve's deferred side chain (side_sched 1)
             if ((rc = allreduce_async(h, h->b, (int64_t)h->C * D))) return rc;
             HIPCHK(hipEventRecord(h->ev_xdone, h->xstream));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
@@ -1867,6 +1934,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         } else {
             rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
             if (rc) return rc;
+            if ((rc = side_drain(h))) return rc;  // the previous solve's deferred side chain (side_sched 1)
             rec(h, 7);
             rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
             if (rc) return rc;
@@ -1918,7 +1986,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             if ((rc = enqueue(0, enq))) return rc;
             CgPoll poll;
             poll.enq = enq;
-            poll.extra_ahead = h->side_slot >= 0 ? kSideAhead : 0;
+            poll.extra_ahead = (h->side_slot >= 0 && side_sched() == 0) ? kSideAhead : 0;
             static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
             int erc = 0;
             const int pr = cg_poll(
@@ -1933,7 +2001,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                     // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax.  While
                     // side units remain, two more CG iterations are kept queued: a side launch can hold the host
                     // for longer than two iterations take on the GPU
-                    if (h->side_slot >= 0) {
+                    if (h->side_slot >= 0 && side_sched() == 0) {
                         const double t0 = htrace ? wall_seconds() : 0.0;
                         const int r = side_issue(h);
                         if (htrace) { const double dt = wall_seconds() - t0; t_side += dt; m_side = std::max(m_side, dt); ++n_side; }
@@ -1947,7 +2015,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 },
                 &erc);
             const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
-            if (!erc) erc = side_drain(h);  // whatever the CG left unissued
+            if (!erc && side_sched() == 0) erc = side_drain(h);  // whatever the CG left unissued
             if (erc) return erc;
             if (htrace)
                 std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
@@ -2063,8 +2131,59 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     return iters;
 }
 
+// lm_step's accept rule for the trial being costed (k_publish copies an accepted trial into the caller's buffers)
+struct TrialAccept {
+    double last;     // the loss before the step
+    int can_reject;  // rejects < max_rejects
+};
+
+// The cost result to the host: k_publish into host-mapped memory and a spin on its sequence word (deferred side
+// units are issued while the GPU is still busy); without the mapped block, a copy and a stream synchronization.
+// Sets h->trial_copied when k_publish also copied an accepted trial (h->pub_host[5] holds its decision).
+int finish_cost(insfm_ba* h, const TrialAccept* ta) {
+    h->trial_copied = false;
+    if (!h->pub_host) {
+        HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
+        if (int rc = side_issue_while_busy(h)) return rc;
+        HIPCHK(hipStreamSynchronize(h->stream));
+        return 0;
+    }
+    if (++h->pub_seq == 0) h->pub_seq = 1;
+    const unsigned seq = h->pub_seq;
+    const bool copy = ta != nullptr && h->ext_cur && h->kind == 0;
+    const long long ncam = copy ? (long long)h->C * h->stride : 0, npts = copy ? (long long)h->Pl * 3 : 0;
+    const int grid = copy ? std::max(1, std::min(1024, cdiv(std::max(ncam, npts / 2 + 1), kThreads))) : 1;
+    k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->pub_dev, seq, ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
+                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
+    if (int rc = launch_err(h, "k_publish")) return rc;
+    if (int rc = side_issue_while_busy(h)) return rc;
+    const unsigned* w = reinterpret_cast<const unsigned*>(h->pub_host + 8);
+    for (unsigned n = 1;; ++n) {
+        if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) break;
+        if ((n & 255) == 0) {
+            const hipError_t q = hipStreamQuery(h->stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                h->err = std::string("cost: ") + hipGetErrorString(q);
+                return INSFM_BA_EHIP;
+            }
+            if (q == hipSuccess && __atomic_load_n(w, __ATOMIC_ACQUIRE) != seq) {
+                h->err = "cost: the stream drained without publishing the result";
+                return INSFM_BA_EHIP;
+            }
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    const volatile double* pv = h->pub_host;
+    for (int k = 0; k < 5; ++k) h->host_res[k] = pv[k];
+    h->trial_copied = copy;
+    return 0;
+}
+
 // cost at (cams, pts_local) -> h->result[0..1]; with gain partials when `gains` (after a solve).
-int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gains, const double* scl = nullptr) {
+int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gains, const double* scl = nullptr,
+             const TrialAccept* ta = nullptr) {
     if (h->kind == 1) {
         if (h->Nl > 0)
             k_gp_cost<<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, cams, pts_local, scl,
@@ -2076,9 +2195,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
         h->flags_dirty = false;
         rc = allreduce(h, h->result, 5);
         if (rc) return rc;
-        HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
-        HIPCHK(hipStreamSynchronize(h->stream));
-        return 0;
+        return finish_cost(h, nullptr);
     }
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
@@ -2093,9 +2210,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
     h->flags_dirty = false;
     rc = allreduce(h, h->result, 5);
     if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return 0;
+    return finish_cost(h, ta);
 }
 
 // One LM step on the parameters loaded into cams_cur / pts_cur (/ scl_cur): bae.optim.LM.step semantics (SURVEY.md
@@ -2123,7 +2238,8 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
         if (it < 0) return it;
         rec(h, 4);
-        if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new))) return rc;  // synchronizes
+        const TrialAccept ta{last, rejects < h->d.max_rejects ? 1 : 0};
+        if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new, &ta))) return rc;  // waits for the result
         rec(h, 5);
         if (h->timing) {
             (void)hipEventSynchronize(h->ev[5]);
@@ -2135,6 +2251,11 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
             acc_time(h, 3, 4, 3);
             acc_time(h, 4, 5, 4);
             rec(h, 1);  // the next trial starts here
+        }
+        if (h->trial_copied && (h->host_res[4] != 0.0 || (last < h->host_res[0] && rejects < h->d.max_rejects)) &&
+            h->pub_host[5] != 0.0) {  // (cannot happen: the same rule on the same doubles)
+            h->err = "k_publish accepted a trial the host rejects";
+            return INSFM_BA_EHIP;
         }
         if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
         pcg_last = it;
@@ -2153,7 +2274,12 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
             h->loss = last;
             continue;
         }
-        if (h->ext_cur) {  // the current parameters live in the caller's buffers: copy the accepted trial there
+        if (h->trial_copied) {  // k_publish already copied the accepted trial into the caller's buffers
+            if (h->pub_host[5] != 1.0) {
+                h->err = "accept decision of k_publish differs from the host's";
+                return INSFM_BA_EHIP;
+            }
+        } else if (h->ext_cur) {  // the current parameters live in the caller's buffers: copy the accepted trial there
             HIPCHK(hipMemcpyAsync(h->cams_cur, h->cams_new, sizeof(double) * (size_t)h->C * h->stride,
                                   hipMemcpyDeviceToDevice, h->stream));
             if (h->Pl)
@@ -2214,10 +2340,11 @@ const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() :
 
 void insfm_ba_destroy(insfm_ba* h) {
     if (!h) return;
-    if (h->side) (void)hipStreamSynchronize(h->side);
+    if (h->side) (void)side_flush(h);
     for (void* p : h->allocs) (void)hipFree(p);
     if (h->host_res) (void)hipHostFree(h->host_res);
     if (h->prog_host) (void)hipHostFree(h->prog_host);
+    if (h->pub_host) (void)hipHostFree(h->pub_host);
     for (auto& e : h->ev)
         if (e) (void)hipEventDestroy(e);
     if (h->side) {
@@ -2730,6 +2857,18 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     {
         hipError_t e = hipHostMalloc((void**)&h->host_res, 128, hipHostMallocDefault);
         if (e != hipSuccess) return fail(INSFM_BA_ENOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        // the published cost block (without it, or with a cross-rank sum installed, costs come back by copy + sync)
+        void* pm = nullptr;
+        if (hipHostMalloc(&pm, 16 * sizeof(double), hipHostMallocMapped) == hipSuccess) {
+            void* dp = nullptr;
+            if (hipHostGetDevicePointer(&dp, pm, 0) == hipSuccess) {
+                h->pub_host = static_cast<double*>(pm);
+                h->pub_dev = static_cast<double*>(dp);
+                std::memset(pm, 0, 16 * sizeof(double));
+            } else {
+                (void)hipHostFree(pm);
+            }
+        }
     }
     for (auto& e : h->ev) {
         hipError_t x = hipEventCreate(&e);
@@ -2917,9 +3056,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("two-level init: ") + hipGetErrorString(e));
-        const int DPd = D + (D & 1), CH = EROW_CH;
-        h->erow_lds = sizeof(double) * ((size_t)D * MC + (size_t)CH * D * DPd + 2 * (size_t)CH * D * MC +
-                                        (size_t)maxseg * MC * MC);
+        h->erow_lds = 0;  // (k_tl_erow's LDS is static: a few KB)
+        (void)maxseg;
         {
             const size_t fixed = sizeof(double) * ((size_t)MC * m + (size_t)m), budget = 144 * 1024;
             h->pc_rows = (int)std::min<size_t>((size_t)C, (budget - fixed) / (sizeof(double) * MC));
@@ -2929,8 +3067,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             return fail(INSFM_BA_EINVAL, "two-level preconditioner: scene too connected for the LDS budget (use precond 0)");
         with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
-            (void)hipFuncSetAttribute((const void*)k_tl_erow<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h->erow_lds);
             (void)hipFuncSetAttribute((const void*)k_tl_pc<DV>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->pc_lds);
             return 0;
@@ -3095,7 +3231,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
     if (which >= 2 && !h->tlon) return INSFM_BA_EINVAL;
-    if (h->side) HIPCHK(hipStreamSynchronize(h->side));  // its pending E build / factorization must not interleave
+    if (int rc0 = side_flush(h)) return rc0;  // its pending E build / factorization must not interleave
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
     int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
@@ -3171,7 +3307,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 16: case 17: src = h->Ebuf[which - 16]; n = h->tlon ? (size_t)h->tl.ldE * h->tl.ldE : 0; break;
         default: return INSFM_BA_EINVAL;
     }
-    if (h->side) HIPCHK(hipStreamSynchronize(h->side));
+    if (int rc0 = side_flush(h)) return rc0;
     if (n) HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return (int64_t)n;

@@ -125,90 +125,117 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
     if (k < D) tl.vc[(size_t)tl.cpos[i] * D + k] = r[k];
 }
 
-#ifndef EROW_CH
-#define EROW_CH 16
-#endif
+// One workgroup per camera row i (rows strided over the grid), its 4 waves taking the row's neighbour-cluster
+// segments round-robin.  Per segment c: A = sum over the segment's neighbours j (slot order) of S~_ij Z~_j (D x MC,
+// one output entry per lane and round, the block and Z~_j staged through the wave's own LDS slice), then
+// Oseg = [c == c_i] Z~_i^T Z~_i + Z~_i^T A (MC x MC).  The next block's loads are issued before the current block's
+// products, so each wave keeps one block in flight while it computes.  No workgroup-wide barrier after the start:
+// a wave's LDS slice is private and LDS operations of one wave complete in order.
 template <int D>
 struct ErowGeom {
     static constexpr int MC = D + 1;
     static constexpr int DP = D + (D & 1);
-    // neighbour blocks staged per round: small enough that a k_tl_erow workgroup (side stream) and a k_tl_pc
-    // workgroup (main stream, ~110 KB of LDS) fit one CU together -- with 32 blocks (59 KB) they did not, and the
-    // CG's k_tl_pc waited ~150 us per solve for the E build's workgroups to drain
-    static constexpr int CH = EROW_CH;
+    static constexpr int SB = D * DP, ZB = D * MC, MM = MC * MC;
+    static constexpr int NS = (SB + 63) / 64, NZ = (ZB + 63) / 64, NO = (MM + 63) / 64;
 };
 
-// One workgroup per camera row i: per neighbour cluster c, Oseg = [c == c_i] Z~_i^T Z~_i + sum over the row's
-// neighbours j in c (slot order) of Z~_i^T S~_ij Z~_j.  Neighbour blocks and Z~_j are staged in rounds of CH through
-// LDS; T = S~_ij Z~_j is formed once per block; each (segment, k, l) output is owned by one thread (fixed order).
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_tl_erow(int C, const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_j,
                                                       const double* __restrict__ Sn, TlBufs tl) {
     using G = ErowGeom<D>;
-    constexpr int MC = G::MC, DP = G::DP, CH = G::CH, MM = MC * MC;
-    extern __shared__ double lds[];
-    double* Zi = lds;                         // [D][MC]
-    double* Sb = Zi + D * MC;                 // [CH][D][DP]
-    double* Zj = Sb + CH * D * DP;            // [CH][D][MC]
-    double* T = Zj + CH * D * MC;             // [CH][D][MC]
-    double* acc = T + CH * D * MC;            // [nseg_row][MC][MC]
-    const int t = threadIdx.x;
-    // rows strided over the grid: the side stream's launch is capped at a few workgroups so it does not take the CUs'
-    // LDS from the CG launches it overlaps (k_tl_pc needs a large LDS slice per workgroup)
+    constexpr int MC = G::MC, DP = G::DP, SB = G::SB, ZB = G::ZB, MM = G::MM, NS = G::NS, NZ = G::NZ, NO = G::NO;
+    constexpr int NWV = kThreads / 64;
+    __shared__ __attribute__((aligned(16))) double Zi[ZB];         // Z~_i, a-major
+    __shared__ __attribute__((aligned(16))) double Sb[NWV][SB];    // the wave's current block, row-major (stride DP)
+    __shared__ __attribute__((aligned(16))) double Zs[NWV][ZB];    // Z~_j transposed: Zs[l * D + b] = Z~_j[b][l]
+    __shared__ __attribute__((aligned(16))) double As[NWV][ZB];    // the segment's A, a-major
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     for (int i = blockIdx.x; i < C; i += gridDim.x) {
-    __syncthreads();
-    const int n0 = nbr_ptr[i], n1 = nbr_ptr[i + 1];
-    const int s0 = tl.rseg_ptr[i], ns = tl.rseg_ptr[i + 1] - s0;
-    const int nout = ns * MM;
-    for (int e = t; e < D * MC; e += kThreads) Zi[e] = tl.Zt[(size_t)i * D * MC + e];
-    __syncthreads();
-    for (int o = t; o < nout; o += kThreads) {
-        const int4 sg = tl.seg[s0 + o / MM];
-        const int k = (o % MM) / MC, l = o % MC;
-        double v = 0.0;
-        if (sg.w) {
-#pragma unroll
-            for (int a = 0; a < D; ++a) v += Zi[a * MC + k] * Zi[a * MC + l];
-        }
-        acc[o] = v;
-    }
-    for (int q0 = n0; q0 < n1; q0 += CH) {
-        const int nq = min(CH, n1 - q0);
         __syncthreads();
-        for (int e = t; e < nq * D * DP; e += kThreads) {
-            const int q = e / (D * DP), r = e % (D * DP);
-            Sb[e] = Sn[(size_t)tl.sperm[q0 + q] * D * DP + r];
-        }
-        for (int e = t; e < nq * D * MC; e += kThreads) {
-            const int q = e / (D * MC), r = e % (D * MC);
-            Zj[e] = tl.Zt[(size_t)nbr_j[tl.sperm[q0 + q]] * D * MC + r];
-        }
+        for (int e = t; e < ZB; e += kThreads) Zi[e] = tl.Zt[(size_t)i * ZB + e];
         __syncthreads();
-        for (int e = t; e < nq * D * MC; e += kThreads) {
-            const int q = e / (D * MC), r = e % (D * MC), a = r / MC, l = r % MC;
-            const double* B = Sb + q * D * DP + a * DP;
-            const double* Z = Zj + q * D * MC + l;
-            double v = 0.0;
+        const int n0 = nbr_ptr[i];
+        const int s0 = tl.rseg_ptr[i], s1 = tl.rseg_ptr[i + 1];
+        for (int s = s0 + wv; s < s1; s += NWV) {
+            const int4 sg = tl.seg[s];
+            double acc[NZ];
 #pragma unroll
-            for (int b = 0; b < D; ++b) v += B[b] * Z[b * MC];
-            T[e] = v;
-        }
-        __syncthreads();
-        for (int o = t; o < nout; o += kThreads) {
-            const int4 sg = tl.seg[s0 + o / MM];
-            const int k = (o % MM) / MC, l = o % MC;
-            const int qa = max(sg.y, q0 - n0), qb = min(sg.z, q0 - n0 + nq);
-            double v = acc[o];
-            for (int q = qa; q < qb; ++q) {
-                const double* Tq = T + (q - (q0 - n0)) * D * MC + l;
+            for (int u = 0; u < NZ; ++u) acc[u] = 0.0;
+            double sv[NS], zv[NZ];
+            auto load = [&](int q) {
+                const int nb = tl.sperm[n0 + q];
+                const int j = nbr_j[nb];
 #pragma unroll
-                for (int a = 0; a < D; ++a) v += Zi[a * MC + k] * Tq[a * MC];
+                for (int u = 0; u < NS; ++u) sv[u] = Sn[(size_t)nb * SB + min(lane + 64 * u, SB - 1)];
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) zv[u] = tl.Zt[(size_t)j * ZB + min(lane + 64 * u, ZB - 1)];
+            };
+            if (sg.y < sg.z) load(sg.y);
+            for (int q = sg.y; q < sg.z; ++q) {
+#pragma unroll
+                for (int u = 0; u < NS; ++u) {
+                    const int e = lane + 64 * u;
+                    if (e < SB) Sb[wv][e] = sv[u];
+                }
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) {
+                    const int e = lane + 64 * u;
+                    if (e < ZB) Zs[wv][(e % MC) * D + e / MC] = zv[u];
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (q + 1 < sg.z) load(q + 1);
+#pragma unroll
+                for (int u = 0; u < NZ; ++u) {
+                    const int o = min(lane + 64 * u, ZB - 1), a = o / MC, l = o % MC;
+                    double v = 0.0;
+                    if constexpr ((D & 1) == 0) {  // 16-byte LDS reads (row a of the block, column l of Z~_j)
+                        const double2* sr = reinterpret_cast<const double2*>(&Sb[wv][a * DP]);
+                        const double2* zc = reinterpret_cast<const double2*>(&Zs[wv][l * D]);
+#pragma unroll
+                        for (int b = 0; b < D / 2; ++b) {
+                            const double2 x = sr[b], y = zc[b];
+                            v += x.x * y.x;
+                            v += x.y * y.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int b = 0; b < D; ++b) v += Sb[wv][a * DP + b] * Zs[wv][l * D + b];
+                    }
+                    acc[u] += v;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
-            acc[o] = v;
+#pragma unroll
+            for (int u = 0; u < NZ; ++u) {
+                const int e = lane + 64 * u;
+                if (e < ZB) As[wv][e] = acc[u];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int u = 0; u < NO; ++u) {
+                const int o = lane + 64 * u;
+                if (o < MM) {
+                    const int k = o / MC, l = o % MC;
+                    double v = 0.0;
+                    if (sg.w) {
+#pragma unroll
+                        for (int a = 0; a < D; ++a) v += Zi[a * MC + k] * Zi[a * MC + l];
+                    }
+#pragma unroll
+                    for (int a = 0; a < D; ++a) v += Zi[a * MC + k] * As[wv][a * MC + l];
+                    tl.Oseg[(size_t)s * MM + o] = v;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-    }
-    __syncthreads();
-    for (int o = t; o < nout; o += kThreads) tl.Oseg[(size_t)s0 * MM + o] = acc[o];
     }
 }
 

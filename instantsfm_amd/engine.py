@@ -105,15 +105,16 @@ class _LibraryStream:
 
     def __enter__(self):
         self.caller = torch.cuda.current_stream(self.lib.device)
-        if self.caller != self.lib:
+        self.ctx = None
+        if self.caller != self.lib:  # (the common case -- the library stream is already current -- costs one query)
             self.lib.wait_stream(self.caller)
-        self.ctx = torch.cuda.stream(self.lib)
-        self.ctx.__enter__()
+            self.ctx = torch.cuda.stream(self.lib)
+            self.ctx.__enter__()
         return self
 
     def __exit__(self, *exc):
-        self.ctx.__exit__(*exc)
-        if self.caller != self.lib:
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
             self.caller.wait_stream(self.lib)
         return False
 
