@@ -1762,9 +1762,9 @@ int side_drain(insfm_ba* h) {
 }
 
 // Side-chain schedule.  0 (default): a lagged solve's chain is issued from the CG poll loop while the host waits
-// (E build and inversion overlap the CG).  1: the chain is deferred past the CG -- issued while the host waits for
-// the trial cost and, whatever remains, right after the next solve's k_schur is enqueued -- so it overlaps
-// back-substitution, the cost, the next linearization and k_schur instead of the CG.  The lag rule is the same in
+// (E build and inversion overlap the CG); what the CG leaves unissued is issued while the host waits for the trial
+// cost, the rest right after the next solve's k_schur is enqueued.  1: nothing is issued from the poll loop -- the
+// whole chain overlaps back-substitution, the cost, the next linearization and k_schur instead of the CG.  The lag rule is the same in
 // both (the next solve's k_cg_scale / k_tl_basis wait for the E build; its CG waits for the factorization).
 // Measured on config 3: the CG gets 10 % faster under 1, linearization and k_schur slower by about as much
 // (INSFM_SIDE_SCHED=1 selects it).
@@ -1791,7 +1791,7 @@ int side_flush(insfm_ba* h) {
 // rule the CG runs with the previous solve's E^-1 and the chain is issued piecemeal from the CG's poll loop (the
 // host time of issuing it does not hold back the CG); a solve that needs its own E^-1 issues it here and waits.
 int run_tl_setup(insfm_ba* h, const double* cams) {
-    int rc = side_drain(h);  // (never pending here: every solve drains its chain before it returns)
+    int rc = side_drain(h);  // (normally already issued after the previous k_schur; see run_solve)
     if (rc) return rc;
     const int slot = (int)(h->tl_solves & 1);
     if ((rc = run_tl_basis(h, cams, h->stream))) return rc;
@@ -1926,7 +1926,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
                 if (b1 > b0 && (rc = allreduce_async(h, h->S + b0 * D * D, (b1 - b0) * D * D))) return rc;
             }
-            if ((rc = side_drain(h))) return rc;  // the previous solve's deferred side chain (side_sched 1)
+            if ((rc = side_drain(h))) return rc;  // what remains of the previous solve's side chain
             if ((rc = allreduce_async(h, h->b, (int64_t)h->C * D))) return rc;
             HIPCHK(hipEventRecord(h->ev_xdone, h->xstream));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
@@ -1934,7 +1934,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         } else {
             rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
             if (rc) return rc;
-            if ((rc = side_drain(h))) return rc;  // the previous solve's deferred side chain (side_sched 1)
+            if ((rc = side_drain(h))) return rc;  // what remains of the previous solve's side chain
             rec(h, 7);
             rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
             if (rc) return rc;
@@ -2014,8 +2014,10 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
 #endif
                 },
                 &erc);
+            // whatever the CG left unissued stays pending: it is issued while the GPU runs the back-substitution
+            // and cost (finish_cost), the rest after the next solve's k_schur is enqueued (run_solve) -- issuing it
+            // here would hold back k_cg_finish by the host time of every remaining launch
             const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
-            if (!erc && side_sched() == 0) erc = side_drain(h);  // whatever the CG left unissued
             if (erc) return erc;
             if (htrace)
                 std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
