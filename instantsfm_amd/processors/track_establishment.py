@@ -126,11 +126,16 @@ class TrackEngine:
         registered = np.array([bool(im.is_registered) for im in self.images] + [False])
         lo = TRACK_ESTABLISHMENT_OPTIONS['min_num_view_per_track']
         hi = TRACK_ESTABLISHMENT_OPTIONS['max_num_view_per_track']
+        # every image registered and every image index in range: the mask keeps every row, a plain copy is the same
+        all_reg = bool(registered[:-1].all())
+        if all_reg and tracks_full:
+            img = np.concatenate([o[:, 0] for o in tracks_full.values()])
+            all_reg = img.size == 0 or (int(img.min()) >= 0 and int(img.max()) < len(self.images))
         tracks = {}
         for track_id, track_obs in tracks_full.items():
             if track_obs.shape[0] < lo or track_obs.shape[0] > hi:
                 continue
             t = Track(id=track_id)
-            t.observations = track_obs[registered[track_obs[:, 0]]]
+            t.observations = track_obs.copy() if all_reg else track_obs[registered[track_obs[:, 0]]]
             tracks[track_id] = t
         return tracks

@@ -14,13 +14,38 @@ EPSILON = 1e-10
 
 
 def _gather_obs(tracks):
-    obs = [np.asarray(t.observations).reshape(-1, 2).astype(np.int64, copy=False) for t in tracks.values()]
-    if not obs:
+    """All observations of all tracks in dict order: (the per-track arrays, [X,2] int64, per-track counts, track row
+    of each observation).  One concatenation over the tracks' own arrays; tracks whose observations are not (n, 2)
+    arrays (lists, empty 1-D arrays) go through the per-track reshape."""
+    raw = [t.observations for t in tracks.values()]
+    if not raw:
         raise ValueError("need at least one array to concatenate")  # what the reference's np.concatenate raises
-    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
-    allobs = np.concatenate(obs)
+    try:
+        if not all(isinstance(o, np.ndarray) and o.ndim == 2 for o in raw):
+            raise ValueError
+        counts = np.fromiter((o.shape[0] for o in raw), dtype=np.int64, count=len(raw))
+        allobs = np.concatenate(raw).astype(np.int64, copy=False).reshape(-1, 2)
+        obs = raw
+    except ValueError:
+        obs = [np.asarray(o).reshape(-1, 2).astype(np.int64, copy=False) for o in raw]
+        counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+        allobs = np.concatenate(obs)
     trow = np.repeat(np.arange(len(obs), dtype=np.int64), counts)
     return obs, allobs, counts, trow, None, None
+
+
+def _apply_mask(tracks, valid, counts):
+    """track.observations = track.observations[mask] for every track (track_filter.py:62-63 / :107-110); a track whose
+    observations all pass keeps its array (the same values the reference's copy holds)."""
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    bad = np.concatenate([[0], np.cumsum(~valid)])
+    touched = np.flatnonzero(bad[starts[1:]] - bad[starts[:-1]] > 0)
+    if touched.size == 0:
+        return
+    vals = list(tracks.values())
+    for j in touched.tolist():
+        track = vals[j]
+        track.observations = track.observations[valid[starts[j]:starts[j + 1]]]
 
 
 def _gather(images, tracks):
@@ -40,7 +65,7 @@ def _world2cams(images):
 
 
 def _xyz(tracks):
-    return np.array([np.asarray(t.xyz, dtype=np.float64) for t in tracks.values()]).reshape(-1, 3)
+    return np.array([t.xyz for t in tracks.values()], dtype=np.float64).reshape(-1, 3)
 
 
 def quirk_counter(valid, counts):
@@ -58,9 +83,7 @@ def FilterTracksByReprojectionNormalized(cameras, images, tracks, max_reprojecti
     obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
     valid = passes.filter_reproj_normalized(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays,
                                             max_reprojection_error, device)
-    starts = np.concatenate([[0], np.cumsum(counts)])
-    for j, track in enumerate(tracks.values()):
-        track.observations = track.observations[valid[starts[j]:starts[j + 1]]]
+    _apply_mask(tracks, valid, counts)
     counter = quirk_counter(valid, counts)
     print(f'Filtered {counter} / {len(tracks)} tracks by reprojection error')
     return counter
@@ -85,9 +108,7 @@ def FilterTracksByReprojection(cameras, images, tracks, max_reprojection_error, 
     valid = passes.filter_reproj_pixel(allobs[:, 0], trow, foff[allobs[:, 0]] + allobs[:, 1], feats, img_cam,
                                        [cam.model_id.value for cam in cameras], [cam.params for cam in cameras],
                                        _world2cams(images), _xyz(tracks), max_reprojection_error, device)
-    starts = np.concatenate([[0], np.cumsum(counts)])
-    for j, track in enumerate(tracks.values()):
-        track.observations = track.observations[valid[starts[j]:starts[j + 1]]]
+    _apply_mask(tracks, valid, counts)
     counter = quirk_counter(valid, counts)
     print(f'Filtered {counter} / {len(tracks)} tracks by reprojection error')
     return counter
@@ -99,12 +120,13 @@ def FilterTracksByAngle(cameras, images, tracks, max_angle_error, device="cuda:0
     obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
     valid = passes.filter_angle(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays, thres, device)
     starts = np.concatenate([[0], np.cumsum(counts)])
-    counter = 0
-    for j, track in enumerate(tracks.values()):
-        v = valid[starts[j]:starts[j + 1]]
-        if not v.all():
-            counter += 1
-            track.observations = track.observations[np.flatnonzero(v)]
+    bad = np.concatenate([[0], np.cumsum(~valid)])
+    touched = np.flatnonzero(bad[starts[1:]] - bad[starts[:-1]] > 0)  # the tracks with a failing observation
+    counter = int(touched.size)
+    vals = list(tracks.values()) if counter else []
+    for j in touched.tolist():
+        track = vals[j]
+        track.observations = track.observations[np.flatnonzero(valid[starts[j]:starts[j + 1]])]
     print(f'Filtered {counter} / {len(tracks)} tracks by angle error')
     return tracks
 

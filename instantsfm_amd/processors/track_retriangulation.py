@@ -45,19 +45,20 @@ def complete_tracks(cameras, images, tracks, tracks_orig, TRIANGULATOR_OPTIONS, 
 
     keys = list(tracks.keys())
     track_id2idx = {track_id: idx for idx, track_id in enumerate(keys)}
-    cand, rows = [], []
+    cand, cidx = [], []
     for track_id, track_obs in tracks_orig.items():
         idx = track_id2idx.get(track_id)
         if idx is None:
             continue
-        o = np.asarray(track_obs).reshape(-1, 2)
-        cand.append(o)
-        rows.append(np.full(o.shape[0], idx, dtype=np.int32))
-    if not cand or sum(c.shape[0] for c in cand) == 0:
+        cand.append(track_obs if isinstance(track_obs, np.ndarray) and track_obs.ndim == 2
+                    else np.asarray(track_obs).reshape(-1, 2))
+        cidx.append(idx)
+    ccount = np.fromiter((c.shape[0] for c in cand), dtype=np.int64, count=len(cand))
+    if not cand or int(ccount.sum()) == 0:
         # the reference indexes obs_info_tensor[:, 0] of an empty 1-D tensor
         raise IndexError("too many indices for tensor of dimension 1")
-    obs_info = np.concatenate(cand).astype(np.int32)  # torch.tensor(..., dtype=torch.int32) (:61)
-    point_rows = np.concatenate(rows)
+    obs_info = np.concatenate(cand).astype(np.int32).reshape(-1, 2)  # torch.tensor(..., dtype=torch.int32) (:61)
+    point_rows = np.repeat(np.asarray(cidx, dtype=np.int32), ccount)
 
     feats, foff = _features(images)
     image_rows, image_pps = _image_rows(cameras, images, info['pp'])
@@ -72,11 +73,12 @@ def complete_tracks(cameras, images, tracks, tracks_orig, TRIANGULATOR_OPTIONS, 
         # the reference reads point_indices_tensor[0] of an empty tensor (:102)
         raise IndexError("index 0 is out of bounds for dimension 0 with size 0")
     split = np.flatnonzero(np.diff(point_rows)) + 1
-    bounds = np.concatenate([[0], split, [point_rows.shape[0]]])
+    bounds = np.concatenate([[0], split, [point_rows.shape[0]]]).tolist()
+    firsts = point_rows[np.asarray(bounds[:-1], dtype=np.int64)].tolist()
+    vals = list(tracks.values())
     num_completed = 0
-    for i in range(len(bounds) - 1):
-        a, b = int(bounds[i]), int(bounds[i + 1])
-        track = tracks[keys[int(point_rows[a])]]
+    for a, b, r in zip(bounds[:-1], bounds[1:], firsts):
+        track = vals[r]
         num_completed += abs((b - a) - track.observations.shape[0])
         track.observations = obs_info[a:b]
     return num_completed
