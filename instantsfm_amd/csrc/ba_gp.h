@@ -415,10 +415,26 @@ __global__ __launch_bounds__(kThreads) void k_gp_gather(int Nl, const int* __res
     if (o < Nl) dst[o] = src[osrc[o]];
 }
 
-__global__ __launch_bounds__(kThreads) void k_gp_scatter(int Nl, const int* __restrict__ osrc, const double* __restrict__ src,
-                                                         double* __restrict__ dst) {
-    const int o = blockIdx.x * kThreads + threadIdx.x;
-    if (o < Nl) dst[osrc[o]] = src[o];
+
+// insfm_gp_step's parameter exchange with the caller's buffers in one launch: positions (3C), the shard's points
+// (3Pl) and the per-observation scales (caller order <-> track order through osrc); `in` = 1 loads the LM state
+// from the caller, 0 writes it back.
+__global__ __launch_bounds__(kThreads) void k_gp_io(int in, long long n3c, double* __restrict__ pos, double* __restrict__ cams,
+                                                    long long n3p, double* __restrict__ upts, double* __restrict__ pts,
+                                                    long long nl, const int* __restrict__ osrc, double* __restrict__ uscl,
+                                                    double* __restrict__ scl) {
+    const long long tot = n3c + n3p + nl;
+    for (long long k = (long long)blockIdx.x * kThreads + threadIdx.x; k < tot; k += (long long)gridDim.x * kThreads) {
+        if (k < n3c) {
+            if (in) cams[k] = pos[k]; else pos[k] = cams[k];
+        } else if (k < n3c + n3p) {
+            const long long q = k - n3c;
+            if (in) pts[q] = upts[q]; else upts[q] = pts[q];
+        } else {
+            const long long o = k - n3c - n3p;
+            if (in) scl[o] = uscl[osrc[o]]; else uscl[osrc[o]] = scl[o];
+        }
+    }
 }
 
 }  // namespace insfm

@@ -3329,28 +3329,24 @@ int insfm_gp_create(const insfm_ba_desc* desc, const double* trans, const int32_
     return create_impl(desc, 1, trans, cam_idx, pt_idx, cam_factor, scale_free, stream, out);
 }
 
-static int gp_load(insfm_ba* h, const double* pos, const double* pts, const double* scales, double* scl_dst) {
-    HIPCHK(hipMemcpyAsync(h->cams_cur, pos, sizeof(double) * 3 * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
-    if (h->Pl)
-        HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * 3 * (size_t)h->Pl, hipMemcpyDeviceToDevice,
-                              h->stream));
-    if (h->Nl) k_gp_gather<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->osrc, scales, scl_dst);
-    return launch_err(h, "k_gp_gather");
+// Positions, the shard's points and the scales between the caller's buffers and the LM state (one k_gp_io launch).
+static int gp_io(insfm_ba* h, int in, const double* pos, const double* pts, const double* scales) {
+    const long long n3c = 3LL * h->C, n3p = 3LL * h->Pl, nl = h->Nl, tot = n3c + n3p + nl;
+    if (tot == 0) return 0;
+    const int grid = std::max(1, std::min(2048, cdiv(tot, kThreads)));
+    k_gp_io<<<grid, kThreads, 0, h->stream>>>(in, n3c, const_cast<double*>(pos), h->cams_cur, n3p,
+                                              const_cast<double*>(pts) + 3 * (size_t)h->p0, h->pts_cur, nl, h->osrc,
+                                              const_cast<double*>(scales), h->scl_cur);
+    return launch_err(h, "k_gp_io");
 }
 
 int insfm_gp_step(insfm_ba* h, double* pos, double* pts, double* scales, insfm_ba_stats* st) {
     if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
-    int rc = gp_load(h, pos, pts, scales, h->scl_cur);
+    int rc = gp_io(h, 1, pos, pts, scales);
     if (rc) return rc;
     if ((rc = lm_step(h, st))) return rc;
-    HIPCHK(hipMemcpyAsync(pos, h->cams_cur, sizeof(double) * 3 * (size_t)h->C, hipMemcpyDeviceToDevice, h->stream));
-    if (h->Pl)
-        HIPCHK(hipMemcpyAsync(pts + 3 * (size_t)h->p0, h->pts_cur, sizeof(double) * 3 * (size_t)h->Pl, hipMemcpyDeviceToDevice,
-                              h->stream));
-    if (h->Nl) k_gp_scatter<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->osrc, h->scl_cur, scales);
-    if ((rc = launch_err(h, "k_gp_scatter"))) return rc;
-    HIPCHK(hipStreamSynchronize(h->stream));
-    return INSFM_BA_OK;
+    // written back in stream order (no host wait: the step's loss is already on the host), like insfm_ba_step
+    return gp_io(h, 0, pos, pts, scales);
 }
 
 int insfm_gp_cost(insfm_ba* h, const double* pos, const double* pts, const double* scales, double* loss, double* rmse) {
@@ -3370,7 +3366,7 @@ int insfm_gp_cost(insfm_ba* h, const double* pos, const double* pts, const doubl
 int insfm_gp_debug_linearize(insfm_ba* h, const double* pos, const double* pts, const double* scales) {
     if (!h || !pos || !pts || !scales || h->kind != 1) return INSFM_BA_EINVAL;
     h->keep_S = 1;
-    int rc = gp_load(h, pos, pts, scales, h->scl_cur);
+    int rc = gp_io(h, 1, pos, pts, scales);
     if (rc) return rc;
     if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
     HIPCHK(hipStreamSynchronize(h->stream));
