@@ -61,25 +61,53 @@ __global__ __launch_bounds__(kThreads) void k_gp_lin(int Nl, const int* __restri
 }
 
 // One wave per camera: h_c -> U[c][0], g_c -> gc[c] (summed over ranks afterwards, like the BA's U / g_c).
+// Sum NV per-thread values over the workgroup (wave butterflies, then the waves' sums in wave order through LDS);
+// thread 0 gets the totals.
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NV]) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = wave_sum(v[k]);
+    if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) red[wv][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double t = red[0][k];
+            for (int w = 1; w < kWaves; ++w) t += red[w][k];
+            v[k] = t;
+        }
+}
+
+// One workgroup per camera (its observations strided over the workgroup, two records in flight per thread).
 __global__ __launch_bounds__(kThreads) void k_gp_lin_cams(int C, const int* __restrict__ cam_ptr, const int* __restrict__ cam_obs,
                                                           const double* __restrict__ gobs, double* __restrict__ U,
                                                           double* __restrict__ gc) {
-    const int c = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (c >= C) return;
-    double h = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    for (int e = cam_ptr[c] + lane; e < cam_ptr[c + 1]; e += 64) {
+    __shared__ double red[kWaves][4];
+    const int c = blockIdx.x;
+    double v[4] = {0.0, 0.0, 0.0, 0.0};  // h | g
+    const int e0 = cam_ptr[c], e1 = cam_ptr[c + 1];
+    for (int e = e0 + (int)threadIdx.x; e < e1; e += 2 * kThreads) {
+        const int e2 = e + kThreads;
         const double4* q = reinterpret_cast<const double4*>(gobs + (size_t)cam_obs[e] * kGO);
-        const double4 A = q[0], R = q[1];
-        h += A.w * A.w;
-        g0 -= A.w * R.x; g1 -= A.w * R.y; g2 -= A.w * R.z;
+        const double4* q2 = reinterpret_cast<const double4*>(gobs + (size_t)cam_obs[min(e2, e1 - 1)] * kGO);
+        const double4 A = q[0], R = q[1], A2 = q2[0], R2 = q2[1];
+        v[0] += A.w * A.w;
+        v[1] -= A.w * R.x; v[2] -= A.w * R.y; v[3] -= A.w * R.z;
+        if (e2 < e1) {
+            v[0] += A2.w * A2.w;
+            v[1] -= A2.w * R2.x; v[2] -= A2.w * R2.y; v[3] -= A2.w * R2.z;
+        }
     }
-    h = wave_sum(h); g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
-    if (lane == 0) {
+    block_sum<4>(v, red);
+    if (threadIdx.x == 0) {
         double* u = U + (size_t)c * 9;
-        u[0] = h;
+        u[0] = v[0];
 #pragma unroll
         for (int k = 1; k < 9; ++k) u[k] = 0.0;
-        gc[3 * (size_t)c] = g0; gc[3 * (size_t)c + 1] = g1; gc[3 * (size_t)c + 2] = g2;
+        gc[3 * (size_t)c] = v[1]; gc[3 * (size_t)c + 1] = v[2]; gc[3 * (size_t)c + 2] = v[3];
     }
 }
 
@@ -157,22 +185,28 @@ __global__ __launch_bounds__(kThreads) void k_gp_prep_cams(int C, const int* __r
                                                            const double* __restrict__ gobs, const double* __restrict__ U,
                                                            const double* __restrict__ gc, double f, double cmin, double cmax,
                                                            int add_diag, double* __restrict__ Up, double* __restrict__ gpc) {
-    const int c = blockIdx.x * kWaves + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (c >= C) return;
+    __shared__ double red[kWaves][9];
+    const int c = blockIdx.x;
     double v[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // packed sym U correction (6) | g correction (3)
-    for (int e = cam_ptr[c] + lane; e < cam_ptr[c + 1]; e += 64) {
-        const double4* q = reinterpret_cast<const double4*>(gobs + (size_t)cam_obs[e] * kGO);
-        const double4 A = q[0], R = q[1];
+    const int e0 = cam_ptr[c], e1 = cam_ptr[c + 1];
+    auto add = [&](const double4& A, const double4& R) {
         const double hss = gp_hss(A, R, f, cmin, cmax);
-        if (!(hss > 0.0)) continue;
+        if (!(hss > 0.0)) return;
         const double b = A.w, c2 = b * b / hss, cg = -b * (A.x * R.x + A.y * R.y + A.z * R.z) / hss;
         v[0] -= c2 * A.x * A.x; v[1] -= c2 * A.x * A.y; v[2] -= c2 * A.x * A.z;
         v[3] -= c2 * A.y * A.y; v[4] -= c2 * A.y * A.z; v[5] -= c2 * A.z * A.z;
         v[6] -= cg * A.x; v[7] -= cg * A.y; v[8] -= cg * A.z;
+    };
+    for (int e = e0 + (int)threadIdx.x; e < e1; e += 2 * kThreads) {
+        const int e2 = e + kThreads;
+        const double4* q = reinterpret_cast<const double4*>(gobs + (size_t)cam_obs[e] * kGO);
+        const double4* q2 = reinterpret_cast<const double4*>(gobs + (size_t)cam_obs[min(e2, e1 - 1)] * kGO);
+        const double4 A = q[0], R = q[1], A2 = q2[0], R2 = q2[1];
+        add(A, R);
+        if (e2 < e1) add(A2, R2);
     }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) v[k] = wave_sum(v[k]);
-    if (lane == 0) {
+    block_sum<9>(v, red);
+    if (threadIdx.x == 0) {
         const double d = add_diag ? clampd(U[(size_t)c * 9], cmin, cmax) * f : 0.0;
         double* u = Up + (size_t)c * 9;
         u[0] = d + v[0]; u[1] = v[1]; u[2] = v[2];

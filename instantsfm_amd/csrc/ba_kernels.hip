@@ -1634,7 +1634,7 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         if (h->Nl > 0)
             k_gp_lin<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, h->sfree,
                                                                        cams, pts_local, h->scl_cur, h->d.huber_delta, h->gobs);
-        k_gp_lin_cams<<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc);
+        k_gp_lin_cams<<<h->C, kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc);
         int rc = launch_err(h, "k_gp_lin");
         if (rc) return rc;
         return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
@@ -1903,7 +1903,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             k_gp_prep_points<kGPG><<<cdiv((long long)h->Pl * kGPG, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->gobs, f, h->d.clamp_min,
                                                                                h->d.clamp_max, h->W, h->V, h->gp, h->Vinv,
                                                                                h->y, h->VY, h->flags);
-        k_gp_prep_cams<<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
+        k_gp_prep_cams<<<h->C, kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
                                                                      h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->Up,
                                                                      h->gpc);
     } else if (h->Pl > 0)
