@@ -106,10 +106,12 @@ int insfm_ba_create(const insfm_ba_desc* desc, const double* obs_uv, const int32
 
 /* One LM step (bae.optim.LM.step semantics).  cam_params [C, 7+n_intr] ([t, q_xyzw, intrinsics without pp]) and
  * points [P,3] are DEVICE pointers, read at the start and updated in place at the end (on a multi-rank run each
- * rank updates only its shard's points).  `stats` may be NULL.  Blocks for one 64-byte device->host copy per trial.
+ * rank updates only its shard's points).  `stats` may be NULL.  Per trial the host waits for the trial cost (five
+ * scalars published into host-mapped memory by the last kernel of the trial, read by a spin on a sequence word).
  * The buffers are read in place as the step's linearization point (they must not be written by other work while the
- * step runs); an accepted trial is copied into them as the last work enqueued on the handle's stream (stream-ordered:
- * work queued after the call on that stream sees it; other streams or host reads synchronize with the stream first). */
+ * step runs); an accepted trial is copied into them by that same kernel, the last work enqueued on the handle's
+ * stream (stream-ordered: work queued after the call on that stream sees it; other streams or host reads
+ * synchronize with the stream first). */
 int insfm_ba_step(insfm_ba* h, double* cam_params, double* points, insfm_ba_stats* stats);
 
 /* Enable (1) / disable (0, default) the per-phase hipEvent timing reported in insfm_ba_stats.time_ms. */
@@ -148,7 +150,7 @@ int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);
 /* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */
 int64_t insfm_ba_nnzb(const insfm_ba* h);
 /* E^-1 of a dense SPD matrix (DEVICE pointers, row-major m x m, 1 <= m <= 4096) by the two-level preconditioner's
- * blocked Gauss-Jordan kernels (k_gj_pivot / k_gj_update), on `stream` (NULL: the default stream); blocks until done.
+ * blocked Gauss-Jordan kernels (k_gj_pinv0 / k_gj_step), on `stream` (NULL: the default stream); blocks until done.
  * Returns 1 when E is positive definite, 0 when a pivot was not positive (Einv is then meaningless), or a negative
  * code.  If us_per_inverse is non-NULL, the inversion is repeated `reps` times and the mean device time stored. */
 int insfm_ba_debug_spd_inverse(int32_t m, const double* E, double* Einv, void* stream, int32_t reps,

@@ -38,7 +38,9 @@ int insfm_gp_create(const insfm_ba_desc* desc, const double* trans, const int32_
                     const double* cam_factor, const int32_t* scale_free, void* stream, insfm_ba** out);
 
 /* One LM step.  positions [C,3], points [P,3], scales [N] (per observation, the caller's order): DEVICE pointers,
- * updated in place (multi-rank: this rank's points and their observations' scales only). */
+ * updated in place (multi-rank: this rank's points and their observations' scales only).  Loaded into the LM state
+ * and written back by one launch each on the handle's stream (stream-ordered like insfm_ba_step: no host wait after
+ * the write-back). */
 int insfm_gp_step(insfm_ba* h, double* positions, double* points, double* scales, insfm_ba_stats* stats);
 
 /* Robust loss and raw RMSE sqrt(sum ||r||^2 / N) at DEVICE parameters. */
