@@ -96,6 +96,11 @@ typedef struct {
 } insfm_ba_stats;
 
 /* Fill `desc` with the reference's defaults (TorchBA + BUNDLE_ADJUSTER_OPTIONS, config/colmap.py:47-54). */
+/* Provenance of this build: "src=<16 hex digits> arch=<gfx> flags=<hipcc flags>", the hash taken over the library's
+ * sources and headers by instantsfm_amd/build.py (the Python loader refuses a library whose hash differs from the
+ * tree it is loaded from). */
+const char* insfm_build_info(void);
+
 void insfm_ba_default_desc(insfm_ba_desc* desc);
 
 /* Create a solver.  obs_uv [N,2] f64, cam_idx [N] i32 (compacted camera row), pt_idx [N] i32 (compacted point row,

@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
 
 
 # exported symbols (every one declared in include/*.h)
-SYMBOLS = ("insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
+SYMBOLS = ("insfm_build_info", "insfm_ba_default_desc", "insfm_ba_create", "insfm_ba_step", "insfm_ba_cost", "insfm_ba_reset",
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
            "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters", "insfm_ba_debug_spd_inverse",
@@ -75,6 +75,27 @@ class BAError(RuntimeError):
         self.code = code
 
 
+def build_info(L=None):
+    """The provenance string the library was built with ("src=<hash> arch=... flags=...")."""
+    L = L or load()
+    L.insfm_build_info.argtypes = []
+    L.insfm_build_info.restype = ctypes.c_char_p
+    return L.insfm_build_info().decode()
+
+
+def _check_provenance(L, path):
+    """The in-tree library must have been built from the sources in this tree (instantsfm_amd/build.py hashes them):
+    a stale or foreign binary fails loudly instead of running unverified code."""
+    from . import build as _b
+    if not all(os.path.exists(p) for p in _b.SRCS + _b.HEADERS):
+        return  # (an installed copy without sources: nothing to compare against)
+    info = build_info(L)
+    want = _b.source_hash()
+    if f"src={want} " not in info + " ":
+        raise RuntimeError(f"{path} was built from other sources ({info}; this tree hashes to src={want}): "
+                           "rebuild it (python -c 'import __graft_entry__ as g; g.build()')")
+
+
 def load(path=None):
     """Load the HIP library (no GPU needed to load it).  Raises if it was not built.  ``INSFM_LIB`` names another
     build of the same library (tools/schur_variants.sh compiles kernel variants for timing)."""
@@ -85,6 +106,8 @@ def load(path=None):
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
     L = ctypes.CDLL(path)
+    if not os.environ.get("INSFM_LIB"):
+        _check_provenance(L, path)
     vp, dp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
     L.insfm_ba_default_desc.argtypes = [ctypes.POINTER(Desc)]
     L.insfm_ba_default_desc.restype = None

@@ -4,6 +4,7 @@ Each source compiles to its own object under build/ (rebuilt when it or any head
 produces instantsfm_amd/_lib/libinsfm_ba.so.
 """
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -21,6 +22,31 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-Wall"]
 
 def _obj(src):
     return os.path.join(OBJDIR, os.path.basename(src) + ".o")
+
+
+def source_hash():
+    """SHA-256 (first 16 hex digits) over the library's sources and headers (contents, in a fixed order) and the
+    compile flags / target: what insfm_build_info() reports, so a loaded library can be matched to the tree."""
+    h = hashlib.sha256()
+    for path in SRCS + HEADERS:
+        h.update(os.path.relpath(path, REPO).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    h.update(" ".join([ARCH, *FLAGS]).encode())
+    return h.hexdigest()[:16]
+
+
+def _build_info_src():
+    """A one-function source carrying the provenance string (regenerated when the hash changes)."""
+    info = f"src={source_hash()} arch={ARCH} flags={' '.join(FLAGS)}"
+    path = os.path.join(OBJDIR, "build_info.cpp")
+    text = ('extern "C" __attribute__((visibility("default"))) const char* insfm_build_info(void) '
+            f'{{ return "{info}"; }}\n')
+    old = open(path).read() if os.path.exists(path) else None
+    if old != text:
+        with open(path, "w") as f:
+            f.write(text)
+    return path
 
 
 def _stale(target, deps):
@@ -49,8 +75,13 @@ def build(force=False, verbose=True):
         if p.wait() != 0:
             raise subprocess.CalledProcessError(p.returncode, f"hipcc {obj}")
         os.replace(obj + ".tmp", obj)
-    if procs or force or _stale(OUT, [_obj(s) for s in SRCS]):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *[_obj(s) for s in SRCS]]
+    info_src = _build_info_src()
+    info_obj = info_src + ".o"
+    if force or _stale(info_obj, [info_src]):
+        subprocess.run([os.environ.get("CXX", "g++"), "-O2", "-fPIC", "-c", "-o", info_obj, info_src], check=True)
+    if procs or force or _stale(OUT, [_obj(s) for s in SRCS] + [info_obj]):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp", *[_obj(s) for s in SRCS],
+               info_obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

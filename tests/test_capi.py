@@ -126,3 +126,16 @@ def test_product_path_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 src = open(os.path.join(root, f)).read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", src).replace("oracle's", ""), f
+
+
+def test_library_built_from_this_tree(monkeypatch):
+    """insfm_build_info() carries the hash of the sources the library was compiled from (instantsfm_amd/build.py); the
+    loader compares it with the tree and refuses a stale or foreign binary."""
+    from instantsfm_amd import _capi
+    from instantsfm_amd import build as b
+    L = _capi.load()
+    info = _capi.build_info(L)
+    assert info.startswith(f"src={b.source_hash()} arch=gfx950"), info
+    monkeypatch.setattr(b, "source_hash", lambda: "0000000000000000")
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        _capi._check_provenance(L, _capi.LIB_PATH)
