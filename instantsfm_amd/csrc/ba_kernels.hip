@@ -2160,6 +2160,9 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     if (int rc = launch_err(h, "k_publish")) return rc;
     if (int rc = side_issue_while_busy(h)) return rc;
     const unsigned* w = reinterpret_cast<const unsigned*>(h->pub_host + 8);
+    // bounded like the CG poll: a device that neither publishes nor reports an error ends the step with EHIP
+    static const double stall_s = 6.0 * cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
+    const double t_wait = wall_seconds();
     for (unsigned n = 1;; ++n) {
         if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == seq) break;
         if ((n & 255) == 0) {
@@ -2170,6 +2173,11 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
             }
             if (q == hipSuccess && __atomic_load_n(w, __ATOMIC_ACQUIRE) != seq) {
                 h->err = "cost: the stream drained without publishing the result";
+                return INSFM_BA_EHIP;
+            }
+            if (wall_seconds() - t_wait > stall_s) {
+                h->err = "cost: no result from the device for " + std::to_string(stall_s) +
+                         " s (INSFM_CG_STALL_S scales the limit)";
                 return INSFM_BA_EHIP;
             }
         }
