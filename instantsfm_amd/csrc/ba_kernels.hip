@@ -610,20 +610,39 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
 // then forms column c of L^-1 by forward substitution, and r0 = L^-1 b, zero p/x/s.  Same operations in the same
 // order as the left-looking entry-wise loops (a[c] -= L[r][j] L[c][j] for j ascending, L[r][c] = s / L[c][c],
 // I[r][c] = -sum_k L[r][k] I[k][c] / L[r][r]).
+// U / g_c (`Ul` non-null): k_schur built S_ii and b_i without the camera terms (k_lin_cams ran beside it on another
+// stream), so they are added here -- S_ii += U_i with the diagonal clamped and scaled by the damping factor, b_i =
+// g_c + b_i, the same single additions k_schur makes -- and the completed block and right-hand side are written back.
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, const double* __restrict__ S,
-                                                        const double* __restrict__ b, double* __restrict__ Lf,
-                                                        double* __restrict__ Li, CgBufs cg) {
+__global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, double* __restrict__ S,
+                                                        double* __restrict__ b, double* __restrict__ Lf,
+                                                        double* __restrict__ Li, CgBufs cg, const double* __restrict__ Ul,
+                                                        const double* __restrict__ gcl, double f, double cmin, double cmax) {
     constexpr int DD = D * D;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = blockIdx.x * kWaves + wv;
     if (i >= C) return;
     const int rl = min(lane, D - 1);
-    const double* blk = S + (size_t)row_ptr[i] * DD;
+    double* blk = S + (size_t)row_ptr[i] * DD;
     double a[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) a[c] = blk[rl * D + c];
-    const double bl = b[(size_t)i * D + rl];
+    double bl = b[(size_t)i * D + rl];
+    if (Ul) {
+        const double* Ui = Ul + (size_t)i * DD + rl * D;
+#pragma unroll
+        for (int c = 0; c < D; ++c) {
+            double u = Ui[c];
+            if (c == rl) u = clampd(u, cmin, cmax) * f;
+            a[c] += u;
+        }
+        bl = gcl[(size_t)i * D + rl] + bl;
+        if (lane < D) {
+#pragma unroll
+            for (int c = 0; c < D; ++c) blk[rl * D + c] = a[c];
+            b[(size_t)i * D + rl] = bl;
+        }
+    }
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < D; ++j) {
@@ -1377,6 +1396,11 @@ struct insfm_ba {
     // chunked [S | b] exchange (desc.allreduce_async): work-item / row boundaries of the chunks, the exchange stream
     std::vector<int> xw, xr, rptr_host;
     hipStream_t xstream = nullptr;
+    // u_late: k_lin_cams runs on `aux` beside k_lin_points / k_schur; k_schur builds S / b without U / g_c and
+    // k_cg_factor adds them after waiting for ev_lc (lin_join).  Single-rank W-path only.
+    bool u_late = false, lin_pending = false;
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_lin0 = nullptr, ev_lc = nullptr;
     hipEvent_t ev_x = nullptr, ev_xdone = nullptr;
     bool built_pending = false;
     long long tl_solves = 0;
@@ -1627,6 +1651,14 @@ int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
 }
 
 // ---- phases --------------------------------------------------------------------------------------------------
+// The main stream waits for the camera linearization on `aux` (before anything reads U / g_c).
+int lin_join(insfm_ba* h) {
+    if (!h->lin_pending) return 0;
+    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_lc, 0));
+    h->lin_pending = false;
+    return 0;
+}
+
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     h->tl_fresh = true;
     h->cams_lin = cams;  // the re-deriving Schur evaluates the camera Jacobians at this linearization point
@@ -1639,9 +1671,33 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         if (rc) return rc;
         return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
     }
+    if (int rc0 = lin_join(h)) return rc0;  // (the previous linearization's U / g_c writes come first)
+    hipStream_t cst = h->aux;
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
+        // k_lin_cams (compute-bound) forks after k_lin_points (HBM-bound) so that it overlaps k_schur (bound by
+        // gather latency) instead of competing with k_lin_points for bandwidth
+        if (h->u_late && h->Pl > 0)
+            k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
+                                                                 cams, pts_local, h->d.huber_delta, h->W, h->V, h->gp,
+                                                                 nullptr);
+        if (h->u_late) {
+            HIPCHK(hipEventRecord(h->ev_lin0, h->stream));
+            HIPCHK(hipStreamWaitEvent(h->aux, h->ev_lin0, 0));
+            if constexpr (D <= 9) {
+                k_lin_cams_reg<M><<<h->C, LIN_CAMS_NT, 0, cst>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams, pts_local,
+                                                              h->d.huber_delta, h->U, h->gc);
+            } else {
+                const size_t lds = sizeof(double) * kThreads * (2 * D + 2);
+                k_lin_cams<M><<<h->C, kThreads, lds, cst>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams, pts_local,
+                                                            h->d.huber_delta, h->U, h->gc);
+            }
+            if (int e = launch_err(h, "k_lin_cams")) return e;
+            HIPCHK(hipEventRecord(h->ev_lc, h->aux));
+            h->lin_pending = true;
+            return launch_err(h, "k_lin_points");
+        }
         if (h->Pl > 0) {
             if (h->schur_rc)
                 k_lin_points<M, false><<<h->n_lin, kLinThreads, 0, h->stream>>>(
@@ -1897,7 +1953,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     const double* gcin = gpk ? h->gpc : h->gc;
     const double sf = gpk ? 1.0 : f;
     const double smin = gpk ? -1.0e308 : h->d.clamp_min, smax = gpk ? 1.0e308 : h->d.clamp_max;
-    const int sdiag = gpk ? 1 : (h->d.rank == 0);
+    const int sdiag = gpk ? 1 : (h->u_late ? 0 : (h->d.rank == 0));  // u_late: U / g_c added by k_cg_factor
     if (gpk) {
         if (h->Pl > 0)
             k_gp_prep_points<kGPG><<<cdiv((long long)h->Pl * kGPG, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->pt_ptr, h->gobs, f, h->d.clamp_min,
@@ -1943,9 +1999,13 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_built, 0));
             h->built_pending = false;
         }
+        if ((rc = lin_join(h))) return rc;
+        const bool ul = h->u_late && !gpk;
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
-            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg);
+            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
+                h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
+                h->d.clamp_min, h->d.clamp_max);
             k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
                                                                             h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
             return launch_err(h, "k_cg_factor/scale");
@@ -2104,6 +2164,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (rc) return rc;
         return iters;
     }
+    if (int rc0 = lin_join(h)) return rc0;  // the camera update reads U / g_c (points-only solves skip the factor)
     static const bool backsub_w_env = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
     const bool backsub_w = backsub_w_env && h->W != nullptr;
     int rc = backsub_w ? with_D(D, [&](auto dc_) -> int {
@@ -2238,6 +2299,7 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
     const double last = h->loss;
     rec(h, 0);
     if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
+    if (h->timing && (rc = lin_join(h))) return rc;  // (the phase split times both linearization kernels)
     rec(h, 1);
     double f = 1.0;
     int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
@@ -2365,6 +2427,12 @@ void insfm_ba_destroy(insfm_ba* h) {
         (void)hipStreamSynchronize(h->xstream);
         (void)hipStreamDestroy(h->xstream);
     }
+    if (h->aux) {
+        (void)hipStreamSynchronize(h->aux);
+        (void)hipStreamDestroy(h->aux);
+    }
+    if (h->ev_lin0) (void)hipEventDestroy(h->ev_lin0);
+    if (h->ev_lc) (void)hipEventDestroy(h->ev_lc);
     if (h->ev_x) (void)hipEventDestroy(h->ev_x);
     if (h->ev_xdone) (void)hipEventDestroy(h->ev_xdone);
     if (h->ev_E) (void)hipEventDestroy(h->ev_E);
@@ -2727,6 +2795,18 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             h->mf_pcap = std::max(pcap, 16);  // >= 16: the slot-0 quarters are summed in the staging area
             h->schur_mf_lds = lds;
             h->n_mf_work = (int)mfw.size();
+        }
+    }
+    // Camera linearization beside k_lin_points / k_schur (u_late), single rank on the W-reading Schur build.
+    // INSFM_U_LATE=0 keeps it on the main stream (U added inside k_schur).
+    {
+        static const bool env_on = [] { const char* e = std::getenv("INSFM_U_LATE"); return !e || std::atoi(e) != 0; }();
+        if (env_on && kind == 0 && desc->world_size <= 1 && !desc->allreduce && !h->schur_rc && !h->schur_mf) {
+            hipError_t e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lin0, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lc, hipEventDisableTiming);
+            if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("linearization stream: ") + hipGetErrorString(e));
+            h->u_late = true;
         }
     }
 
@@ -3172,6 +3252,7 @@ int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts)
         HIPCHK(hipMemcpyAsync(h->pts_cur, pts + 3 * (size_t)h->p0, sizeof(double) * (size_t)h->Pl * 3, hipMemcpyDeviceToDevice,
                               h->stream));
     int rc = run_linearize(h, h->cams_cur, h->pts_cur);
+    if (!rc) rc = lin_join(h);
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(h->stream));
     return 0;
@@ -3242,6 +3323,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
     if (which >= 2 && !h->tlon) return INSFM_BA_EINVAL;
     if (int rc0 = side_flush(h)) return rc0;  // its pending E build / factorization must not interleave
+    if (int rc0 = lin_join(h)) return rc0;
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
     int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
@@ -3318,6 +3400,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         default: return INSFM_BA_EINVAL;
     }
     if (int rc0 = side_flush(h)) return rc0;
+    if (int rc0 = lin_join(h)) return rc0;
     if (n) HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     return (int64_t)n;
