@@ -51,6 +51,14 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
                 + 8 * C * D * 8        # z, q, s, p, x, r, u, w written
                 + C * D * D * 8        # L_i (true-residual norm)
                 + 3 * C * 8 + C * (D + 1) * 8)  # row partials and restriction partials written
+    if kernel == "k_lin_points":
+        return (N * 2 * 8              # observed uv
+                + N * 4 * 2            # cam, ptl
+                + (P + 1) * 4          # pt_ptr
+                + C * (D + 1 + 2) * 8  # camera rows and principal points (each read once)
+                + P * 3 * 8            # points
+                + N * D * 3 * 8        # W written
+                + P * 9 * 8)           # V (6) + g_p (3) written
     raise ValueError(kernel)
 
 
@@ -716,6 +724,7 @@ def main():
     us_schur = eng.debug_time_kernel(1, 5)
     us_tl_iter = eng.debug_time_kernel(2, 50) if tl else None
     us_tl_setup = eng.debug_time_kernel(4, 10) if tl else None
+    us_lin = eng.debug_time_kernel(5, 20)
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
@@ -743,6 +752,21 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(nbytes), "launches_per_run": int(launches),
             "timing": "hipEvents on the library stream around 100 back-to-back launches (insfm_ba_debug_time_kernel)"}
+
+    # the next kernels by time per step, on the same footing (algorithmic bytes / hipEvent-timed launch)
+    others = []
+    for kname, us, nb in ((("k_tl_pspmv" if tl else "k_cg_iter"), us_cg,
+                           algorithmic_bytes("k_tl_pspmv" if tl else "k_cg_iter", C, Pl, Nl, D, nnzb)),
+                          ("k_lin_points", us_lin, algorithmic_bytes("k_lin_points", C, Pl, Nl, D, nnzb))):
+        if kname == name or not us:
+            continue
+        ach = nb / (us * 1e-6) / 1e9
+        others.append({"kernel": kname, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_us": round(us, 3),
+                       "algorithmic_bytes_per_launch": int(nb),
+                       "timing": "back-to-back launches (hipEvents): for k_lin_points that is the sustained rate of its "
+                                 "384-MB W write; in the step its trace time is shorter (profiles/r2_v6/kernel_stats.csv)"
+                                 if kname == "k_lin_points" else "back-to-back launches (hipEvents)"})
 
     out = {
         "metric": "LM-BA iterations/sec (+ final reprojection RMSE)",
@@ -772,9 +796,10 @@ def main():
                                    "cg_iterations"], ph)},
         "kernel_us": {("k_tl_pspmv" if tl else "k_cg_iter"): round(us_cg, 3), "k_schur": round(us_schur, 2),
                       "two_level_iteration": us_tl_iter and round(us_tl_iter, 3),
-                      "two_level_setup": us_tl_setup and round(us_tl_setup, 2)},
+                      "two_level_setup": us_tl_setup and round(us_tl_setup, 2), "k_lin_points": round(us_lin, 2)},
         "preconditioner": "two-level (block-Jacobi + camera-cluster similarity coarse space)" if tl else "block-Jacobi",
         "roofline": roof,
+        "roofline_next_kernels": others,
     }
     if rank == 0 and world == 1 and not args.no_solve:
         out["solve_end_to_end"] = solve_end_to_end(prob, dev)

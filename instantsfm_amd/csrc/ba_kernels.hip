@@ -3319,9 +3319,12 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     if (!h || reps <= 0 || !us_per_launch || !h->d.optimize_poses) return INSFM_BA_EINVAL;
     // re-run one kernel `reps` times back to back on the data of the last solve; the CG state it overwrites is
     // scratch once the solve has finished (dc already extracted).  0: k_cg_iter  1: k_schur (damping factor 1)
+    // 2: one two-level CG iteration  3: k_tl_pspmv  4: the two-level setup  5: k_lin_points (overwrites W / V / g_p)
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
-    if (which >= 2 && !h->tlon) return INSFM_BA_EINVAL;
+    if (which >= 2 && which <= 4 && !h->tlon) return INSFM_BA_EINVAL;
+    if (which == 5 && (h->kind != 0 || !h->W)) return INSFM_BA_EINVAL;
+    if (which < 0 || which > 5) return INSFM_BA_EINVAL;
     if (int rc0 = side_flush(h)) return rc0;  // its pending E build / factorization must not interleave
     if (int rc0 = lin_join(h)) return rc0;
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
@@ -3338,6 +3341,15 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 if (!rc2) rc2 = run_tl_build(h, 0, h->stream);
                 for (int u = 0; u <= gj_steps(h->tl.m) && !rc2; ++u) rc2 = run_tl_gj_unit(h, 0, u, h->stream);
                 if (rc2) return rc2;
+            } else if (which == 5 && h->kind == 0 && h->W) {  // k_lin_points at the last trial's parameters
+                with_model(h->model, [&](auto mc) -> int {
+                    constexpr int M = decltype(mc)::value;
+                    if (h->Pl > 0)
+                        k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(
+                            h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, h->cams_new, h->pts_new, h->d.huber_delta,
+                            h->W, h->V, h->gp, nullptr);
+                    return 0;
+                });
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                 h->Lf, h->cg, 0);
