@@ -28,9 +28,14 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     for track_id in short:                                                                      # :86-89
         del tracks[track_id]
     track_list = list(tracks.values())
-    obs = [np.asarray(t.observations, dtype=np.int64).reshape(-1, 2) for t in track_list]
-    counts = np.fromiter(map(len, obs), dtype=np.int64, count=len(obs))
-    obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
+    raw = [t.observations for t in track_list]
+    if raw and all(isinstance(o, np.ndarray) and o.ndim == 2 for o in raw):  # one concatenation over the arrays
+        counts = np.fromiter((o.shape[0] for o in raw), dtype=np.int64, count=len(raw))
+        obs = np.concatenate(raw).astype(np.int64, copy=False).reshape(-1, 2)
+    else:
+        obs = [np.asarray(o, dtype=np.int64).reshape(-1, 2) for o in raw]
+        counts = np.fromiter(map(len, obs), dtype=np.int64, count=len(obs))
+        obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
     image_used = np.zeros(len(images), dtype=bool)                                              # :91-99
     image_used[obs[:, 0]] = True  # the union over all tracks (the reference's early exit does not change it)
     for image_id, image in enumerate(images):
