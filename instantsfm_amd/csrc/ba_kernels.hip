@@ -696,10 +696,13 @@ __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __rest
     }
 }
 
-// One wave per upper block: S~_ij = L_i^-1 S_ij L_j^-T (diagonal blocks -> I).  Off-diagonal blocks are also
+// One wave per scale_nb(D) upper blocks: S~_ij = L_i^-1 S_ij L_j^-T (diagonal blocks -> I).  Off-diagonal blocks are also
 // written, padded to DP = D + (D & 1) columns, into the row-contiguous neighbour copy Sn: S~_ij at slot pos_up[e]
 // of row i and S~_ij^T at slot pos_lo[e] of row j, so the CG iteration reads every row's blocks as one
 // contiguous, 16-byte-coalesced stream.
+// Blocks per wave: their loads are issued together (one memory latency per NB blocks); fewer for large D so that the
+// staging (3 NB D^2 doubles per wave) leaves several workgroups per CU.
+__host__ __device__ constexpr int scale_nb(int D) { return D * D <= 64 ? 4 : (D * D <= 144 ? 2 : 1); }
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __restrict__ blk_row, const int* __restrict__ col,
                                                        const int* __restrict__ row_ptr, const int* __restrict__ pos_up,
@@ -707,57 +710,84 @@ __global__ __launch_bounds__(kThreads) void k_cg_scale(int nnzb, const int* __re
                                                        double* __restrict__ S, double* __restrict__ Sn, int keep_S) {
     constexpr int DD = D * D;
     constexpr int DP = D + (D & 1);
+    constexpr int NB = scale_nb(D);
+    constexpr int UL = (DD + 63) / 64;  // elements of a block per lane
     __shared__ double T[kWaves][DD];
-    __shared__ double Sb[kWaves][DD];
-    __shared__ double La[kWaves][DD];
-    __shared__ double Lb[kWaves][DD];
+    __shared__ double Sb[kWaves][NB][DD];
+    __shared__ double La[kWaves][NB][DD];
+    __shared__ double Lb[kWaves][NB][DD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int e = blockIdx.x * kWaves + wv;
-    if (e >= nnzb) return;
-    const int i = blk_row[e], j = col[e];
-    double* blk = S + (size_t)e * DD;
-    if (e == row_ptr[i]) {
-        if (keep_S)
-            for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
-        return;
+    const int e0 = (blockIdx.x * kWaves + wv) * NB;
+    if (e0 >= nnzb) return;
+    // every block of the wave and both factors' inverses staged together (all loads in flight at once; indices past
+    // the end clamped to the last block, whose products are then not stored)
+    int ei[NB], ii[NB], jj[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        ei[u] = min(e0 + u, nnzb - 1);
+        ii[u] = blk_row[ei[u]];
+        jj[u] = col[ei[u]];
     }
-    // the block and both factors' inverses staged together (every load in flight at once), the result kept in LDS for
-    // the transposed copy; same products in the same order as entry-wise loops over global memory
-    const double* Lii = Li + (size_t)i * DD;
-    const double* Ljj = Li + (size_t)j * DD;
-    for (int k = lane; k < DD; k += 64) {
-        Sb[wv][k] = blk[k];
-        La[wv][k] = Lii[k];
-        Lb[wv][k] = Ljj[k];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k = lane; k < DD; k += 64) {
-        const int a = k / D, bb = k % D;
-        double s = 0.0;
-        for (int m = 0; m <= a; ++m) s += La[wv][a * D + m] * Sb[wv][m * D + bb];
-        T[wv][k] = s;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    double* up = Sn + (size_t)pos_up[e] * D * DP;
-    double* lo = Sn + (size_t)pos_lo[e] * D * DP;
-    for (int k = lane; k < D * DP; k += 64) {
-        const int a = k / DP, bb = k % DP;
-        double v = 0.0;
-        if (bb < D) {
-            for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Lb[wv][bb * D + m];
-            if (keep_S) blk[a * D + bb] = v;  // the scaled upper S is only read by the debug getter
-            Sb[wv][a * D + bb] = v;
+    double sv[NB][UL], av[NB][UL], bv[NB][UL];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+#pragma unroll
+        for (int q = 0; q < UL; ++q) {
+            const int k = min(lane + 64 * q, DD - 1);
+            sv[u][q] = S[(size_t)ei[u] * DD + k];
+            av[u][q] = Li[(size_t)ii[u] * DD + k];
+            bv[u][q] = Li[(size_t)jj[u] * DD + k];
         }
-        up[k] = v;
-    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+#pragma unroll
+        for (int q = 0; q < UL; ++q) {
+            const int k = lane + 64 * q;
+            if (k < DD) { Sb[wv][u][k] = sv[u][q]; La[wv][u][k] = av[u][q]; Lb[wv][u][k] = bv[u][q]; }
+        }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // transpose: lo[a][bb] = S~_ij[bb][a]
-    for (int k = lane; k < D * DP; k += 64) {
-        const int a = k / DP, bb = k % DP;
-        lo[k] = (bb < D) ? Sb[wv][bb * D + a] : 0.0;
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const int e = e0 + u;
+        if (e >= nnzb) break;
+        const int i = ii[u];
+        double* blk = S + (size_t)e * DD;
+        if (e == row_ptr[i]) {
+            if (keep_S)
+                for (int k = lane; k < DD; k += 64) blk[k] = (k / D == k % D) ? 1.0 : 0.0;
+            continue;
+        }
+        // same products in the same order as entry-wise loops over global memory
+        for (int k = lane; k < DD; k += 64) {
+            const int a = k / D, bb = k % D;
+            double s = 0.0;
+            for (int m = 0; m <= a; ++m) s += La[wv][u][a * D + m] * Sb[wv][u][m * D + bb];
+            T[wv][k] = s;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        double* up = Sn + (size_t)pos_up[e] * D * DP;
+        double* lo = Sn + (size_t)pos_lo[e] * D * DP;
+        for (int k = lane; k < D * DP; k += 64) {
+            const int a = k / DP, bb = k % DP;
+            double v = 0.0;
+            if (bb < D) {
+                for (int m = 0; m <= bb; ++m) v += T[wv][a * D + m] * Lb[wv][u][bb * D + m];
+                if (keep_S) blk[a * D + bb] = v;  // the scaled upper S is only read by the debug getters
+                Sb[wv][u][a * D + bb] = v;
+            }
+            up[k] = v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        // transpose: lo[a][bb] = S~_ij[bb][a]
+        for (int k = lane; k < D * DP; k += 64) {
+            const int a = k / DP, bb = k % DP;
+            lo[k] = (bb < D) ? Sb[wv][u][bb * D + a] : 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
 }
 
@@ -2006,7 +2036,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
                 h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
                 h->d.clamp_min, h->d.clamp_max);
-            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
+            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
                                                                             h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
             return launch_err(h, "k_cg_factor/scale");
         });
