@@ -134,7 +134,10 @@ class OracleBA:
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().ora_destroy(self.h)
+            try:
+                lib().ora_destroy(self.h)
+            except TypeError:  # interpreter shutdown: the module globals are already gone
+                pass
             self.h = None
 
     def step(self, cams, pts):
