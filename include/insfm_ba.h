@@ -70,7 +70,9 @@ typedef struct {
     int32_t schur_variant; /* reduced-system build (BA, deterministic = 0): 0 (default) reads the stored camera-point
                               blocks W; 1 re-derives them per pair, LDS-atomic row accumulation; 2 re-derives them,
                               MFMA register accumulation (D <= 8, else 1).  1 and 2 never form W (no 192 B/obs write).
-                              The environment variable INSFM_SCHUR=w|rc|mf overrides it. */
+                              3 stores compact W records {J~p^T J~p, J~c,intr^T J~p} (96 B/obs for D = 8) and applies
+                              each camera's rotation and centre per block (any deterministic setting).
+                              The environment variable INSFM_SCHUR=w|rc|mf|cw overrides it. */
     insfm_ba_allreduce_async_fn allreduce_async; /* optional (see above); uses allreduce_ctx */
     int32_t exchange_chunks;  /* row chunks of the [S | b] exchange overlapped with the Schur build when allreduce_async
                                  is set (default 4; 1 = one all-reduce after the whole build) */

@@ -57,6 +57,17 @@ constexpr int kCostThreads = 256;  // k_cost workgroup size (64 / 128 / 512: sam
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
+#ifndef SCHUR_UP_C
+#define SCHUR_UP_C 5  // partners in flight per group with the compact W record (6 values per lane each)
+#endif
+#ifndef SCHUR_CW_VEC
+#define SCHUR_CW_VEC 0  // 1: compact records of even length read in 16-B pieces (measured: k_schur 556 -> 755 us)
+#endif
+#ifndef SCHUR_CW_TAB
+#define SCHUR_CW_TAB 1  // k_schur's row write-out: each block's column camera {R, c} formed once into LDS
+#endif
+// doubles per compact W record {H (6), Wi [ni][3]} for camera block dimension D = 6 + ni (see k_schur)
+__host__ __device__ constexpr int wrec_len(int D) { return 6 + 3 * (D - 6); }
 #ifndef SCHUR_RC_WAVES
 #define SCHUR_RC_WAVES 4  // waves per k_schur_rc workgroup
 #endif
@@ -114,7 +125,7 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // as one contiguous segment in k_schur); each track reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~.
 constexpr int kLinThreads = 128;  // k_lin_points workgroup (LDS: W staging + V/g terms of its observations)
 
-template <int M, bool STORE_W = true>
+template <int M, bool STORE_W = true, bool CW = false>
 __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
                                                          const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
@@ -128,7 +139,8 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
     // consecutive lanes (16 B per lane).  Each observation's V / g_p terms go to LDS and one thread per track adds them
     // in observation order -- the same sequence of additions as a thread walking its track.  The terms reuse the W
     // staging area once the records are stored (one 25.6-KB LDS buffer: 6 workgroups per CU instead of 4).
-    constexpr int D = kD<M>, ST = kStride<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride: no bank conflicts
+    // CW: the compact record {H, Wi} (wrec_len) instead of W_o [3][D]
+    constexpr int D = kD<M>, ST = kStride<M>, WR = CW ? wrec_len(D) : 3 * D, WRP = WR | 1;  // odd LDS row stride
     static_assert(WRP >= 9, "the V / g terms reuse a W staging row");
     __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here; then the V / g terms
     const int t = threadIdx.x;
@@ -155,19 +167,27 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
 #pragma unroll
             for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
-            if constexpr (STORE_W) {
-                double* Wo = wst + (size_t)t * WRP;
-#pragma unroll
-                for (int a = 0; a < D; ++a)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
-            }
             cv[0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
             cv[1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
             cv[2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
             cv[3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
             cv[4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
             cv[5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+            if constexpr (STORE_W && CW) {
+                double* Wo = wst + (size_t)t * WRP;
+#pragma unroll
+                for (int k = 0; k < 6; ++k) Wo[k] = cv[k];
+#pragma unroll
+                for (int a = 6; a < D; ++a)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) Wo[6 + 3 * (a - 6) + k] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+            } else if constexpr (STORE_W) {
+                double* Wo = wst + (size_t)t * WRP;
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+            }
 #pragma unroll
             for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
         }
@@ -462,7 +482,127 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
     }
 }
 
-template <int D, int WAVES, bool GPW = false>
+// ------------------------------------------------------------------------------------------------------------
+// Compact W record (BA, D = 6 + ni; the default): 96 B instead of 192 B per observation for D = 8.
+// With the pose tangent under left perturbation (ba_device.h) and R the camera's rotation matrix,
+//   J~p = A R,  J~c = [A | -A [p_c]x | J~c,intr],  p_c = R X + t = R (X - c),  c = -R^T t (camera centre), so
+//   W_o = J~c^T J~p = [R H ; R [X - c]x H ; Wi],  H = J~p^T J~p (3x3 symmetric),  Wi = J~c,intr^T J~p (ni x 3).
+// The record stores {H packed [xx xy xz yy yz zz], Wi [ni][3]}; every camera-dependent factor is applied where the
+// camera is known: the own observation's rows are rebuilt with camera i's R and the point (row of the workgroup), and
+// for a partner q on camera j the products against W_q^T factor as
+//   W^_o W_q^T = [T R_j^T | -(T [X - c_i]x + T [c_i - c_j]x) R_j^T | W^_o Wi_q^T],  T = W^_o H_q,
+// so k_schur accumulates A1 = sum T, A2 = sum T [X - c_i]x (the point is the own observation's, so X - c_i is fixed
+// over its partners) and A3 = sum W^_o Wi_q^T per block -- the same D x D slots and the same LDS adds as the full
+// record -- and applies R_j, c_j once per block when the row is written.  Assumes unit quaternions, like the analytic
+// pose Jacobian itself (dp_c/dphi = -[p_c]x holds only for a rotation).
+// ------------------------------------------------------------------------------------------------------------
+
+// Rotation matrix of a stored pose [t, q_xyzw] (the matrix eval_obs applies: I + 2w[q]x + 2[q]x^2) and the camera
+// centre c = -R^T t: out = {R row-major (9), c (3)}.
+__device__ __forceinline__ void pose_rc(const double* __restrict__ cam, double out[12]) {
+    const double qx = cam[3], qy = cam[4], qz = cam[5], qw = cam[6];
+    const double K[3][3] = {{0.0, -qz, qy}, {qz, 0.0, -qx}, {-qy, qx, 0.0}};
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const double kk = K[a][0] * K[0][b] + K[a][1] * K[1][b] + K[a][2] * K[2][b];
+            out[3 * a + b] = (a == b ? 1.0 : 0.0) + 2.0 * qw * K[a][b] + 2.0 * kk;
+        }
+#pragma unroll
+    for (int b = 0; b < 3; ++b) out[9 + b] = -(out[b] * cam[0] + out[3 + b] * cam[1] + out[6 + b] * cam[2]);
+}
+
+// Lane cb's view of compact record o: cb < 6 -> x = H (packed); cb >= 6 -> x = {row cb - 6 of Wi, 0, 0, 0}.  Every
+// lane then forms its column as v = H u (hmul) with a per-lane u: a Wi row comes out of the same product with u = e0.
+template <int D>
+__device__ __forceinline__ void load_crec(const double* __restrict__ W, int o, int cb, double x[6]) {
+    constexpr int R = wrec_len(D);
+    const int s = cb < 6 ? 0 : 6 + 3 * (cb - 6);  // first value of this lane's part of the record
+    if constexpr (SCHUR_CW_VEC && R % 2 == 0) {
+        // even record length: every record starts 16-B aligned, so the lane's values come in 16-B pieces from the
+        // aligned start at or below s (a Wi row at an odd offset takes the upper half of the first piece; the W
+        // allocation is padded so the last record's last piece stays inside it)
+        const double2* p = reinterpret_cast<const double2*>(W + (size_t)o * R + (s & ~1));
+        const double2 l0 = p[0], l1 = p[1];
+        const double2 l2 = cb < 6 ? p[2] : make_double2(0.0, 0.0);
+        if (cb < 6) {
+            x[0] = l0.x; x[1] = l0.y; x[2] = l1.x; x[3] = l1.y; x[4] = l2.x; x[5] = l2.y;
+        } else {
+            const bool odd = s & 1;
+            x[0] = odd ? l0.y : l0.x; x[1] = odd ? l1.x : l0.y; x[2] = odd ? l1.y : l1.x;
+            x[3] = 0.0; x[4] = 0.0; x[5] = 0.0;
+        }
+    } else {
+        const double* r = W + (size_t)o * R + s;
+        x[0] = r[0]; x[1] = r[1]; x[2] = r[2];
+        x[3] = 0.0; x[4] = 0.0; x[5] = 0.0;
+        if (cb < 6) { x[3] = r[3]; x[4] = r[4]; x[5] = r[5]; }
+    }
+}
+__device__ __forceinline__ void hmul(const double x[6], const double u[3], double& v0, double& v1, double& v2) {
+    v0 = x[0] * u[0] + x[1] * u[1] + x[2] * u[2];
+    v1 = x[1] * u[0] + x[3] * u[1] + x[4] * u[2];
+    v2 = x[2] * u[0] + x[4] * u[1] + x[5] * u[2];
+}
+// The per-lane vectors of one own observation (point X, row camera {R, c} in rc):
+//   own (row cb of W_o = (H uo)^T): cb < 3 -> row cb of R; cb 3..5 -> row k of R [d]x = R[k] x d; else e0;
+//   partner (column cb of the accumulated slot = W^_o H_q up):  cb < 3 -> e_cb;  cb 3..5 -> d x e_k;  else e0;
+// with d = X - c and k = cb - 3.
+__device__ __forceinline__ void crec_u(int cb, const double* rc, const double X[3], double uo[3], double up[3]) {
+    const double d0 = X[0] - rc[9], d1 = X[1] - rc[10], d2 = X[2] - rc[11];
+    uo[0] = 1.0; uo[1] = 0.0; uo[2] = 0.0;
+    up[0] = 1.0; up[1] = 0.0; up[2] = 0.0;
+    if (cb < 3) {
+        uo[0] = rc[3 * cb]; uo[1] = rc[3 * cb + 1]; uo[2] = rc[3 * cb + 2];
+        up[0] = cb == 0 ? 1.0 : 0.0; up[1] = cb == 1 ? 1.0 : 0.0; up[2] = cb == 2 ? 1.0 : 0.0;
+    } else if (cb < 6) {
+        const int k = cb - 3;
+        const double r0 = rc[3 * k], r1 = rc[3 * k + 1], r2 = rc[3 * k + 2];
+        uo[0] = r1 * d2 - r2 * d1; uo[1] = r2 * d0 - r0 * d2; uo[2] = r0 * d1 - r1 * d0;
+        // d x e_k
+        up[0] = k == 0 ? 0.0 : (k == 1 ? -d2 : d1);
+        up[1] = k == 0 ? d2 : (k == 1 ? 0.0 : -d0);
+        up[2] = k == 0 ? -d1 : (k == 1 ? d0 : 0.0);
+    }
+}
+// Entry (a, b) of the written block for column camera j from the accumulated slot row ab = acc row a (see above):
+// b < 3: A1_a . R_j[b];  b in 3..5: -(A2_a + A1_a x (c_i - c_j)) . R_j[b - 3];  else A3_a,b.
+__device__ __forceinline__ double crec_out(const double* ab, int b, const double* rj, const double* ci) {
+    if (b < 3) return ab[0] * rj[3 * b] + ab[1] * rj[3 * b + 1] + ab[2] * rj[3 * b + 2];
+    if (b < 6) {
+        const int k = b - 3;
+        const double e0 = ci[0] - rj[9], e1 = ci[1] - rj[10], e2 = ci[2] - rj[11];
+        const double s0 = ab[3] + (ab[1] * e2 - ab[2] * e1);
+        const double s1 = ab[4] + (ab[2] * e0 - ab[0] * e2);
+        const double s2 = ab[5] + (ab[0] * e1 - ab[1] * e0);
+        return -(s0 * rj[3 * k] + s1 * rj[3 * k + 1] + s2 * rj[3 * k + 2]);
+    }
+    return ab[b];
+}
+
+// Debug getter: the full W_o [3][D] of every observation rebuilt from its compact record (the own-row path of k_schur).
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_w_expand(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
+                                                       const double* __restrict__ camsl, const double* __restrict__ ptsl,
+                                                       const double* __restrict__ W, double* __restrict__ out) {
+    const int o = blockIdx.x * kThreads + threadIdx.x;
+    if (o >= Nl) return;
+    double rc[12];
+    pose_rc(camsl + (size_t)cam[o] * (D + 1), rc);
+    const double* xp = ptsl + 3 * (size_t)ptl[o];
+    const double X[3] = {xp[0], xp[1], xp[2]};
+    for (int cb = 0; cb < D; ++cb) {
+        double x[6], uo[3], up[3], w0, w1, w2;
+        load_crec<D>(W, o, cb, x);
+        crec_u(cb, rc, X, uo, up);
+        hmul(x, uo, w0, w1, w2);
+        double* wo = out + (size_t)o * 3 * D + cb;
+        wo[0] = w0; wo[D] = w1; wo[2 * D] = w2;
+    }
+}
+
+template <int D, int WAVES, bool GPW = false, bool CW = false>
 __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
@@ -472,23 +612,35 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                                                       const double* __restrict__ Vinv, const double* __restrict__ y,
                                                       const double* __restrict__ U, const double* __restrict__ gc, double f,
                                                       double cmin, double cmax, int add_diag, double* __restrict__ S,
-                                                      double* __restrict__ b) {
+                                                      double* __restrict__ b, const double* __restrict__ camsl = nullptr,
+                                                      const double* __restrict__ ptsl = nullptr) {
+    // CW: compact W records (see wrec_len); camsl / ptsl = cameras and points of the linearization
     constexpr int DD = D * D;
     constexpr int BS = schur_bs(D);  // LDS stride of an accumulated block (padded off the 64-bank period)
     constexpr int WS = schur_ws(D);  // LDS stride of a group's W^ staging
     constexpr int NG = 64 / D;  // observation groups per wave
     constexpr int NT = WAVES * 64;
+    constexpr int XN = CW ? 6 : 3;  // values per lane of a partner record
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int4 wk = work[blockIdx.x];
     const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
     double* acc = sh;
     double* wsh = acc + (size_t)nb * BS;           // [WAVES][NG][WS]  W^ rows ([D][4], padded group stride)
     double* bacc = wsh + (size_t)WAVES * NG * WS;  // [D]
-    int* slot = reinterpret_cast<int*>(bacc + D);  // [C]
+    double* rci = bacc + D;                        // [12] row camera {R, c} (CW)
+    int* slot = reinterpret_cast<int*>(rci + 12);  // [C]
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     for (int k = t; k < nb * BS; k += NT) acc[k] = 0.0;
     for (int k = t; k < C; k += NT) slot[k] = -1;
     if (t < D) bacc[t] = 0.0;
+    if constexpr (CW) {
+        if (t == 0) {
+            double rc[12];
+            pose_rc(camsl + (size_t)i * (D + 1), rc);
+#pragma unroll
+            for (int k = 0; k < 12; ++k) rci[k] = rc[k];
+        }
+    }
     __syncthreads();
     for (int e = kb + t; e < ke; e += NT) slot[col[e]] = e - kb;
     __syncthreads();
@@ -513,25 +665,42 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             const int en = e + WAVES * NG;
             if (active && en < oe) dnext = sdesc[en];
         }
-        constexpr int UP = SCHUR_UP;  // partners in flight per group
+        constexpr int UP = CW ? SCHUR_UP_C : SCHUR_UP;  // partners in flight per group
         const int qs = has ? dcur.z : 0, qe = has ? dcur.w : 0;
         const int n = qe - qs;
         // issue order = wait order (vmcnt retires in order): the own record first, then the first UP partner records,
         // so the W^ staging waits only for the own record while the partner loads stay in flight
         double w0 = 0.0, w1 = 0.0, w2 = 0.0, v00 = 0.0, v01 = 0.0, v02 = 0.0, v11 = 0.0, v12 = 0.0, v22 = 0.0;
+        double xo[XN];
+        double up[3] = {1.0, 0.0, 0.0};
+        double X[3] = {0.0, 0.0, 0.0};
         if (has) {
             const double* vi = Vinv + 6 * (size_t)dcur.y;
             v00 = vi[0]; v01 = vi[1]; v02 = vi[2]; v11 = vi[3]; v12 = vi[4]; v22 = vi[5];
-            load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
+            if constexpr (CW) {
+                load_crec<D>(W, dcur.x, cb, xo);
+                const double* xp = ptsl + 3 * (size_t)dcur.y;
+                X[0] = xp[0]; X[1] = xp[1]; X[2] = xp[2];
+            } else {
+                load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
+            }
         }
-        double x[UP][3];
+        double x[UP][XN];
         int cj[UP];
 #pragma unroll
         for (int u = 0; u < UP; ++u) {
             cj[u] = -1;
             if (u < n) {
-                load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
+                if constexpr (CW) load_crec<D>(W, qs + u, cb, x[u]);
+                else load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
                 cj[u] = cam[qs + u];
+            }
+        }
+        if constexpr (CW) {
+            if (has) {  // own row cb of W_o from the record, the row camera and the point
+                double uo[3];
+                crec_u(cb, rci, X, uo, up);
+                hmul(xo, uo, w0, w1, w2);
             }
         }
         if (has) {
@@ -565,7 +734,8 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     cj[u] = -1;
                     if (k0 + u < n) {
                         const int q = qs + k0 + u;
-                        load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
+                        if constexpr (CW) load_crec<D>(W, q, cb, x[u]);
+                        else load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
                         cj[u] = cam[q];
                     }
                 }
@@ -576,9 +746,12 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     const int sl = slot[cj[u]];
                     if (sl >= 0) {
                         double* dst = acc + (size_t)sl * BS + cb;
+                        double y0, y1, y2;
+                        if constexpr (CW) hmul(x[u], up, y0, y1, y2);
+                        else { y0 = x[u][0]; y1 = x[u][1]; y2 = x[u][2]; }
 #pragma unroll
                         for (int a2 = 0; a2 < D; ++a2)
-                            atomicAdd(dst + a2 * D, -(wh[a2][0] * x[u][0] + wh[a2][1] * x[u][1] + wh[a2][2] * x[u][2]));
+                            atomicAdd(dst + a2 * D, -(wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2));
                     }
                 }
             }
@@ -587,10 +760,40 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
     }
     if (diag_chunk && active) atomicAdd(bacc + cb, breg);
     __syncthreads();
+    // CW: the blocks' column cameras {R, c}, formed once per block into the (now free) W^ staging area when it fits
+    const bool ctab = CW && SCHUR_CW_TAB && nb * 12 <= WAVES * NG * WS;
+    if constexpr (CW) {
+        if (ctab) {
+            for (int bk = t; bk < nb; bk += NT) {
+                double rj[12];
+                pose_rc(camsl + (size_t)col[kb + bk] * (D + 1), rj);
+#pragma unroll
+                for (int q = 0; q < 12; ++q) wsh[12 * bk + q] = rj[q];
+            }
+            __syncthreads();
+        }
+    }
     double* Sout = S + (size_t)kb * DD;
     const double* Ui = U + (size_t)i * DD;
     for (int k = t; k < nb * DD; k += NT) {
-        double v = acc[(k / DD) * BS + k % DD];
+        double v;
+        if constexpr (CW) {  // camera j's rotation and centre applied to the block's accumulated [A1 | A2 | A3]
+            const int bk = k / DD, e2 = k - bk * DD, a2 = e2 / D, bb = e2 - a2 * D;
+            const double* ab = acc + (size_t)bk * BS + a2 * D;
+            if (bb < 6) {
+                if (ctab) {
+                    v = crec_out(ab, bb, wsh + 12 * bk, rci + 9);
+                } else {
+                    double rj[12];
+                    pose_rc(camsl + (size_t)col[kb + bk] * (D + 1), rj);
+                    v = crec_out(ab, bb, rj, rci + 9);
+                }
+            } else {
+                v = ab[bb];
+            }
+        } else {
+            v = acc[(k / DD) * BS + k % DD];
+        }
         if (diag_chunk && add_diag && k < DD) {
             const int a2 = k / D, bb = k % D;
             double u = Ui[k];
@@ -1366,6 +1569,8 @@ struct insfm_ba {
     double2* obrec = nullptr;
     double* ptrec = nullptr;
     const double* cams_lin = nullptr;  // camera rows of the last linearization (caller's or internal buffer)
+    const double* pts_lin = nullptr;   // its (local) points
+    bool w_compact = false;            // W holds the compact records {H, Wi} (wrec_len); INSFM_W_FULL=1: [3][D] records
     // MFMA-accumulating variant (ba_schur_mf.h, D <= 8): work items, batch-ordered own descriptors, staging positions
     bool schur_mf = false;
     MfWork* mf_work = nullptr;
@@ -1689,9 +1894,22 @@ int lin_join(insfm_ba* h) {
     return 0;
 }
 
+// k_lin_points writing W in the handle's record format (compact or [3][D]).
+template <int M>
+void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local) {
+    if (h->w_compact)
+        k_lin_points<M, true, true><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv,
+                                                                           h->pp, cams, pts_local, h->d.huber_delta, h->W,
+                                                                           h->V, h->gp, nullptr);
+    else
+        k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
+                                                             pts_local, h->d.huber_delta, h->W, h->V, h->gp, nullptr);
+}
+
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     h->tl_fresh = true;
     h->cams_lin = cams;  // the re-deriving Schur evaluates the camera Jacobians at this linearization point
+    h->pts_lin = pts_local;  // (and the compact-record Schur rebuilds the camera factors of W from both)
     if (h->kind == 1) {
         if (h->Nl > 0)
             k_gp_lin<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, h->sfree,
@@ -1708,10 +1926,7 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         constexpr int D = kD<M>;
         // k_lin_cams (compute-bound) forks after k_lin_points (HBM-bound) so that it overlaps k_schur (bound by
         // gather latency) instead of competing with k_lin_points for bandwidth
-        if (h->u_late && h->Pl > 0)
-            k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
-                                                                 cams, pts_local, h->d.huber_delta, h->W, h->V, h->gp,
-                                                                 nullptr);
+        if (h->u_late && h->Pl > 0) launch_lin_points_w<M>(h, cams, pts_local);
         if (h->u_late) {
             HIPCHK(hipEventRecord(h->ev_lin0, h->stream));
             HIPCHK(hipStreamWaitEvent(h->aux, h->ev_lin0, 0));
@@ -1734,9 +1949,7 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
                     h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, pts_local, h->d.huber_delta, nullptr, h->V,
                     h->gp, h->obrec);
             else
-                k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp,
-                                                                     cams, pts_local, h->d.huber_delta, h->W, h->V, h->gp,
-                                                                     nullptr);
+                launch_lin_points_w<M>(h, cams, pts_local);
         }
         static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
         if constexpr (D <= 9) {
@@ -1953,14 +2166,22 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (w1 <= w0) return 0;
-        if (det)
-            k_schur<DV, 1><<<w1 - w0, nt, h->schur_lds, h->stream>>>(
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(w1 - w0), dim3(nt), h->schur_lds, h->stream,
                 h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
-                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
-        else
-            k_schur<DV, kSchurWaves><<<w1 - w0, nt, h->schur_lds, h->stream>>>(
-                h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
-                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, h->cams_lin, h->pts_lin);
+        };
+        if constexpr (DV >= 7) {
+            if (h->w_compact) {
+                if (det) go(k_schur<DV, 1, false, true>);
+                else go(k_schur<DV, kSchurWaves, false, true>);
+                return launch_err(h, "k_schur");
+            }
+        }
+        {
+            if (det) go(k_schur<DV, 1>);
+            else go(k_schur<DV, kSchurWaves>);
+        }
         return launch_err(h, "k_schur");
     });
 }
@@ -2196,7 +2417,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     }
     if (int rc0 = lin_join(h)) return rc0;  // the camera update reads U / g_c (points-only solves skip the factor)
     static const bool backsub_w_env = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
-    const bool backsub_w = backsub_w_env && h->W != nullptr;
+    const bool backsub_w = backsub_w_env && h->W != nullptr && !h->w_compact;  // (reads [3][D] records)
     int rc = backsub_w ? with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         if (h->Pl > 0)
@@ -2681,7 +2902,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     tick("CG neighbour lists");
     // Schur work items: split long rows so a chunk fits the LDS budget
     const size_t wsh_lds = sizeof(double) * kSchurWaves * (64 / D) * schur_ws(D);  // W^ staging, up to kSchurWaves waves
-    const size_t fixed_lds = sizeof(double) * D + sizeof(int) * (size_t)C + wsh_lds + 64;
+    const size_t fixed_lds = sizeof(double) * (D + 12) + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
     const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * schur_bs(D)));
     std::vector<int4> work;
@@ -2724,7 +2945,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_xdone, hipEventDisableTiming);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("exchange stream: ") + hipGetErrorString(e));
     }
-    h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D) + wsh_lds + sizeof(int) * (size_t)C;
+    h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D + 12) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
     // Schur variant (INSFM_SCHUR): "w" (default) reads the stored W records (k_schur); "rc" re-derives the camera-point
     // blocks per pair and adds them with LDS atomics (ba_schur_rc.h); "mf" re-derives them and accumulates in MFMA
@@ -2732,7 +2953,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     // (LDS-atomic bound), mf 1.2-1.6 ms (latency / barrier bound); rc / mf save the 384-MB W write of k_lin_points.
     static const char* schur_env = std::getenv("INSFM_SCHUR");
     const std::string schur_kind = schur_env ? std::string(schur_env)
-                                             : (desc->schur_variant == 1 ? "rc" : (desc->schur_variant == 2 ? "mf" : "w"));
+                                             : (desc->schur_variant == 1 ? "rc"
+                                                : (desc->schur_variant == 2 ? "mf" : (desc->schur_variant == 3 ? "cw" : "w")));
     h->schur_rc = kind == 0 && !desc->deterministic && desc->optimize_poses && (schur_kind == "rc" || schur_kind == "mf");
     std::vector<int4> work_rc;
     if (h->schur_rc) {
@@ -2925,8 +3147,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = upload(h, &h->work_rc, work_rc.data(), work_rc.size()))) return fail(rc, "");
         if ((rc = dalloc(h, (void**)&h->obrec, sizeof(double2) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
         if ((rc = dd(&h->ptrec, (size_t)std::max(Pl, 1) * 12))) return fail(rc, "");
-    } else if ((rc = dd(&h->W, (size_t)Nl * D * 3))) {
-        return fail(rc, "");
+    } else {
+        // BA: [3][D] records, or the compact ones for schur_variant 3 ("cw")
+        h->w_compact = kind == 0 && D >= 7 && schur_kind == "cw";
+        // (+2: load_crec's 16-B pieces of the last record may reach one value past it)
+        if ((rc = dd(&h->W, (size_t)Nl * (h->w_compact ? wrec_len(D) : D * 3) + 2))) return fail(rc, "");
     }
     if ((rc = dd(&h->V, (size_t)Pl * 6))) return fail(rc, "");
     if ((rc = dd(&h->gp, (size_t)Pl * 3))) return fail(rc, "");
@@ -3018,6 +3243,12 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)h->schur_lds);
+        if constexpr (DV >= 7) {
+            (void)hipFuncSetAttribute((const void*)k_schur<DV, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)h->schur_lds);
+            (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves, false, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
+        }
         if constexpr (DV == 3) {
             (void)hipFuncSetAttribute((const void*)k_schur<3, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->schur_lds);
@@ -3374,10 +3605,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 5 && h->kind == 0 && h->W) {  // k_lin_points at the last trial's parameters
                 with_model(h->model, [&](auto mc) -> int {
                     constexpr int M = decltype(mc)::value;
-                    if (h->Pl > 0)
-                        k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(
-                            h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, h->cams_new, h->pts_new, h->d.huber_delta,
-                            h->W, h->V, h->gp, nullptr);
+                    if (h->Pl > 0) launch_lin_points_w<M>(h, h->cams_new, h->pts_new);
                     return 0;
                 });
             } else if (which == 0)
@@ -3419,6 +3647,25 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     switch (which) {
         case 0:
             if (!h->W) { h->err = "W is not formed by the re-deriving Schur (use deterministic = 1 or INSFM_SCHUR_W=1)"; return INSFM_BA_EINVAL; }
+            if (h->w_compact) {  // rebuilt as [3][D] records from the compact ones at the linearization point
+                n = Nl * D * 3;
+                if (n == 0) return 0;
+                double* tmp = nullptr;
+                HIPCHK(hipMalloc(&tmp, sizeof(double) * n));
+                int rc = with_D(h->D, [&](auto dc_) -> int {
+                    constexpr int DV = decltype(dc_)::value;
+                    if constexpr (DV >= 7)
+                        k_w_expand<DV><<<cdiv(Nl, kThreads), kThreads, 0, h->stream>>>(
+                            (int)Nl, h->cam, h->ptl, h->cams_lin, h->pts_lin, h->W, tmp);
+                    return launch_err(h, "k_w_expand");
+                });
+                hipError_t e = hipStreamSynchronize(h->stream);
+                if (!rc && e == hipSuccess) e = hipMemcpy(host, tmp, sizeof(double) * n, hipMemcpyDeviceToHost);
+                (void)hipFree(tmp);
+                if (rc) return rc;
+                if (e != hipSuccess) { h->err = hipGetErrorString(e); return INSFM_BA_EHIP; }
+                return (int64_t)n;
+            }
             src = h->W; n = Nl * D * 3; break;
         case 1: src = h->V; n = Pl * 6; break;
         case 2: src = h->gp; n = Pl * 3; break;

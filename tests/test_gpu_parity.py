@@ -376,16 +376,20 @@ def test_solver_failure_leaves_caller_buffers_unchanged():
     assert np.array_equal(co, prob.cams_init) and np.array_equal(po, prob.points_init)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("model", (0, 2, 4, 9))
 def test_schur_variant_solve_parity(model, variant):
-    """The re-deriving Schur builds (desc.schur_variant 1: LDS-atomic rows, 2: MFMA register accumulation for D <= 8;
-    D > 8 falls back to 1) against the oracle: b, S~, dc, dp at equal PCG iterations, same tolerances as
-    test_solve_parity.  They never form W, so the camera-point blocks are checked through S~."""
+    """The other Schur builds (desc.schur_variant 1: re-derived blocks, LDS-atomic rows, 2: re-derived, MFMA register
+    accumulation for D <= 8, D > 8 falls back to 1; 3: compact W records with the camera factors applied per block)
+    against the oracle: b, S~, dc, dp at equal PCG iterations, same tolerances as test_solve_parity.  1 and 2 never
+    form W, so the camera-point blocks are checked through S~; 3's records are rebuilt into W_o and checked too."""
     prob = make_problem(30, 800, seed=5, model=model)
     eng, ora = engines(prob, schur_variant=variant)
     eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
     ora.linearize(prob.cams_init, prob.points_init)
+    if variant == 3:
+        N, D = prob.n_obs, eng.D
+        assert rel(eng.debug_get(0, (N, 3, D)).transpose(0, 2, 1), ora.get(O.W)) < 1e-12
     f = 1.0 + 1e-4
     assert eng.debug_solve(f) == ora.solve(f)
     C, P, D = prob.n_cams, prob.n_points, eng.D
@@ -396,7 +400,7 @@ def test_schur_variant_solve_parity(model, variant):
     assert rel(eng.debug_get(8, (P, 3)), ora.get(O.DP)) < 1e-8
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_schur_variant_step_parity(variant):
     """Config 2 LM steps with the re-deriving Schur builds: same trials / PCG iterations as the oracle, parameters
     1e-9 (long rows: more than 64 upper blocks split into several work items)."""
