@@ -43,6 +43,10 @@ using namespace insfm;
 namespace {
 
 constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgroup
+#ifndef SCHUR_LDS_KB
+#define SCHUR_LDS_KB 96  // k_schur row-chunk LDS target (rows with more upper blocks are split into chunks)
+#endif
+constexpr int kLdsTarget = SCHUR_LDS_KB * 1024;
 #ifndef INSFM_SCHUR_WAVES
 #define INSFM_SCHUR_WAVES 8
 #endif
@@ -2904,7 +2908,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     const size_t wsh_lds = sizeof(double) * kSchurWaves * (64 / D) * schur_ws(D);  // W^ staging, up to kSchurWaves waves
     const size_t fixed_lds = sizeof(double) * (D + 12) + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
-    const int cap = (int)((kLdsBudget - fixed_lds) / (sizeof(double) * schur_bs(D)));
+    // chunk target: kLdsTarget when at least 8 blocks fit under it, else the hard budget
+    const size_t tgt = (size_t)kLdsTarget >= fixed_lds + 8 * sizeof(double) * schur_bs(D) ? (size_t)kLdsTarget
+                                                                                         : (size_t)kLdsBudget;
+    const int cap = (int)((tgt - fixed_lds) / (sizeof(double) * schur_bs(D)));
     std::vector<int4> work;
     int maxc = 1;
     for (int i = 0; i < C; ++i) {
