@@ -27,10 +27,17 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def w_record_doubles(D):
+    """Doubles per stored W record: [3][D], or the compact {H, Wi} record under INSFM_SCHUR=cw."""
+    return 6 + 3 * (D - 6) if os.environ.get("INSFM_SCHUR") == "cw" else 3 * D
+
+
 def algorithmic_bytes(kernel, C, P, N, D, nnzb):
     """Compulsory HBM bytes of one launch (every input byte read once, every output byte written once)."""
     if kernel == "k_schur":
-        return (N * D * 3 * 8          # W_o
+        cw = os.environ.get("INSFM_SCHUR") == "cw"
+        return (N * w_record_doubles(D) * 8  # W_o records
+                + (P * 3 * 8 + C * (D + 1) * 8 if cw else 0)  # points and camera rows (compact records)
                 + N * 4 * 3            # cam_obs, ptl, cam
                 + (P + 1) * 4          # pt_ptr
                 + P * 9 * 8            # V^-1 (6) + y (3)
@@ -57,7 +64,7 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
                 + (P + 1) * 4          # pt_ptr
                 + C * (D + 1 + 2) * 8  # camera rows and principal points (each read once)
                 + P * 3 * 8            # points
-                + N * D * 3 * 8        # W written
+                + N * w_record_doubles(D) * 8  # W records written
                 + P * 9 * 8)           # V (6) + g_p (3) written
     raise ValueError(kernel)
 
