@@ -54,7 +54,10 @@ constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (
 #ifndef LIN_CAMS_NT
 #define LIN_CAMS_NT 128  // k_lin_cams_reg threads per camera (measured 128 / 192 / 256 / 320: 0.156 / 0.161 / 0.167 / 0.194 ms linearize)
 #endif
-constexpr int kCostThreads = 256;  // k_cost workgroup size (64 / 128 / 512: same time, 25-26 us)
+#ifndef COST_THREADS
+#define COST_THREADS 256
+#endif
+constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 / 512: same time, 25-26 us; 1024: trial cost 0.045 -> 0.055 ms)
 #ifndef SCHUR_MINW
 #define SCHUR_MINW 1  // k_schur launch bound: minimum waves per SIMD (caps VGPRs: 4 -> 128)
 #endif
