@@ -731,10 +731,9 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                 wh[a2][2] = my_wh[a2 * 4 + 2];
             }
         }
-        int nmax = n;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-        for (int k0 = 0; k0 < nmax; k0 += UP) {
+        // rounds while any lane of the wave has partners left: a ballot (scalar compare) instead of a shuffle max of n,
+        // which cost six ds_bpermute per own-observation round on the LDS pipe the accumulation already saturates
+        for (int k0 = 0; __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
             if (k0 > 0) {
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
