@@ -225,10 +225,8 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur_rc(const int4* __restrict_
                 if (m == a) { v0 = Jc[0][m]; v1 = Jc[1][m]; }
             Jr[0][k] = v0; Jr[1][k] = v1;
         }
-        int nmax = n;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off, 64));
-        for (int k0 = 0; k0 < nmax; k0 += UP) {
+        // rounds while any lane has partners left (ballot: no ds_bpermute on the LDS pipe, as in k_schur)
+        for (int k0 = 0; __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
             if (k0 > 0) {  // tracks longer than UP + 1 observations: the next batch of partners
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
