@@ -2107,7 +2107,11 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
     h->side_slot = slot;
     h->side_next = 0;
     if (use == slot && (rc = side_drain(h))) return rc;
-    HIPCHK(hipStreamWaitEvent(h->stream, h->ev_fact[use], 0));
+    // a lagged solve's coarse inverse normally finished long ago: a completed event needs no wait marker in the main
+    // queue (each one idles it a few us); INSFM_FACT_WAIT=1 always queues the wait
+    static const bool always_wait = [] { const char* e = std::getenv("INSFM_FACT_WAIT"); return e && std::atoi(e) != 0; }();
+    if (always_wait || use == slot || hipEventQuery(h->ev_fact[use]) != hipSuccess)
+        HIPCHK(hipStreamWaitEvent(h->stream, h->ev_fact[use], 0));
     h->tl.Einv = h->Einvbuf[use];
     h->tl.ok = h->okbuf + use;
     ++h->tl_solves;
