@@ -25,14 +25,15 @@ def _obj(src):
 
 
 def source_hash():
-    """SHA-256 (first 16 hex digits) over the library's sources and headers (contents, in a fixed order) and the
-    compile flags / target: what insfm_build_info() reports, so a loaded library can be matched to the tree."""
+    """SHA-256 (first 16 hex digits) over the library's sources and headers (contents, in a fixed order): the `src=`
+    field of insfm_build_info(), so a loaded library can be matched to the tree.  The target and flags it was built
+    with are reported beside it (arch=, flags=) but not hashed: the load-time check compares sources only, so an
+    environment that sets PYTORCH_ROCM_ARCH differently at load time does not reject an unchanged build."""
     h = hashlib.sha256()
     for path in SRCS + HEADERS:
         h.update(os.path.relpath(path, REPO).encode())
         with open(path, "rb") as f:
             h.update(f.read())
-    h.update(" ".join([ARCH, *FLAGS]).encode())
     return h.hexdigest()[:16]
 
 

@@ -72,13 +72,14 @@ def SolveGlobalMapper(view_graph, cameras, images, config, depths=None, visualiz
         gp_engine = TorchGP(visualizer=visualizer, device=device)
         gp_engine.InitializeRandomPositions(cameras, images, tracks, depths)
         gp_engine.Optimize(cameras, images, tracks, depths, config.GLOBAL_POSITIONER_OPTIONS, progress=progress)
-        trace.append(('gp', len(tracks), _n_obs(tracks), gp_engine.loss_history[-1]))
+        trace.append(('gp', len(tracks), _n_obs(tracks),
+                      gp_engine.loss_history[-1] if gp_engine.loss_history else None))
         tracks = FilterTracksByAngle(cameras, images, tracks, config.INLIER_THRESHOLD_OPTIONS['max_angle_error'],
                                      device=device)
         NormalizeReconstruction(images, tracks, depths)
         trace.append(('gp_filtered', len(tracks), _n_obs(tracks), None))
         T['global_positioning_s'] = time.time() - start_time
-        T['gp'] = dict(gp_engine.timings, final_loss=gp_engine.final_loss)
+        T['gp'] = dict(gp_engine.timings, final_loss=getattr(gp_engine, 'final_loss', None))
         print('Global positioning took: ', T['global_positioning_s'])
 
     if not config.OPTIONS['skip_bundle_adjustment']:                                            # :109-126

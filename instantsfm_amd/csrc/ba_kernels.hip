@@ -1643,6 +1643,7 @@ struct insfm_ba {
     hipStream_t aux = nullptr;
     hipEvent_t ev_lin0 = nullptr, ev_lc = nullptr;
     hipEvent_t ev_x = nullptr, ev_xdone = nullptr;
+    hipEvent_t ev_pre = nullptr;  // multi-rank: recorded in front of the CG (its stall deadline starts after it)
     bool built_pending = false;
     long long tl_solves = 0;
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
@@ -2301,6 +2302,10 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 return r;
             };
             rec(h, 8);
+            // multi-rank: the CG's first launch waits for the exchange (the slowest peer); the stall deadline starts
+            // once everything queued in front of the CG has completed (ev_pre)
+            const bool gated = h->d.world_size > 1 || h->d.allreduce;
+            if (gated) HIPCHK(hipEventRecord(h->ev_pre, h->stream));
             // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step);
             // the loop below tops up one iteration at a time
             int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
@@ -2334,7 +2339,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                     __builtin_ia32_pause();
 #endif
                 },
-                &erc);
+                [&] { return !gated || hipEventQuery(h->ev_pre) != hipErrorNotReady; }, &erc);
             // whatever the CG left unissued stays pending: it is issued while the GPU runs the back-substitution
             // and cost (finish_cost), the rest after the next solve's k_schur is enqueued (run_solve) -- issuing it
             // here would hold back k_cg_finish by the host time of every remaining launch
@@ -2657,7 +2662,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->deterministic = 0;
     d->huber_delta = 1.0;
     d->tr_radius = 1e4; d->tr_max = 1e10; d->tr_min = 1e-6; d->tr_up = 2.0; d->tr_down = 1.0 / 16.0;
-    d->tr_factor = 0.5; d->tr_high = 0.5; d->tr_low = 1e-3;
+    d->tr_factor = 0.25; d->tr_high = 0.5; d->tr_low = 1e-3;
     d->clamp_min = 1e-6; d->clamp_max = 1e32;
     d->max_rejects = 30;
     d->pcg_max_iter = 500;
@@ -2696,6 +2701,7 @@ void insfm_ba_destroy(insfm_ba* h) {
     if (h->ev_lc) (void)hipEventDestroy(h->ev_lc);
     if (h->ev_x) (void)hipEventDestroy(h->ev_x);
     if (h->ev_xdone) (void)hipEventDestroy(h->ev_xdone);
+    if (h->ev_pre) (void)hipEventDestroy(h->ev_pre);
     if (h->ev_E) (void)hipEventDestroy(h->ev_E);
     if (h->ev_built) (void)hipEventDestroy(h->ev_built);
     for (auto& e : h->ev_fact)
@@ -3230,6 +3236,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     }
     for (auto& e : h->ev) {
         hipError_t x = hipEventCreate(&e);
+        if (x != hipSuccess) return fail(INSFM_BA_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(x));
+    }
+    if (desc->world_size > 1 || desc->allreduce) {
+        const hipError_t x = hipEventCreateWithFlags(&h->ev_pre, hipEventDisableTiming);
         if (x != hipSuccess) return fail(INSFM_BA_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(x));
     }
     {

@@ -38,10 +38,14 @@ inline double cg_stall_limit_s(const char* env_value) {
 // query() -> int: 0 = stream drained, 1 = still running, negative = stream error
 // now() -> double seconds (monotonic)
 // pause(): a CPU relax hint
-template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause>
+// started(): whether the work queued in front of the CG has completed; until it has, the deadline clock does not run
+//   (multi-rank: the first CG launch waits for the cross-rank exchange, i.e. for the slowest peer, which is not a
+//   stall of this device)
+template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause, class Started>
 int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reached reached, Enqueue enqueue,
-            Query query, Now now, Pause pause, int* rc) {
+            Query query, Now now, Pause pause, Started started, int* rc) {
     double t_progress = now();
+    bool live = false;
     for (;;) {
         if (status() != 0) return CgPoll::kDone;
         const int r = reached();
@@ -67,6 +71,10 @@ int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reac
                 continue;
             }
             if (q < 0) return CgPoll::kStreamError;
+            if (!live) {
+                live = started();
+                if (!live) t_progress = now();
+            }
             const double dt = now() - t_progress;
             if (dt > stall_s) {
                 s.stalled_s = dt;
@@ -75,6 +83,12 @@ int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reac
         }
         pause();
     }
+}
+
+template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause>
+int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reached reached, Enqueue enqueue,
+            Query query, Now now, Pause pause, int* rc) {
+    return cg_poll(s, limit, ahead, stall_s, status, reached, enqueue, query, now, pause, [] { return true; }, rc);
 }
 
 inline double wall_seconds() {

@@ -10,7 +10,12 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libba_oracle.so")
+# "fma": the same source built with fused multiply-adds contracted wherever the compiler likes (-ffp-contract=fast),
+# i.e. the same algorithm with different last-bit rounding -- the reference point for how far rounding alone moves a
+# result (tests/test_oracle.py::test_pcg_rounding_sensitivity_lives_in_the_near_null_space)
+_VARIANTS = {"": _LIB_PATH, "fma": os.path.join(_HERE, "build", "libba_oracle_fma.so")}
 _lib = None
+_libs = {}
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -23,12 +28,24 @@ def build(quiet=True):
     subprocess.run(["make", "-C", _HERE], check=True, capture_output=quiet)
 
 
-def lib():
+def lib(variant=""):
     global _lib
+    if variant:
+        if variant not in _libs:
+            path = _VARIANTS[variant]
+            if not os.path.exists(path):
+                build()
+            _libs[variant] = _bind(ctypes.CDLL(path))
+        return _libs[variant]
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             build()
-        L = ctypes.CDLL(_LIB_PATH)
+        _lib = _bind(ctypes.CDLL(_LIB_PATH))
+    return _lib
+
+
+def _bind(L):
+    if True:
         L.ora_create.restype = ctypes.c_void_p
         L.ora_create.argtypes = [ctypes.c_int] * 4 + [_dp, _ip, _ip, _dp, _dp, _ip]
         L.ora_destroy.argtypes = [ctypes.c_void_p]
@@ -56,8 +73,7 @@ def lib():
         L.ora_gp_get_ds.argtypes = [ctypes.c_void_p, _dp]
         L.ora_spd_inverse.argtypes = [ctypes.c_int, _dp, _dp]
         L.ora_spd_inverse.restype = ctypes.c_int
-        _lib = L
-    return _lib
+    return L
 
 
 def _d(a):
@@ -106,15 +122,16 @@ def retract_pose(x7, d6):
 
 
 DEFAULTS = dict(huber_delta=1.0, tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4,
-                tr_factor=0.5, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
+                tr_factor=0.25, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
                 max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=16)
 
 
 class OracleBA:
     """CPU LM-BA restatement on a packed problem (track-major obs, pypose camera rows)."""
 
-    def __init__(self, model, uv, cam_idx, pt_idx, pp, n_cams, n_points, **opts):
+    def __init__(self, model, uv, cam_idx, pt_idx, pp, n_cams, n_points, variant="", **opts):
         o = dict(DEFAULTS, **opts)
+        self.L = lib(variant)
         self.model = int(model)
         self.C, self.P = int(n_cams), int(n_points)
         self.uv = np.ascontiguousarray(uv, np.float64)
@@ -127,7 +144,7 @@ class OracleBA:
                          o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
         iopt = np.array([o['max_rejects'], o['pcg_max_iter'], o['optimize_poses'], o['threads'], o['precond'],
                          o['cluster_size']], np.int32)
-        self.h = lib().ora_create(self.model, self.C, self.P, self.N, _d(self.uv), _i(self.cam), _i(self.pt),
+        self.h = self.L.ora_create(self.model, self.C, self.P, self.N, _d(self.uv), _i(self.cam), _i(self.pt),
                                   _d(self.pp), _d(dopt), _i(iopt))
         if not self.h:
             raise ValueError("ora_create failed (bad sizes/model or obs not track-major)")
@@ -135,7 +152,7 @@ class OracleBA:
     def __del__(self):
         if getattr(self, "h", None):
             try:
-                lib().ora_destroy(self.h)
+                self.L.ora_destroy(self.h)
             except TypeError:  # interpreter shutdown: the module globals are already gone
                 pass
             self.h = None
@@ -144,45 +161,45 @@ class OracleBA:
         """One LM step; cams [C,stride] / pts [P,3] float64 arrays are updated in place."""
         assert cams.flags.c_contiguous and pts.flags.c_contiguous
         loss = ctypes.c_double()
-        lib().ora_step(self.h, _d(cams), _d(pts), ctypes.byref(loss))
+        self.L.ora_step(self.h, _d(cams), _d(pts), ctypes.byref(loss))
         return loss.value
 
     def stats(self):
         s = np.zeros(8)
-        lib().ora_stats(self.h, _d(s))
+        self.L.ora_stats(self.h, _d(s))
         return dict(trials=int(s[0]), pcg_iters=int(s[1]), pcg_total=int(s[2]), damp_factor=s[3],
                     damping=s[4], failed=int(s[5]), rejects=int(s[6]), coarse_used=int(s[7]))
 
     def cost(self, cams, pts):
         sq = ctypes.c_double()
-        loss = lib().ora_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)), ctypes.byref(sq))
+        loss = self.L.ora_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)), ctypes.byref(sq))
         return loss, float(np.sqrt(sq.value / self.N))
 
     def linearize(self, cams, pts):
-        lib().ora_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)))
+        self.L.ora_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)))
 
     def solve(self, f):
-        return lib().ora_solve(self.h, float(f))
+        return self.L.ora_solve(self.h, float(f))
 
     def build_reduced(self, f):
         """Unscaled reduced camera system for damping factor f: (S upper blocks, b)."""
-        if lib().ora_build_reduced(self.h, float(f)) != 0:
+        if self.L.ora_build_reduced(self.h, float(f)) != 0:
             raise RuntimeError("non-PD point block")
         return self.get(S), self.get(B)
 
     def clusters(self):
         """Camera cluster labels of the two-level preconditioner's coarse space and the cluster count."""
         lab = np.zeros(self.C, np.int32)
-        nc = lib().ora_clusters(self.h, _i(lab))
+        nc = self.L.ora_clusters(self.h, _i(lab))
         return lab, nc
 
     def nnzb(self):
-        return lib().ora_nnzb(self.h)
+        return self.L.ora_nnzb(self.h)
 
     def pattern(self):
         rp = np.zeros(self.C + 1, np.int32)
         col = np.zeros(self.nnzb(), np.int32)
-        lib().ora_pattern(self.h, _i(rp), _i(col))
+        self.L.ora_pattern(self.h, _i(rp), _i(col))
         return rp, col
 
     def get(self, which):
@@ -190,7 +207,7 @@ class OracleBA:
                   GC: (self.C, self.D), S: (self.nnzb(), self.D, self.D), B: (self.C, self.D),
                   DC: (self.C, self.D), DP: (self.P, 3)}
         out = np.zeros(shapes[which])
-        lib().ora_get(self.h, which, _d(out))
+        self.L.ora_get(self.h, which, _d(out))
         return out
 
 
@@ -226,8 +243,9 @@ class OracleGP:
     rays t [N,3] (world frame), camera index / point index per observation (track-major), per-camera factor
     (1.0 calibrated, 0.5 otherwise), per-observation scale-free flag."""
 
-    def __init__(self, trans, cam_idx, pt_idx, fcam, sfree, n_cams, n_points, **opts):
+    def __init__(self, trans, cam_idx, pt_idx, fcam, sfree, n_cams, n_points, variant="", **opts):
         o = dict(GP_DEFAULTS, **opts)
+        self.L = lib(variant)
         self.C, self.P = int(n_cams), int(n_points)
         self.t = np.ascontiguousarray(trans, np.float64)
         self.cam = np.ascontiguousarray(cam_idx, np.int32)
@@ -240,7 +258,7 @@ class OracleGP:
                          o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
         iopt = np.array([o['max_rejects'], o['pcg_max_iter'], 1, o['threads'], o['precond'], o['cluster_size']],
                         np.int32)
-        self.h = lib().ora_gp_create(self.C, self.P, self.N, _d(self.t), _i(self.cam), _i(self.pt), _d(self.fcam),
+        self.h = self.L.ora_gp_create(self.C, self.P, self.N, _d(self.t), _i(self.cam), _i(self.pt), _d(self.fcam),
                                      _i(self.sfree), _d(dopt), _i(iopt))
         if not self.h:
             raise ValueError("ora_gp_create failed")
@@ -254,25 +272,25 @@ class OracleGP:
     def step(self, cams, pts, scales):
         assert cams.flags.c_contiguous and pts.flags.c_contiguous and scales.flags.c_contiguous
         loss = ctypes.c_double()
-        lib().ora_gp_step(self.h, _d(cams), _d(pts), _d(scales), ctypes.byref(loss))
+        self.L.ora_gp_step(self.h, _d(cams), _d(pts), _d(scales), ctypes.byref(loss))
         return loss.value
 
     def cost(self, cams, pts, scales):
         sq = ctypes.c_double()
-        loss = lib().ora_gp_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
+        loss = self.L.ora_gp_cost(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
                                  _d(np.ascontiguousarray(scales)), ctypes.byref(sq))
         return loss, float(np.sqrt(sq.value / self.N))
 
     def linearize(self, cams, pts, scales):
-        lib().ora_gp_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
+        self.L.ora_gp_linearize(self.h, _d(np.ascontiguousarray(cams)), _d(np.ascontiguousarray(pts)),
                                _d(np.ascontiguousarray(scales)))
 
     def solve(self, f):
-        return lib().ora_gp_solve(self.h, float(f))
+        return self.L.ora_gp_solve(self.h, float(f))
 
     def ds(self):
         out = np.zeros(self.N)
-        lib().ora_gp_get_ds(self.h, _d(out))
+        self.L.ora_gp_get_ds(self.h, _d(out))
         return out
 
 
@@ -289,3 +307,31 @@ def gp_solve_to_convergence(problem, max_iters=100, ftol=5e-4, window=4, **opts)
             if abs((prev - recent) / prev) < ftol:
                 break
     return cams, pts, scales, hist
+
+
+def dense_reduced(ora, f):
+    """The damped reduced camera system (S = U' - W V^-1 W^T, both triangles, and b) of `ora`'s current linearization
+    for damping factor f, as a dense (C*D)^2 matrix: the yardstick for comparing two PCG solutions (small C only)."""
+    S, b = ora.build_reduced(f)
+    rp, col = ora.pattern()
+    C, D = ora.C, ora.D
+    Sf = np.zeros((C * D, C * D))
+    for i in range(C):
+        for e in range(rp[i], rp[i + 1]):
+            j = col[e]
+            Sf[i * D:(i + 1) * D, j * D:(j + 1) * D] = S[e]
+            if j != i:
+                Sf[j * D:(j + 1) * D, i * D:(i + 1) * D] = S[e].T
+    return Sf, b.ravel().copy()
+
+
+def solve_differences(S, b, x, x_ref):
+    """How far apart two solutions of S x = b are, three ways:
+      max    max|x - x_ref| / max|x_ref|                  (dominated by the near-null space of S)
+      energy ||x - x_ref||_S / ||x_ref||_S                 (the norm CG minimizes the error in)
+      resid  ||S (x - x_ref)|| / ||b||                     (on the scale of the PCG's relative-residual tolerance)"""
+    x, x_ref = np.ravel(x), np.ravel(x_ref)
+    d = x - x_ref
+    return dict(max=float(np.abs(d).max() / np.abs(x_ref).max()),
+                energy=float(np.sqrt(max(d @ S @ d, 0.0) / max(x_ref @ S @ x_ref, 1e-300))),
+                resid=float(np.linalg.norm(S @ d) / np.linalg.norm(b)))

@@ -62,6 +62,18 @@ int main() {
             [&] { fake_t += 1e-4; return fake_t; }, [] {}, &rc);
         std::printf("hung result=%d stalled_s=%.3f enq=%d\n", r, s.stalled_s, s.enq);
     }
+    {   // gated: the work in front of the CG (a peer's exchange) completes only after 2 s of fake time; the deadline
+        // (0.5 s) counts from then on, so the poll stalls ~0.5 s after the gate opened, not 0.5 s after the start
+        FakeDevice d; d.hung = true; CgPoll s; s.enq = 4; d.enqueued = 4;
+        int rc = 0;
+        double fake_t = 0.0, opened = -1.0;
+        const int r = cg_poll(
+            s, 502, 2, 0.5, [&] { d.tick(); return d.status; }, [&] { return d.reached; },
+            [&](int, int to) { d.enqueued = to; return 0; }, [&] { return 1; },
+            [&] { fake_t += 1e-4; return fake_t; }, [] {},
+            [&] { const bool o = fake_t >= 2.0; if (o && opened < 0) opened = fake_t; return o; }, &rc);
+        std::printf("gated result=%d stalled_s=%.3f end=%.3f opened=%.3f\n", r, s.stalled_s, fake_t, opened);
+    }
     {   // status never set, device drains everything: stops at the launch limit
         FakeDevice d; CgPoll s;
         const int r = [&] {

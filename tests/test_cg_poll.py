@@ -48,3 +48,13 @@ def test_stream_error_and_enqueue_error(poll_out):
 def test_stall_limit_env(poll_out):
     lim = poll_out["limit"]
     assert float(lim["default"]) == 10.0 and float(lim["env"]) == 0.25 and float(lim["bad"]) == 10.0
+
+
+def test_deadline_starts_after_the_gate(poll_out):
+    """Multi-rank: the CG waits for the cross-rank exchange (the slowest peer); the stall clock starts only once the
+    work queued in front of the CG has completed, so a peer that is seconds behind is not reported as a hung device."""
+    g = poll_out["gated"]
+    assert int(g["result"]) == -3
+    assert float(g["opened"]) >= 2.0
+    assert 0.5 <= float(g["stalled_s"]) < 0.6
+    assert float(g["end"]) >= 2.5

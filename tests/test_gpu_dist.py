@@ -47,9 +47,9 @@ def test_two_ranks_match_single_gpu(extra):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("nproc", [2, 4])
+@pytest.mark.parametrize("nproc", [2, 4, 8])
 def test_config4_sharded_config3_scene(nproc):
-    """BASELINE config 4: the full config-3 scene (1000 cams / 200k points / 2M obs) track-sharded over 2 and 4 ranks
+    """BASELINE config 4: the full config-3 scene (1000 cams / 200k points / 2M obs) track-sharded over 2, 4 and 8 ranks
     (gloo, ranks sharing the one MI355X of the test box) vs the single-GPU LM: loss 1e-9, parameters 1e-7, every rank
     holds bitwise-equal cameras (the replicated CG computed the same dc), RMSE |delta| <= 1e-4 px."""
     out = _run(nproc, "gloo", ["--config", "3", "--steps", "3"], timeout=850)

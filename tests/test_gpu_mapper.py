@@ -49,3 +49,40 @@ def test_mapper_matches_oracle_pipeline(tmp_path, seed):
     assert [b['stage'] for b in T['ba']] == ['ba0', 'ba1', 'ba2', 'ba_final']
     for b in T['ba']:
         assert b['steps'] >= 1 and b['total_s'] >= b['steps_s'] > 0
+
+
+@pytest.mark.timeout(600)
+def test_mapper_config5_size_matches_oracle_pipeline(tmp_path):
+    """BASELINE config 5 at its stated size: a ~500-image database (500 images, 100k points seen by 8 images each,
+    1.8M stored matches; the bench's `--path mapper` scene, synth.write_mapper_database defaults) through the mapper's
+    BA half on the GPU processors vs the oracle-stage pipeline (oracle/mapper.py, ~40 s on CPU): the same stage list
+    with the same track / observation counts after every stage, GP loss to 1e-6 relative, every BA's final RMSE within
+    1e-4 px, the same surviving track ids and camera centres within 1e-4 of the normalized scene extent."""
+    size = dict(n_images=500, n_points=100_000, track_len=8, window=12, reach=3, images_per_camera=50, distractors=200)
+    scene = MS.make_db(tmp_path / "db.db", seed=0, **size)
+    vg, cams, ims, cfg = MS.load(tmp_path / "db.db", scene, seed=0)
+    assert len(ims) == 500
+    np.random.seed(0)
+    T = {}
+    with contextlib.redirect_stdout(io.StringIO()):
+        cams, ims, tracks = SolveGlobalMapper(vg, cams, ims, cfg, timings=T)
+    vg2, cams2, ims2, cfg2 = MS.load(tmp_path / "db.db", scene, seed=0)
+    np.random.seed(0)
+    ref = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        _, _, tracks2 = OM.solve_global_mapper(vg2, cams2, ims2, cfg2, trace=ref)
+    got = T['trace']
+    print("gpu   ", got)
+    print("oracle", ref)
+    assert [g[0] for g in got] == [r[0] for r in ref]
+    assert got[0][1] > 50_000 and got[0][2] > 500_000, got[0]   # ~71k tracks / ~570k observations
+    for g, r in zip(got, ref):
+        assert g[1:3] == r[1:3], (g, r)
+        if g[0] == 'gp':
+            assert abs(g[3] - r[3]) <= 1e-6 * abs(r[3]), (g, r)
+        elif g[3] is not None:
+            assert abs(g[3] - r[3]) <= 1e-4, (g, r)
+    assert list(tracks.keys()) == list(tracks2.keys())
+    C = np.array([im.center() for im in ims])
+    C2 = np.array([im.center() for im in ims2])
+    assert np.abs(C - C2).max() <= 1e-4, np.abs(C - C2).max()

@@ -267,10 +267,21 @@ def test_two_level_step_with_coarse_active_and_fewer_iterations():
 def test_repeated_solves_lagged_coarse_inverse(model):
     """Consecutive solves on one engine under the lag rule: the first solve after a linearization runs with the coarse
     inverse of the previous solve (factorized on the side stream while that CG ran), retries at the same
-    linearization use their own.  Every solve matches the oracle's (same rule): iterations and dc.  The coarse sizes
-    here (m = 45 / 65 / 85) end in a partial dense block."""
+    linearization use their own.  Every solve matches the oracle's (same rule): iterations, and dc in residual space
+    (||S (dc_gpu - dc_oracle)|| / ||b|| <= 1e-9, 4 decades inside the PCG's 1e-5 tolerance; 1e-8 for the lagged D = 16
+    solves) and in the energy norm (<= 1e-6; 1e-5 there); max-abs 1e-8 for own-E solves and 1e-6 for lagged ones with
+    D <= 12.  The coarse sizes here
+    (m = 45 / 65 / 85) end in a partial dense block.
+
+    FULL_OPENCV (D = 16) at k = 0 has exactly dependent distortion columns (k1..k3 vs k4..k6), held apart only by
+    the damping: cond(S) ~ 5e13, and a lagged solve's max-abs difference is set by rounding, not by the algorithm --
+    the oracle against itself built with other rounding moves 4e-6 there while agreeing to 1.6e-11 in residual space
+    (tests/test_oracle.py::test_pcg_rounding_sensitivity_lives_in_the_near_null_space).  So for D = 16 lagged solves
+    the residual-space and energy bounds are the parity check (max-abs is reported)."""
     prob = make_problem(30, 800, seed=5, model=model)
     cams, pts = prob.cams_init.copy(), prob.points_init.copy()
+    ref = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
+    ref.linearize(cams, pts)
     for rep in range(3):
         eng, ora = engines(prob, cluster_size=6)
         # (relinearize?, damping factor): LM-like sequences -- fresh trials change f by <= 16x, retries by more
@@ -282,18 +293,74 @@ def test_repeated_solves_lagged_coarse_inverse(model):
             it_g = eng.debug_solve(f)
             it_o = ora.solve(f)
             assert it_g == it_o, (rep, k, it_g, it_o)
-            err = rel(eng.debug_get(7, (prob.n_cams, eng.D)), ora.get(O.DC))
-            # own-E solves: 1e-8 like every other solve.  Lagged solves run with the previous solve's E^-1, a worse
-            # fit to the current S~, which amplifies last-bit differences of E: the E^-1 computation itself is bitwise
-            # the oracle's (test_coarse_inverse_matches_numpy), but E is summed in a different order, and k_schur's
-            # LDS atomics make S~ (hence E) vary in its last bits from run to run.  With D = 16 (ten intrinsics,
-            # cond(E) ~ 4e11) E^-1 is only determined to ~cond(E) u ~ 4e-5 in its worst direction by any f64
-            # computation: 4e-6 .. 1.3e-4 seen across runs there (the PCG's own 1e-5 residual tolerance allows far
-            # larger solution differences at this conditioning), <= 1e-7 for D <= 12.
+            dc_g = eng.debug_get(7, (prob.n_cams, eng.D))
+            S, b = O.dense_reduced(ref, f)
+            d = O.solve_differences(S, b, dc_g, ora.get(O.DC))
+            print(f"model {model} rep {rep} solve {k}: {d}")
             lagged = relin and k > 0
-            tol_lag = 1e-3 if eng.D == 16 else 1e-6
-            assert err < (tol_lag if lagged else 1e-8), (rep, k, err)
+            if lagged and eng.D == 16:
+                # round 3 on the MI355X: resid 2e-11 .. 5e-10, energy 3e-8 .. 2.3e-7 over 3 reps (k_schur's LDS-atomic
+                # order varies from run to run); the oracle against its own FMA-contracted build: 1.6e-11 / 2.6e-8
+                assert d["resid"] < 1e-8 and d["energy"] < 1e-5, (rep, k, d)
+            else:
+                assert d["resid"] < 1e-9 and d["energy"] < 1e-6, (rep, k, d)
+            if not lagged:
+                assert d["max"] < 1e-8, (rep, k, d)
+            elif eng.D <= 12:
+                assert d["max"] < 1e-6, (rep, k, d)
         eng.close()
+
+
+@pytest.mark.parametrize("model", (4, 6))
+def test_high_d_models_to_convergence_match_oracle(model):
+    """OPENCV (D = 12) and FULL_OPENCV (D = 16) scenes run to the reference stop rule (bundle_adjustment.py:128-150),
+    GPU two-level PCG vs the oracle step by step: the same number of LM steps, the same trials per step, the loss per
+    step to 1e-8 and the final RMSE to 1e-6 px (the north_star bar is 1e-4 px)."""
+    prob = make_problem(200, 20000, seed=7, model=model)
+    eng, ora = engines(prob)
+    cg, pg = dev(prob.cams_init), dev(prob.points_init)
+    co, po = prob.cams_init.copy(), prob.points_init.copy()
+    hist = []
+    for s in range(60):
+        lg, st = eng.step(cg, pg)
+        lo = ora.step(co, po)
+        so = ora.stats()
+        assert st["trials"] == so["trials"], (s, st, so)
+        assert abs(lg - lo) / lo < 1e-8, (s, lg, lo)
+        hist.append(lg)
+        if len(hist) >= 8:
+            a, b = np.mean(hist[-4:]), np.mean(hist[-8:-4])
+            if abs((b - a) / b) < 5e-4 or hist[-1] == hist[-2]:
+                break
+    assert 5 <= len(hist) < 60, len(hist)
+    _, rmse_g = eng.cost(cg, pg)
+    _, rmse_o = ora.cost(co, po)
+    print(f"model {model}: {len(hist)} steps, rmse gpu {rmse_g:.12f} oracle {rmse_o:.12f}")
+    assert abs(rmse_g - rmse_o) < 1e-6, (rmse_g, rmse_o)
+    assert rmse_g < 2.5
+
+
+def test_two_level_converges_to_the_block_jacobi_oracle_on_config3():
+    """The product default (two-level PCG, the build's preconditioner) against the oracle's block-Jacobi PCG(1e-5) --
+    the closest restatement of the reference's PCG(tol=1e-5) (bundle_adjustment.py:117) -- on the full config-3 scene,
+    each run to the reference stop rule: the same number of LM steps and final RMSE |delta| <= 1e-4 px (north_star);
+    in practice they agree to ~1e-8 px."""
+    prob = make_config(3)
+    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=DEV)
+    cg, pg = dev(prob.cams_init), dev(prob.points_init)
+    hist = []
+    for _ in range(200):
+        hist.append(eng.step(cg, pg)[0])
+        if len(hist) >= 8:
+            a, b = np.mean(hist[-4:]), np.mean(hist[-8:-4])
+            if abs((b - a) / b) < 5e-4 or hist[-1] == hist[-2]:
+                break
+    _, rmse_g = eng.cost(cg, pg)
+    eng.close()
+    _, _, hist_o, rmse_o = O.solve_to_convergence(prob, precond=0)
+    print(f"two-level GPU {len(hist)} steps rmse {rmse_g:.10f}; block-Jacobi oracle {len(hist_o)} steps rmse {rmse_o:.10f}")
+    assert len(hist) == len(hist_o)
+    assert abs(rmse_g - rmse_o) <= 1e-4, (rmse_g, rmse_o)
 
 
 def _reject_scene(seed, frac):
@@ -450,7 +517,7 @@ def test_coarse_inverse_matches_numpy(m):
     assert oko
     dev_o = np.abs((X - Xo) * sc[:, None] * sc[None, :]).max()
     print(f"m={m}: {us.value:.1f} us per inverse; vs oracle: bitwise {np.array_equal(X, Xo)}, max scaled diff {dev_o:.2e}")
-    assert dev_o < 1e-12
+    assert np.array_equal(X, Xo)  # same steps, pivots and fused multiply-adds: bitwise
     if m > 1:
         En = E.copy()
         En[m // 2, m // 2] = -abs(En[m // 2, m // 2])   # not positive definite
