@@ -37,6 +37,7 @@
 #include "cg_poll.h"
 #include "ba_schur_rc.h"
 #include "ba_schur_mf.h"
+#include "create_host.h"
 
 using namespace insfm;
 
@@ -1491,6 +1492,38 @@ __global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ c
 }
 
 // flags[0..3] = 0, status[0..3] = 0
+// ---- create: structure derived on the device --------------------------------------------------------------------
+// Per local track p (observations sorted by camera): each observation's track and the start of its camera run, i.e.
+// of its upper partners (the tail of the track from there on).
+__global__ __launch_bounds__(kThreads) void k_derive_tracks(int Pl, const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+                                                            int* __restrict__ ptl, int* __restrict__ ustart) {
+    const int p = blockIdx.x * kThreads + threadIdx.x;
+    if (p >= Pl) return;
+    const int b0 = pt_ptr[p], b1 = pt_ptr[p + 1];
+    int u = b0, prev = -1;
+    for (int o = b0; o < b1; ++o) {
+        const int c = cam[o];
+        if (c != prev) { u = o; prev = c; }
+        ptl[o] = p;
+        ustart[o] = u;
+    }
+}
+// Per camera-major entry e (observation o = cam_obs[e]): the Schur descriptor {o, p, partner begin, partner end} and,
+// for the BA, the point and uv the camera linearization reads.
+__global__ __launch_bounds__(kThreads) void k_derive_cm(int Nl, const int* __restrict__ cam_obs, const int* __restrict__ ptl,
+                                                        const int* __restrict__ ustart, const int* __restrict__ pt_ptr,
+                                                        const double* __restrict__ uv, int4* __restrict__ sdesc,
+                                                        int* __restrict__ cm_pt, double* __restrict__ cm_uv) {
+    const int e = blockIdx.x * kThreads + threadIdx.x;
+    if (e >= Nl) return;
+    const int o = cam_obs[e], p = ptl[o];
+    sdesc[e] = make_int4(o, p, ustart[o], pt_ptr[p + 1]);
+    if (uv) {
+        cm_pt[e] = p;
+        reinterpret_cast<double2*>(cm_uv)[e] = reinterpret_cast<const double2*>(uv)[o];
+    }
+}
+
 __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) {
     const int t = threadIdx.x;
     if (t < 4) flags[t] = 0;
@@ -1669,29 +1702,6 @@ namespace {
         }                                                                                         \
     } while (0)
 
-// Host worker threads for create's independent per-camera loops (transient: joined before create returns).
-int host_threads(int work) {
-    static const int hw = [] {
-        const char* e = std::getenv("INSFM_HOST_THREADS");
-        const int v = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
-        return std::max(1, std::min(v, 16));
-    }();
-    return std::max(1, std::min(hw, work / 64));
-}
-
-// f(thread, begin, end) over [0, n) split into nth contiguous ranges (thread 0 runs on the caller).
-template <typename F>
-void parallel_ranges(int n, int nth, F&& f) {
-    std::vector<std::thread> ts;
-    const int per = (n + nth - 1) / nth;
-    for (int t = 1; t < nth; ++t) {
-        const int a = t * per, b = std::min(n, a + per);
-        if (a < b) ts.emplace_back([&f, t, a, b] { f(t, a, b); });
-    }
-    f(0, 0, std::min(n, per));
-    for (auto& th : ts) th.join();
-}
-
 int dalloc(insfm_ba* h, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     hipError_t e = hipMalloc(p, bytes);
@@ -1788,49 +1798,11 @@ void acc_time(insfm_ba* h, int a, int b, int slot) {
 // in increasing id, growing by the most-connected unassigned camera (ties: smallest id) up to K members; aggregates
 // smaller than K/2 are dissolved into the most-connected aggregate of size >= K/2 (ties: smallest aggregate id);
 // labels renumbered by first appearance.
+// (built in create's block-pattern pass)
 struct CovisGraph {
     std::vector<int> ptr, nb;
     std::vector<long long> w;
 };
-
-CovisGraph covis_graph(int C, const std::vector<int>& gcptr, const std::vector<int>& gcobs, const std::vector<int>& gptr,
-                       const int32_t* cam_idx, const int32_t* pt_idx) {
-    CovisGraph g;
-    g.ptr.assign(C + 1, 0);
-    // rows are independent: camera ranges on transient host threads, concatenated in row order
-    const int nth = host_threads(C);
-    std::vector<std::vector<int>> pnb(nth);
-    std::vector<std::vector<long long>> pw(nth);
-    std::vector<int> rlen(C, 0);
-    parallel_ranges(C, nth, [&](int t, int i0, int i1) {
-        std::vector<int> mark(C, -1), buf;
-        std::vector<long long> acc(C, 0);
-        for (int i = i0; i < i1; ++i) {
-            buf.clear();
-            for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
-                const int o = gcobs[e], p = pt_idx[o];
-                for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
-                    if (q == o) continue;
-                    const int j = cam_idx[q];
-                    if (j == i) continue;
-                    if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf.push_back(j); }
-                    acc[j] += 1;
-                }
-            }
-            std::sort(buf.begin(), buf.end());
-            for (int j : buf) { pnb[t].push_back(j); pw[t].push_back(acc[j]); }
-            rlen[i] = (int)buf.size();
-        }
-    });
-    for (int i = 0; i < C; ++i) g.ptr[i + 1] = g.ptr[i] + rlen[i];
-    g.nb.reserve(g.ptr[C]);
-    g.w.reserve(g.ptr[C]);
-    for (int t = 0; t < nth; ++t) {
-        g.nb.insert(g.nb.end(), pnb[t].begin(), pnb[t].end());
-        g.w.insert(g.w.end(), pw[t].begin(), pw[t].end());
-    }
-    return g;
-}
 
 int aggregate(const CovisGraph& g, int C, int K, std::vector<int>& lab) {
     lab.assign(C, -1);
@@ -2750,10 +2722,23 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (desc->world_size > 1 && !desc->allreduce) return fail(INSFM_BA_EINVAL, "world_size > 1 needs allreduce");
     if (h->C > 30000) return fail(INSFM_BA_EINVAL, "n_cams > 30000 not supported (LDS slot table)");
     const int C = h->C, P = h->P, N = h->N, D = h->D;
-    for (int i = 0; i < N; ++i) {
-        if (cam_idx[i] < 0 || cam_idx[i] >= C) return fail(INSFM_BA_EINVAL, "cam_idx out of range");
-        if (pt_idx[i] < 0 || pt_idx[i] >= P) return fail(INSFM_BA_EINVAL, "pt_idx out of range");
-        if (i && pt_idx[i] < pt_idx[i - 1]) return fail(INSFM_BA_EINVAL, "observations must be track-major (pt_idx nondecreasing)");
+    // every pass over the observations below runs on this pool (create_host.h); joined when create returns
+    HostPool pool(host_pool_size());
+    {
+        // input checks, first failing index wins (the lowest slice with a failure holds it)
+        std::vector<int> bad(pool.size(), 0);
+        pool.ranges(N, [&](int t, long long a, long long b) {
+            for (long long i = a; i < b; ++i) {
+                if (cam_idx[i] < 0 || cam_idx[i] >= C) { bad[t] = 1; return; }
+                if (pt_idx[i] < 0 || pt_idx[i] >= P) { bad[t] = 2; return; }
+                if (i && pt_idx[i] < pt_idx[i - 1]) { bad[t] = 3; return; }
+            }
+        });
+        for (int e : bad) {
+            if (e == 1) return fail(INSFM_BA_EINVAL, "cam_idx out of range");
+            if (e == 2) return fail(INSFM_BA_EINVAL, "pt_idx out of range");
+            if (e == 3) return fail(INSFM_BA_EINVAL, "observations must be track-major (pt_idx nondecreasing)");
+        }
     }
     h->p0 = std::max(0, desc->shard_point_begin);
     h->p1 = desc->shard_point_end < 0 ? P : std::min(P, desc->shard_point_end);
@@ -2765,96 +2750,110 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     auto tick = [&](const char* what) {
         if (ctrace) std::fprintf(stderr, "[insfm create] %-28s %8.1f ms\n", what, 1e3 * (wall_seconds() - ct0));
     };
-    // global track pointers
+    // global track pointers (pt_idx is nondecreasing: one binary search per track)
     std::vector<int> gptr(P + 1, 0);
-    for (int i = 0; i < N; ++i) gptr[pt_idx[i] + 1]++;
-    for (int p = 0; p < P; ++p) gptr[p + 1] += gptr[p];
+    pool.ranges(P + 1, [&](int, long long a, long long b) {
+        for (long long p = a; p < b; ++p) gptr[p] = (int)(std::lower_bound(pt_idx, pt_idx + N, (int32_t)p) - pt_idx);
+    });
     h->o0 = gptr[h->p0];
     h->Nl = gptr[h->p1] - h->o0;
     const int o0 = h->o0, Nl = h->Nl, Pl = h->Pl;
-    // local arrays; each track's observations are reordered by camera (stable) so that the upper-triangle partners
-    // of an observation are the contiguous tail [ustart[o], track end) of its track
-    std::vector<int> lptr(Pl + 1), lptl(Nl), lcam(Nl), lsrc(Nl), lust(Nl);
+    // local arrays; each track's observations are reordered by camera (stable insertion sort: tracks are short) so
+    // that the upper-triangle partners of an observation are the contiguous tail [ustart[o], track end) of its track;
+    // key = that tail's length (the observation's upper-partner count)
+    std::vector<int> lptr(Pl + 1);
+    nivec<int> lptl(Nl), lcam(Nl), lsrc(Nl), lust(Nl), key(Nl);
     for (int p = 0; p <= Pl; ++p) lptr[p] = gptr[h->p0 + p] - o0;
-    for (int p = 0; p < Pl; ++p) {
-        const int b0 = lptr[p], b1 = lptr[p + 1];
-        for (int o = b0; o < b1; ++o) lsrc[o] = o0 + o;
-        std::stable_sort(lsrc.begin() + b0, lsrc.begin() + b1, [&](int x, int y) { return cam_idx[x] < cam_idx[y]; });
-        for (int o = b0; o < b1; ++o) {
-            lcam[o] = cam_idx[lsrc[o]];
-            lptl[o] = p;
+    std::vector<int> kmax_t(pool.size(), 0);
+    pool.ranges(Pl, [&](int t, long long pa, long long pb) {
+        int km = 0;
+        for (long long p = pa; p < pb; ++p) {
+            const int b0 = lptr[p], b1 = lptr[p + 1];
+            for (int o = b0; o < b1; ++o) {
+                const int x = o0 + o, cx = cam_idx[x];
+                int u = o;
+                while (u > b0 && cam_idx[lsrc[u - 1]] > cx) { lsrc[u] = lsrc[u - 1]; --u; }
+                lsrc[u] = x;
+            }
+            int u = b0;
+            for (int o = b0; o < b1; ++o) {
+                lcam[o] = cam_idx[lsrc[o]];
+                lptl[o] = (int)p;
+                if (o > b0 && lcam[o] != lcam[o - 1]) u = o;
+                lust[o] = u;
+                key[o] = b1 - u;
+                km = std::max(km, key[o]);
+            }
         }
-        for (int o = b0; o < b1; ++o) {
-            int u = o;
-            while (u > b0 && lcam[u - 1] == lcam[o]) --u;
-            lust[o] = u;
-        }
-    }
+        kmax_t[t] = km;
+    });
+    const int kmax = *std::max_element(kmax_t.begin(), kmax_t.end());
     tick("local track order");
-    std::vector<int> cptr(C + 1, 0), cobs(Nl);
-    for (int o = 0; o < Nl; ++o) cptr[lcam[o] + 1]++;
-    for (int c = 0; c < C; ++c) cptr[c + 1] += cptr[c];
+    // camera-major lists; within a camera, observations with more upper partners first (stable), which balances the
+    // Schur groups: two stable counting sorts, by descending partner count, then by camera
+    std::vector<int> cptr;
+    nivec<int> cobs;
     {
-        // balance the Schur groups: within a camera, observations with more upper partners first (stable) -- one
-        // counting sort on (camera, descending partner count) instead of a comparison sort per camera
-        std::vector<int> key(Nl);
-        int kmax = 0;
-        for (int o = 0; o < Nl; ++o) {
-            key[o] = lptr[lptl[o] + 1] - lust[o];
-            kmax = std::max(kmax, key[o]);
-        }
-        std::vector<int> byk(kmax + 2, 0), order(Nl);
-        for (int o = 0; o < Nl; ++o) byk[kmax - key[o] + 1]++;
-        for (int k = 0; k <= kmax; ++k) byk[k + 1] += byk[k];
-        for (int o = 0; o < Nl; ++o) order[byk[kmax - key[o]]++] = o;   // descending key, stable
-        std::vector<int> fill(cptr.begin(), cptr.end() - 1);
-        for (int t = 0; t < Nl; ++t) {                                     // stable by camera
-            const int o = order[t];
-            cobs[fill[lcam[o]]++] = o;
-        }
-    }
-    std::vector<int4> sdesc(std::max(Nl, 1));
-    for (int e = 0; e < Nl; ++e) {
-        const int o = cobs[e], p = lptl[o];
-        sdesc[e] = make_int4(o, p, lust[o], lptr[p + 1]);
+        nivec<int> byk;
+        std::vector<int> kptr;
+        pcount_sort(pool, Nl, kmax + 1, nullptr, [&](int o) { return kmax - key[o]; }, byk, kptr);
+        pcount_sort(pool, Nl, C, byk.data(), [&](int o) { return lcam[o]; }, cobs, cptr);
     }
     tick("camera-major lists");
-    // global upper pattern (identical on every rank)
-    std::vector<int> gcptr(C + 1, 0), gcobs(N);
-    for (int i = 0; i < N; ++i) gcptr[cam_idx[i] + 1]++;
-    for (int c = 0; c < C; ++c) gcptr[c + 1] += gcptr[c];
-    {
-        std::vector<int> fill(gcptr.begin(), gcptr.end() - 1);
-        for (int i = 0; i < N; ++i) gcobs[fill[cam_idx[i]]++] = i;
-    }
+    // global camera-major list (identical on every rank), then the co-visibility graph and the upper block pattern in
+    // one pass: per camera i, every other camera j sharing a track, with the number of (obs of i, obs of j) pairs
+    // sharing a track (the two-level clustering's weights); the pattern row of i is i, then the neighbours j > i
+    std::vector<int> gcptr;
+    nivec<int> gcpt;  // the point of every observation, camera-major
+    pcount_sort(pool, N, C, nullptr, [&](int i) { return cam_idx[i]; }, gcpt, gcptr, [&](int i) { return pt_idx[i]; });
+    CovisGraph g;
     std::vector<int> rptr(C + 1, 0), cols;
     {
-        // rows are independent: camera ranges on a few transient host threads, each with its own marks
-        const int nth = host_threads(C);
-        std::vector<std::vector<int>> part(nth);
-        std::vector<int> rlen(C, 0);
-        parallel_ranges(C, nth, [&](int t, int i0, int i1) {
+        const int T = pool.size();
+        std::vector<std::vector<int>> pnb(T);
+        std::vector<std::vector<long long>> pw(T);
+        std::vector<int> nlen(C, 0), ulen(C, 0);
+        pool.ranges(C, [&](int t, long long i0, long long i1) {
             std::vector<int> mark(C, -1), buf;
-            std::vector<int>& out = part[t];
-            for (int i = i0; i < i1; ++i) {
+            std::vector<long long> acc(C, 0);
+            for (int i = (int)i0; i < (int)i1; ++i) {
                 buf.clear();
-                buf.push_back(i);
-                mark[i] = i;
                 for (int e = gcptr[i]; e < gcptr[i + 1]; ++e) {
-                    const int p = pt_idx[gcobs[e]];
+                    const int p = gcpt[e];
                     for (int q = gptr[p]; q < gptr[p + 1]; ++q) {
                         const int j = cam_idx[q];
-                        if (j > i && mark[j] != i) { mark[j] = i; buf.push_back(j); }
+                        if (j == i) continue;  // (the observation itself and same-camera duplicates)
+                        if (mark[j] != i) { mark[j] = i; acc[j] = 0; buf.push_back(j); }
+                        acc[j] += 1;
                     }
                 }
                 std::sort(buf.begin(), buf.end());
-                out.insert(out.end(), buf.begin(), buf.end());
-                rlen[i] = (int)buf.size();
+                int up = 0;
+                for (int j : buf) { pnb[t].push_back(j); pw[t].push_back(acc[j]); up += j > i; }
+                nlen[i] = (int)buf.size();
+                ulen[i] = up;
             }
         });
-        for (int i = 0; i < C; ++i) rptr[i + 1] = rptr[i] + rlen[i];
-        cols.reserve(rptr[C]);
-        for (auto& v : part) cols.insert(cols.end(), v.begin(), v.end());
+        g.ptr.assign(C + 1, 0);
+        for (int i = 0; i < C; ++i) {
+            g.ptr[i + 1] = g.ptr[i] + nlen[i];
+            rptr[i + 1] = rptr[i] + 1 + ulen[i];
+        }
+        g.nb.reserve(g.ptr[C]);
+        g.w.reserve(g.ptr[C]);
+        for (int t = 0; t < T; ++t) {
+            g.nb.insert(g.nb.end(), pnb[t].begin(), pnb[t].end());
+            g.w.insert(g.w.end(), pw[t].begin(), pw[t].end());
+        }
+        cols.resize(rptr[C]);
+        pool.ranges(C, [&](int, long long i0, long long i1) {
+            for (int i = (int)i0; i < (int)i1; ++i) {
+                int k = rptr[i];
+                cols[k++] = i;
+                for (int e = g.ptr[i]; e < g.ptr[i + 1]; ++e)
+                    if (g.nb[e] > i) cols[k++] = g.nb[e];
+            }
+        });
     }
     h->nnzb = rptr[C];
     std::vector<int> brow(h->nnzb);
@@ -2874,7 +2873,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 loblk[k] = e;
             }
     }
-    tick("block pattern");
+    tick("block pattern + covisibility");
     // flattened CG neighbour list per row: upper blocks then lower (transposed) ones; pos_up/pos_lo give each upper
     // block's two slots in the row-contiguous copy Sn
     std::vector<int> nptr(C + 1, 0), nj, pup(std::max(1, h->nnzb), -1), plo(std::max(1, h->nnzb), -1);
@@ -3011,6 +3010,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     std::vector<unsigned short> mfpp;
     std::vector<int> mfbo;
     if (h->schur_rc && D <= 8 && !no_mf) {
+        std::vector<int4> sdesc(std::max(Nl, 1));  // (the device copy is derived by k_derive_cm)
+        for (int e = 0; e < Nl; ++e) {
+            const int o = cobs[e], p = lptl[o];
+            sdesc[e] = make_int4(o, p, lust[o], lptr[p + 1]);
+        }
         std::vector<int> slotmap(C, -1), cnt(kMfSlots + 1), run(kMfSlots + 1);
         int pcap = 0;
         bool ok = true;
@@ -3083,17 +3087,19 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
 
     int rc;
     if (kind == 1) {
-        std::vector<double> tl((size_t)3 * Nl);
-        std::vector<int> sl(Nl);
-        for (int o = 0; o < Nl; ++o) {
-            for (int k = 0; k < 3; ++k) tl[3 * (size_t)o + k] = obs[3 * (size_t)lsrc[o] + k];
-            sl[o] = sfree_in ? (sfree_in[lsrc[o]] != 0) : 1;
-        }
+        nivec<double> tl((size_t)3 * Nl);
+        nivec<int> sl(Nl);
+        pool.ranges(Nl, [&](int, long long a, long long b) {
+            for (long long o = a; o < b; ++o) {
+                for (int k = 0; k < 3; ++k) tl[3 * (size_t)o + k] = obs[3 * (size_t)lsrc[o] + k];
+                sl[o] = sfree_in ? (sfree_in[lsrc[o]] != 0) : 1;
+            }
+        });
         if ((rc = upload(h, &h->trans, tl.data(), tl.size()))) return fail(rc, "");
         if ((rc = upload(h, &h->sfree, sl.data(), sl.size()))) return fail(rc, "");
         if ((rc = upload(h, &h->fcam, cpar, (size_t)C))) return fail(rc, "");
         if ((rc = upload(h, &h->osrc, lsrc.data(), lsrc.size()))) return fail(rc, "");
-        h->osrc_host = lsrc;
+        h->osrc_host.assign(lsrc.begin(), lsrc.end());
         auto dd1 = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
         if ((rc = dd1(&h->gobs, (size_t)Nl * kGO))) return fail(rc, "");
         if ((rc = dd1(&h->Up, (size_t)C * 9))) return fail(rc, "");
@@ -3103,19 +3109,36 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd1(&h->scl_new, (size_t)std::max(Nl, 1)))) return fail(rc, "");
         if ((rc = dd1(&h->ds, (size_t)std::max(Nl, 1)))) return fail(rc, "");
     } else {
-        std::vector<double> uvl((size_t)2 * Nl);
-        for (int o = 0; o < Nl; ++o) {
-            uvl[2 * (size_t)o] = obs[2 * (size_t)lsrc[o]];
-            uvl[2 * (size_t)o + 1] = obs[2 * (size_t)lsrc[o] + 1];
-        }
+        nivec<double> uvl((size_t)2 * Nl);
+        pool.ranges(Nl, [&](int, long long a, long long b) {
+            for (long long o = a; o < b; ++o) {
+                uvl[2 * (size_t)o] = obs[2 * (size_t)lsrc[o]];
+                uvl[2 * (size_t)o + 1] = obs[2 * (size_t)lsrc[o] + 1];
+            }
+        });
         if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
         if ((rc = upload(h, &h->pp, cpar, (size_t)2 * C))) return fail(rc, "");
     }
     if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->ptl, lptl.data(), lptl.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->cam_ptr, cptr.data(), cptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->cam_obs, cobs.data(), cobs.size()))) return fail(rc, "");
+    // derived on the device from the four arrays above instead of uploaded (88 of 140 MB for config 3):
+    // per observation its track and the start of its upper partners; per camera-major entry the Schur descriptor and
+    // (BA) the linearization's point / uv gathers
+    if ((rc = dalloc(h, (void**)&h->ptl, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if ((rc = dalloc(h, (void**)&h->ustart, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if ((rc = dalloc(h, (void**)&h->sdesc, sizeof(int4) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if (kind != 1) {
+        if ((rc = dalloc(h, (void**)&h->cm_pt, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dalloc(h, (void**)&h->cm_uv, sizeof(double) * 2 * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    }
+    if (Pl > 0) k_derive_tracks<<<cdiv(Pl, kThreads), kThreads, 0, h->stream>>>(Pl, h->pt_ptr, h->cam, h->ptl, h->ustart);
+    if (Nl > 0)
+        k_derive_cm<<<cdiv(Nl, kThreads), kThreads, 0, h->stream>>>(Nl, h->cam_obs, h->ptl, h->ustart, h->pt_ptr,
+                                                                    kind != 1 ? h->uv : nullptr, h->sdesc, h->cm_pt,
+                                                                    h->cm_uv);
+    if ((rc = launch_err(h, "k_derive"))) return fail(rc, "");
     if (kind != 1) {
         std::vector<int> lb(1, 0);
         for (int p = 0; p < Pl; ++p)  // close the run before a track that would overflow it
@@ -3124,23 +3147,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (Pl > 0) lb.push_back(Pl);
         h->n_lin = (int)lb.size() - 1;
         if ((rc = upload(h, &h->lin_blk, lb.data(), lb.size()))) return fail(rc, "");
-        std::vector<int> cmp(cobs.size());
-        std::vector<double> cmuv(2 * cobs.size());
-        for (size_t e = 0; e < cobs.size(); ++e) {
-            const int o = cobs[e];
-            if (o < 0 || o >= Nl) continue;
-            cmp[e] = lptl[o];
-            cmuv[2 * e] = obs[2 * (size_t)lsrc[o]];
-            cmuv[2 * e + 1] = obs[2 * (size_t)lsrc[o] + 1];
-        }
-        if ((rc = upload(h, &h->cm_pt, cmp.data(), cmp.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->cm_uv, cmuv.data(), cmuv.size()))) return fail(rc, "");
     }
     if ((rc = upload(h, &h->row_ptr, rptr.data(), rptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->col, cols.data(), cols.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->blk_row, brow.data(), brow.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->ustart, lust.data(), lust.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->sdesc, sdesc.data(), sdesc.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->nbr_ptr, nptr.data(), nptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->nbr_j, nj.data(), nj.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pos_up, pup.data(), pup.size()))) return fail(rc, "");
@@ -3287,7 +3297,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (desc->precond == 1 && h->d.optimize_poses) {
         // ---- two-level preconditioner: clusters, source lists of E, buffers ----
         const int MC = D + 1;
-        CovisGraph g = covis_graph(C, gcptr, gcobs, gptr, cam_idx, pt_idx);
         int K = desc->cluster_size > 0 ? desc->cluster_size : 16;
         std::vector<int>& lab = h->clab_host;
         int nc = aggregate(g, C, K, lab);
@@ -3312,31 +3321,41 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         std::vector<int> sperm(std::max<int64_t>(h->n_nbr, 1), 0), rsp(C + 1, 0);
         std::vector<int4> segs;
         int maxseg = 1;
-        for (int i = 0; i < C; ++i) {
-            const int n0 = nptr[i], n1 = nptr[i + 1];
-            std::vector<int> ord(n1 - n0);
-            for (int q = 0; q < n1 - n0; ++q) ord[q] = n0 + q;
-            std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lab[nj[x]] < lab[nj[y]]; });
-            for (int q = 0; q < n1 - n0; ++q) sperm[n0 + q] = ord[q];
-            const int own = lab[i];
-            bool own_done = false;
-            int q = 0;
-            const int before = (int)segs.size();
-            while (q < n1 - n0 || !own_done) {
-                const int cq = q < n1 - n0 ? lab[nj[ord[q]]] : nc;
-                if (!own_done && own < cq) {  // own cluster without neighbours in it
-                    segs.push_back(make_int4(own, q, q, 1));
-                    own_done = true;
-                    continue;
+        {
+            // rows in parallel (each row's segments into its own list), then concatenated in row order
+            std::vector<std::vector<int4>> rsegs(C);
+            pool.ranges(C, [&](int, long long i0, long long i1) {
+                std::vector<int> ord;
+                for (int i = (int)i0; i < (int)i1; ++i) {
+                    const int n0 = nptr[i], n1 = nptr[i + 1];
+                    ord.resize(n1 - n0);
+                    for (int q = 0; q < n1 - n0; ++q) ord[q] = n0 + q;
+                    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return lab[nj[x]] < lab[nj[y]]; });
+                    for (int q = 0; q < n1 - n0; ++q) sperm[n0 + q] = ord[q];
+                    const int own = lab[i];
+                    bool own_done = false;
+                    int q = 0;
+                    std::vector<int4>& out = rsegs[i];
+                    while (q < n1 - n0 || !own_done) {
+                        const int cq = q < n1 - n0 ? lab[nj[ord[q]]] : nc;
+                        if (!own_done && own < cq) {  // own cluster without neighbours in it
+                            out.push_back(make_int4(own, q, q, 1));
+                            own_done = true;
+                            continue;
+                        }
+                        int qe = q;
+                        while (qe < n1 - n0 && lab[nj[ord[qe]]] == cq) ++qe;
+                        out.push_back(make_int4(cq, q, qe, cq == own ? 1 : 0));
+                        if (cq == own) own_done = true;
+                        q = qe;
+                    }
                 }
-                int qe = q;
-                while (qe < n1 - n0 && lab[nj[ord[qe]]] == cq) ++qe;
-                segs.push_back(make_int4(cq, q, qe, cq == own ? 1 : 0));
-                if (cq == own) own_done = true;
-                q = qe;
+            });
+            for (int i = 0; i < C; ++i) {
+                segs.insert(segs.end(), rsegs[i].begin(), rsegs[i].end());
+                rsp[i + 1] = (int)segs.size();
+                maxseg = std::max(maxseg, (int)rsegs[i].size());
             }
-            rsp[i + 1] = (int)segs.size();
-            maxseg = std::max(maxseg, (int)segs.size() - before);
         }
         // E source lists per cluster pair (row cluster c', column cluster c): the segments of c's rows, rows ascending
         std::vector<int> eptr((size_t)nc * nc + 1, 0), eseg;
