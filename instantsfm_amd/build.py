@@ -8,6 +8,7 @@ import hashlib
 import os
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
@@ -15,6 +16,9 @@ SRCS = [os.path.join(HERE, "csrc", n) for n in ("ba_kernels.hip", "passes.hip", 
 HEADERS = [*sorted(glob.glob(os.path.join(HERE, "csrc", "*.h"))), *sorted(glob.glob(os.path.join(REPO, "include", "*.h")))]
 OBJDIR = os.path.join(REPO, "build", "obj")
 OUT = os.path.join(HERE, "_lib", "libinsfm_ba.so")
+# host-side packing extension (plain C / OpenMP, CPython buffer protocol): processors/bundle_adjustment.py pack()
+PACKX_SRC = os.path.join(HERE, "csrc", "packx.c")
+PACKX_OUT = os.path.join(HERE, "_lib", "_packx" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-Wall"]
@@ -87,7 +91,26 @@ def build(force=False, verbose=True):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
         os.replace(OUT + ".tmp", OUT)
+    build_packx(force, verbose)
     return OUT
+
+
+def _numpy_include():
+    import numpy
+    return numpy.get_include()
+
+
+def build_packx(force=False, verbose=True):
+    """The packing extension: no FMA contraction (its cheirality test must round like numpy's unfused operations)."""
+    if not (force or _stale(PACKX_OUT, [PACKX_SRC])):
+        return PACKX_OUT
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-std=c99",
+           "-Wall", f"-I{sysconfig.get_paths()['include']}", f"-I{_numpy_include()}", "-o", PACKX_OUT + ".tmp", PACKX_SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(PACKX_OUT + ".tmp", PACKX_OUT)
+    return PACKX_OUT
 
 
 if __name__ == "__main__":

@@ -1,0 +1,323 @@
+/* Native host half of TorchBA.Solve's packing (instantsfm/processors/bundle_adjustment.py:66-113), used by
+ * processors/bundle_adjustment.py pack().  CPython extension module `_packx` (plain C, numpy C API, OpenMP).
+ *
+ * The reference packs with a Python double loop over tracks x observations (~6.8 us per observation).  The vectorized
+ * numpy pack still paid ~0.4 us per Track object inside np.concatenate (200k observation arrays and 200k xyz arrays
+ * on config 3) plus single-threaded gathers for the cheirality test; here
+ *   collect(track_vals, min_len)  reads every Track's `observations` / `xyz` arrays in place (numpy C API) in one loop;
+ *   finish(...)                   does the registered-image filter, the feature gather, the cheirality test
+ *                                 (z of rotate_quat > 0.1, the same operations in the same order as numpy, no FMA
+ *                                 contraction) and the torch.unique compaction, on all host cores.
+ * collect returns None when an object is not the plain ndarray layout it expects (a Python list, another dtype or
+ * shape); pack() then takes the numpy path, which gives the same result. */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
+#include <numpy/arrayobject.h>
+#include <omp.h>
+#include <stdint.h>
+#include <string.h>
+
+static PyObject *s_obs = NULL, *s_xyz = NULL;  /* interned attribute names */
+
+/* 8: int64, 4: int32, 0: not a C-contiguous [k, 2] integer array */
+static int obs_kind(PyObject* o) {
+    if (!PyArray_Check(o)) return 0;
+    PyArrayObject* a = (PyArrayObject*)o;
+    if (PyArray_NDIM(a) != 2 || PyArray_DIM(a, 1) != 2 || !PyArray_IS_C_CONTIGUOUS(a) || !PyArray_ISNOTSWAPPED(a))
+        return 0;
+    const int t = PyArray_TYPE(a);
+    if (t == NPY_INT64 || (t == NPY_LONGLONG && sizeof(long long) == 8) || (t == NPY_LONG && sizeof(long) == 8)) return 8;
+    if (t == NPY_INT32 || (t == NPY_INT && sizeof(int) == 4)) return 4;
+    return 0;
+}
+
+/* 8: float64, 4: float32, 0: not a C-contiguous (3,) float array */
+static int xyz_kind(PyObject* o) {
+    if (!PyArray_Check(o)) return 0;
+    PyArrayObject* a = (PyArrayObject*)o;
+    if (PyArray_NDIM(a) != 1 || PyArray_DIM(a, 0) != 3 || !PyArray_IS_C_CONTIGUOUS(a) || !PyArray_ISNOTSWAPPED(a)) return 0;
+    const int t = PyArray_TYPE(a);
+    return t == NPY_FLOAT64 ? 8 : (t == NPY_FLOAT32 ? 4 : 0);
+}
+
+/* collect(track_vals, min_len) -> (lengths int64[T], obs int64[n, 2] of the tracks with >= min_len observations,
+ * xyz float64[T, 3]) as bytes, or None (take the numpy path).  The arrays are read in place (numpy C API): one
+ * attribute lookup and a few header reads per Track object. */
+static PyObject* collect(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject* seq;
+    long long min_len;
+    if (!PyArg_ParseTuple(args, "OL", &seq, &min_len)) return NULL;
+    PyObject* fast = PySequence_Fast(seq, "collect: a sequence of tracks");
+    if (!fast) return NULL;
+    const Py_ssize_t T = PySequence_Fast_GET_SIZE(fast);
+    PyObject** items = PySequence_Fast_ITEMS(fast);
+    PyObject** ob = (PyObject**)PyMem_Calloc(T > 0 ? (size_t)T : 1, sizeof(PyObject*));
+    PyObject *lb = NULL, *obb = NULL, *xb = NULL, *res = NULL;
+    if (!ob) { Py_DECREF(fast); return PyErr_NoMemory(); }
+    lb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(int64_t) * (size_t)T));
+    xb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(double) * 3 * (size_t)T));
+    if (!lb || !xb) goto done;
+    int64_t* lengths = (int64_t*)PyBytes_AS_STRING(lb);
+    double* xo = (double*)PyBytes_AS_STRING(xb);
+    Py_ssize_t nvalid = 0;
+    for (Py_ssize_t t = 0; t < T; ++t) {
+        PyObject* o = PyObject_GetAttr(items[t], s_obs);
+        if (!o) goto done;
+        ob[t] = o;
+        if (!obs_kind(o)) goto fallback;
+        lengths[t] = PyArray_DIM((PyArrayObject*)o, 0);
+        if (lengths[t] >= min_len) nvalid += lengths[t];
+        PyObject* x = PyObject_GetAttr(items[t], s_xyz);
+        if (!x) goto done;
+        const int k = xyz_kind(x);
+        if (k == 8) {
+            memcpy(xo + 3 * t, PyArray_DATA((PyArrayObject*)x), 3 * sizeof(double));
+        } else if (k == 4) {
+            const float* f = (const float*)PyArray_DATA((PyArrayObject*)x);
+            xo[3 * t] = f[0]; xo[3 * t + 1] = f[1]; xo[3 * t + 2] = f[2];
+        }
+        Py_DECREF(x);
+        if (!k) goto fallback;
+    }
+    obb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(int64_t) * 2 * (size_t)nvalid));
+    if (!obb) goto done;
+    {
+        int64_t* out = (int64_t*)PyBytes_AS_STRING(obb);
+        for (Py_ssize_t t = 0; t < T; ++t) {
+            if (lengths[t] < min_len) continue;
+            const Py_ssize_t n = 2 * lengths[t];
+            const void* src = PyArray_DATA((PyArrayObject*)ob[t]);
+            if (obs_kind(ob[t]) == 8) {
+                memcpy(out, src, sizeof(int64_t) * (size_t)n);
+            } else {
+                const int32_t* s = (const int32_t*)src;
+                for (Py_ssize_t k = 0; k < n; ++k) out[k] = s[k];
+            }
+            out += n;
+        }
+    }
+    res = PyTuple_Pack(3, lb, obb, xb);
+    goto done;
+fallback:
+    res = Py_None;
+    Py_INCREF(res);
+done:
+    for (Py_ssize_t t = 0; t < T; ++t) Py_XDECREF(ob[t]);
+    PyMem_Free(ob);
+    Py_XDECREF(lb);
+    Py_XDECREF(obb);
+    Py_XDECREF(xb);
+    Py_DECREF(fast);
+    return res;
+}
+
+static int get_buf(PyObject* o, Py_buffer* b, Py_ssize_t itemsize, const char* what) {
+    if (PyObject_GetBuffer(o, b, PyBUF_C_CONTIGUOUS) < 0) return -1;
+    if (b->itemsize != itemsize && b->len % itemsize != 0) {
+        PyBuffer_Release(b);
+        PyErr_Format(PyExc_TypeError, "finish: %s has the wrong element size", what);
+        return -1;
+    }
+    return 0;
+}
+
+/* finish(obs int64[n,2], lengths int64[T], min_len, registered uint8[I], features float64[F,2], foff int64[I+1],
+ *        points float64[T,3], poses float64[I,stride], stride)
+ *   -> (points_2d float64[m,2], camera_indices int64[m], point_indices int64[m], unique_cameras int64[], unique_points
+ *       int64[]) as bytearrays (writable): the observations of registered images whose point lies in front of the camera
+ *       (bundle_adjustment.py:85-113). */
+static PyObject* finish(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject *o_obs, *o_len, *o_reg, *o_feat, *o_foff, *o_pts, *o_pose;
+    long long min_len;
+    int stride;
+    if (!PyArg_ParseTuple(args, "OOLOOOOOi", &o_obs, &o_len, &min_len, &o_reg, &o_feat, &o_foff, &o_pts, &o_pose, &stride))
+        return NULL;
+    Py_buffer bo = {0}, bl = {0}, br = {0}, bf = {0}, bff = {0}, bp = {0}, bq = {0};
+    PyObject* res = NULL;
+    char *pc = NULL, *pp = NULL;
+    int64_t *tid = NULL, *cnt = NULL;
+    if (get_buf(o_obs, &bo, 8, "obs") || get_buf(o_len, &bl, 8, "lengths") || get_buf(o_reg, &br, 1, "registered") ||
+        get_buf(o_feat, &bf, 8, "features") || get_buf(o_foff, &bff, 8, "foff") || get_buf(o_pts, &bp, 8, "points") ||
+        get_buf(o_pose, &bq, 8, "poses"))
+        goto done;
+    {
+        const int64_t* obs = (const int64_t*)bo.buf;
+        const int64_t* len = (const int64_t*)bl.buf;
+        const uint8_t* reg = (const uint8_t*)br.buf;
+        const double* feat = (const double*)bf.buf;
+        const int64_t* foff = (const int64_t*)bff.buf;
+        const double* pts = (const double*)bp.buf;
+        const double* pose = (const double*)bq.buf;
+        const int64_t n = bo.len / 16, nT = bl.len / 8, nI = br.len, nF = bf.len / 16;
+        if (bff.len / 8 != nI + 1 || bp.len / 24 != nT || stride < 7 || bq.len / 8 != nI * (int64_t)stride) {
+            PyErr_SetString(PyExc_ValueError, "finish: inconsistent array sizes");
+            goto done;
+        }
+        /* track id of every observation (valid tracks only, in order) */
+        tid = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+        if (!tid) { PyErr_NoMemory(); goto done; }
+        {
+            int64_t k = 0;
+            for (int64_t t = 0; t < nT; ++t) {
+                if (len[t] < min_len) continue;
+                for (int64_t q = 0; q < len[t] && k < n; ++q) tid[k++] = t;
+            }
+            if (k != n) { PyErr_SetString(PyExc_ValueError, "finish: lengths do not match obs"); goto done; }
+        }
+        int bad = 0;
+        #pragma omp parallel for schedule(static) reduction(|:bad)
+        for (int64_t k = 0; k < n; ++k) {
+            const int64_t im = obs[2 * k];
+            if (im < 0 || im >= nI) { bad |= 1; continue; }
+            if (reg[im]) {
+                const int64_t f = foff[im] + obs[2 * k + 1];
+                if (obs[2 * k + 1] < 0 || f >= foff[im + 1] || f >= nF) bad |= 2;
+            }
+        }
+        if (bad) {
+            PyErr_SetString(PyExc_IndexError, (bad & 1) ? "finish: image id out of range" : "finish: feature id out of range");
+            goto done;
+        }
+        const int nth = omp_get_max_threads();
+        cnt = (int64_t*)PyMem_Calloc((size_t)nth + 1, sizeof(int64_t));
+        pc = (char*)PyMem_Calloc((size_t)(nI > 0 ? nI : 1), 1);
+        pp = (char*)PyMem_Calloc((size_t)(nT > 0 ? nT : 1), 1);
+        uint8_t* ok = (uint8_t*)PyMem_Malloc((size_t)(n > 0 ? n : 1));
+        if (!cnt || !pc || !pp || !ok) { PyMem_Free(ok); PyErr_NoMemory(); goto done; }
+        /* cheirality: z of rotate_quat(points[tid], pose[img]) exactly as _rotated_z's numpy expression */
+        #pragma omp parallel num_threads(nth)
+        {
+            const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
+            const int64_t a = n * t / T_, b = n * (t + 1) / T_;
+            int64_t c = 0;
+            for (int64_t k = a; k < b; ++k) {
+                const int64_t im = obs[2 * k];
+                uint8_t keep = 0;
+                if (reg[im]) {
+                    const double* X = pts + 3 * tid[k];
+                    const double* Q = pose + (int64_t)stride * im;
+                    const double px = X[0], py = X[1], pz = X[2];
+                    const double qx = Q[3], qy = Q[4], qz = Q[5], w = Q[6];
+                    const double uvx = qy * pz - qz * py;
+                    const double uvy = qz * px - qx * pz;
+                    const double uvz = qx * py - qy * px;
+                    const double z = pz + 2.0 * (w * uvz + (qx * uvy - qy * uvx)) + Q[2];
+                    keep = z > 0.1;
+                }
+                ok[k] = keep;
+                if (keep) { pc[im] = 1; pp[tid[k]] = 1; ++c; }
+            }
+            cnt[t + 1] = c;
+        }
+        for (int t = 0; t < nth; ++t) cnt[t + 1] += cnt[t];
+        const int64_t m = cnt[nth];
+        /* compaction maps */
+        int64_t nuc = 0, nup = 0;
+        for (int64_t i = 0; i < nI; ++i) nuc += pc[i];
+        for (int64_t i = 0; i < nT; ++i) nup += pp[i];
+        PyObject *b2d = PyByteArray_FromStringAndSize(NULL, 16 * m), *bci = PyByteArray_FromStringAndSize(NULL, 8 * m);
+        PyObject *bpi = PyByteArray_FromStringAndSize(NULL, 8 * m), *buc = PyByteArray_FromStringAndSize(NULL, 8 * nuc);
+        PyObject* bup = PyByteArray_FromStringAndSize(NULL, 8 * nup);
+        int64_t* cmap = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(nI > 0 ? nI : 1));
+        int64_t* pmap = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(nT > 0 ? nT : 1));
+        if (!b2d || !bci || !bpi || !buc || !bup || !cmap || !pmap) {
+            Py_XDECREF(b2d); Py_XDECREF(bci); Py_XDECREF(bpi); Py_XDECREF(buc); Py_XDECREF(bup);
+            PyMem_Free(cmap); PyMem_Free(pmap); PyMem_Free(ok);
+            if (!PyErr_Occurred()) PyErr_NoMemory();
+            goto done;
+        }
+        int64_t* uc = (int64_t*)PyByteArray_AS_STRING(buc);
+        int64_t* up = (int64_t*)PyByteArray_AS_STRING(bup);
+        for (int64_t i = 0, r = 0; i < nI; ++i) { cmap[i] = r; if (pc[i]) uc[r++] = i; }
+        for (int64_t i = 0, r = 0; i < nT; ++i) { pmap[i] = r; if (pp[i]) up[r++] = i; }
+        double* o2d = (double*)PyByteArray_AS_STRING(b2d);
+        int64_t* oci = (int64_t*)PyByteArray_AS_STRING(bci);
+        int64_t* opi = (int64_t*)PyByteArray_AS_STRING(bpi);
+        #pragma omp parallel num_threads(nth)
+        {
+            const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
+            const int64_t a = n * t / T_, b = n * (t + 1) / T_;
+            int64_t w = cnt[t];
+            for (int64_t k = a; k < b; ++k) {
+                if (!ok[k]) continue;
+                const int64_t im = obs[2 * k];
+                const double* fp = feat + 2 * (foff[im] + obs[2 * k + 1]);
+                o2d[2 * w] = fp[0];
+                o2d[2 * w + 1] = fp[1];
+                oci[w] = cmap[im];
+                opi[w] = pmap[tid[k]];
+                ++w;
+            }
+        }
+        PyMem_Free(cmap); PyMem_Free(pmap); PyMem_Free(ok);
+        res = PyTuple_Pack(5, b2d, bci, bpi, buc, bup);
+        Py_DECREF(b2d); Py_DECREF(bci); Py_DECREF(bpi); Py_DECREF(buc); Py_DECREF(bup);
+    }
+done:
+    PyMem_Free(tid); PyMem_Free(cnt); PyMem_Free(pc); PyMem_Free(pp);
+    if (bo.obj) PyBuffer_Release(&bo);
+    if (bl.obj) PyBuffer_Release(&bl);
+    if (br.obj) PyBuffer_Release(&br);
+    if (bf.obj) PyBuffer_Release(&bf);
+    if (bff.obj) PyBuffer_Release(&bff);
+    if (bp.obj) PyBuffer_Release(&bp);
+    if (bq.obj) PyBuffer_Release(&bq);
+    return res;
+}
+
+/* assign_xyz(track_vals, unique_points int64[n], points float64[n, 3]): track_vals[unique_points[i]].xyz = points[i]
+ * (a row view of `points`, as the Python loop of update() assigns it; bundle_adjustment.py:18-36). */
+static PyObject* assign_xyz(PyObject* self, PyObject* args) {
+    (void)self;
+    PyObject *seq, *o_idx, *o_pts;
+    if (!PyArg_ParseTuple(args, "OOO", &seq, &o_idx, &o_pts)) return NULL;
+    if (!PyArray_Check(o_idx) || !PyArray_Check(o_pts)) { PyErr_SetString(PyExc_TypeError, "assign_xyz: arrays"); return NULL; }
+    PyArrayObject *ai = (PyArrayObject*)o_idx, *ap = (PyArrayObject*)o_pts;
+    if (PyArray_TYPE(ai) != NPY_INT64 || !PyArray_IS_C_CONTIGUOUS(ai) || PyArray_TYPE(ap) != NPY_FLOAT64 ||
+        !PyArray_IS_C_CONTIGUOUS(ap) || PyArray_NDIM(ap) != 2 || PyArray_DIM(ap, 1) != 3 ||
+        PyArray_SIZE(ai) != PyArray_DIM(ap, 0)) {
+        PyErr_SetString(PyExc_ValueError, "assign_xyz: int64 [n] indices and a C-contiguous float64 [n, 3] array");
+        return NULL;
+    }
+    PyObject* fast = PySequence_Fast(seq, "assign_xyz: a sequence of tracks");
+    if (!fast) return NULL;
+    const Py_ssize_t T = PySequence_Fast_GET_SIZE(fast);
+    PyObject** items = PySequence_Fast_ITEMS(fast);
+    const int64_t* idx = (const int64_t*)PyArray_DATA(ai);
+    char* base = (char*)PyArray_DATA(ap);
+    const npy_intp n = PyArray_DIM(ap, 0);
+    npy_intp dims[1] = {3};
+    for (npy_intp i = 0; i < n; ++i) {
+        if (idx[i] < 0 || idx[i] >= T) { PyErr_SetString(PyExc_IndexError, "assign_xyz: track index"); Py_DECREF(fast); return NULL; }
+        PyObject* row = PyArray_New(&PyArray_Type, 1, dims, NPY_FLOAT64, NULL, base + 24 * i, 0,
+                                    NPY_ARRAY_CARRAY, NULL);
+        if (!row) { Py_DECREF(fast); return NULL; }
+        Py_INCREF(o_pts);
+        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) { Py_DECREF(row); Py_DECREF(fast); return NULL; }
+        const int r = PyObject_SetAttr(items[idx[i]], s_xyz, row);
+        Py_DECREF(row);
+        if (r < 0) { Py_DECREF(fast); return NULL; }
+    }
+    Py_DECREF(fast);
+    Py_RETURN_NONE;
+}
+
+static PyMethodDef methods[] = {
+    {"assign_xyz", assign_xyz, METH_VARARGS, "track.xyz = row view of the optimized points, per packed point."},
+    {"collect", collect, METH_VARARGS, "Track observations / xyz through the buffer protocol (or None)."},
+    {"finish", finish, METH_VARARGS, "Registered filter, feature gather, cheirality test and compaction."},
+    {NULL, NULL, 0, NULL},
+};
+
+static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_packx", NULL, -1, methods, NULL, NULL, NULL, NULL};
+
+PyMODINIT_FUNC PyInit__packx(void) {
+    import_array();
+    s_obs = PyUnicode_InternFromString("observations");
+    s_xyz = PyUnicode_InternFromString("xyz");
+    if (!s_obs || !s_xyz) return NULL;
+    return PyModule_Create(&mod);
+}

@@ -13,6 +13,24 @@ from ..engine import BundleAdjuster
 from ..scene.defs import CameraModelId, IMPLEMENTED_MODELS, get_camera_model_info
 
 
+def _load_packx():
+    """The native packing extension (csrc/packx.c, built by instantsfm_amd.build next to libinsfm_ba.so)."""
+    import importlib.util
+    import os
+    import sysconfig
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib",
+                        "_packx" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+    if not os.path.exists(path):
+        return None
+    spec = importlib.util.spec_from_file_location("_packx", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_packx = _load_packx()
+
+
 def _quat_xyzw_from_matrix(R):
     """pp.mat2SE3 rotation part: rotation matrix (or a batch) -> quaternion [x, y, z, w] (sign: w >= 0)."""
     from scipy.spatial.transform import Rotation
@@ -78,7 +96,7 @@ class PackedProblem:
     """What TorchBA.Solve hands the LM (reference :98-126): compacted, track-major arrays + bookkeeping."""
 
     def __init__(self, model, points_2d, camera_indices, point_indices, camera_pps, camera_params, points_3d,
-                 unique_cameras, unique_points, track_keys, remaining_indices, pp_indices):
+                 unique_cameras, unique_points, track_keys, remaining_indices, pp_indices, track_vals=None):
         self.model = model
         self.points_2d = points_2d
         self.camera_indices = camera_indices
@@ -91,19 +109,31 @@ class PackedProblem:
         self.track_keys = track_keys
         self.remaining_indices = remaining_indices
         self.pp_indices = pp_indices
+        self.track_vals = track_vals  # the Track objects in track_keys order (update() writes xyz through it)
 
 
-def pack(cameras, images, tracks, options):
-    """Vectorized restatement of bundle_adjustment.py:66-113."""
+def pack(cameras, images, tracks, options, native=True):
+    """Vectorized restatement of bundle_adjustment.py:66-113.  With the native extension (csrc/packx.c) the per-Track
+    reads and the per-observation filtering run in C on all host cores; ``native=False`` (or Track attributes that are
+    not plain ndarrays) takes the numpy path, which gives the same arrays (tests/test_packing.py checks both)."""
     model = cameras[0].model_id  # :45 "assume all cameras are under the same model"
     info = get_camera_model_info(model)
     if model.value not in IMPLEMENTED_MODELS:
         raise NotImplementedError("Unsupported camera model")
+    min_len = options['min_num_view_per_track']
     track_keys = list(tracks.keys())
     track_vals = list(tracks.values())
-    obs_all = [t.observations for t in track_vals]
-    lengths = np.fromiter(map(len, obs_all), dtype=np.int64, count=len(obs_all))
-    is_valid = lengths >= options['min_num_view_per_track']                                   # :66-68
+    got = _packx.collect(track_vals, int(min_len)) if (native and _packx is not None) else None
+    if got is not None:
+        lengths = np.frombuffer(got[0], np.int64)
+        obs_valid = np.frombuffer(got[1], np.int64).reshape(-1, 2)
+        xyz = None
+        points_3d = np.frombuffer(got[2], np.float64).reshape(-1, 3)
+    else:
+        obs_all = [t.observations for t in track_vals]
+        lengths = np.fromiter(map(len, obs_all), dtype=np.int64, count=len(obs_all))
+        xyz = [t.xyz for t in track_vals]                                                     # :82-83
+    is_valid = lengths >= min_len                                                             # :66-68
     registered = np.array([img.is_registered for img in images], dtype=bool)                  # :70
     # :71-73, one batched matrix -> quaternion conversion; unregistered images get the identity row
     se3 = np.tile(np.array([0, 0, 0, 0, 0, 0, 1.0]), (len(images), 1))
@@ -121,7 +151,21 @@ def pack(cameras, images, tracks, options):
     remaining = np.array([i for i in range(camera_params.shape[1]) if i not in pp_indices])
     camera_pps = camera_params[:, pp_indices]
     camera_params = camera_params[:, remaining]
-    xyz = [t.xyz for t in track_vals]                                                         # :82-83
+    feats = [np.asarray(im.features).reshape(-1, 2) for im in images]
+    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])]).astype(np.int64)
+    feat_all = np.ascontiguousarray(np.concatenate(feats), dtype=np.float64) if feats else np.zeros((0, 2))
+    if got is not None:
+        # :85-113 in C: registered filter, feature gather, cheirality z > 0.1, torch.unique compaction
+        cp = np.ascontiguousarray(camera_params)
+        r = _packx.finish(obs_valid, lengths, int(min_len), registered.astype(np.uint8), feat_all, foff,
+                          np.ascontiguousarray(points_3d), cp, cp.shape[1])
+        points_2d = np.frombuffer(r[0], np.float64).reshape(-1, 2)
+        cam_inv, pt_inv = np.frombuffer(r[1], np.int64), np.frombuffer(r[2], np.int64)
+        unique_cameras, unique_points = np.frombuffer(r[3], np.int64), np.frombuffer(r[4], np.int64)
+        return PackedProblem(model, points_2d, cam_inv, pt_inv, np.ascontiguousarray(camera_pps[unique_cameras]),
+                             np.ascontiguousarray(camera_params[unique_cameras]),
+                             np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points,
+                             track_keys, remaining, pp_indices, track_vals)
     try:
         points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
         if points_3d.shape[0] != len(xyz):
@@ -147,9 +191,6 @@ def pack(cameras, images, tracks, options):
     keep = registered[img_id]
     if not keep.all():
         img_id, feat_id, tid = img_id[keep], feat_id[keep], tid[keep]
-    feats = [np.asarray(im.features).reshape(-1, 2) for im in images]
-    foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])]).astype(np.int64)
-    feat_all = np.ascontiguousarray(np.concatenate(feats), dtype=np.float64) if feats else np.zeros((0, 2))
     # one 16-byte gather per observation (a row of feat_all viewed as one complex128)
     points_2d = feat_all.view(np.complex128).reshape(-1)[foff[img_id] + feat_id].view(np.float64).reshape(-1, 2)
 
@@ -163,7 +204,7 @@ def pack(cameras, images, tracks, options):
                          np.ascontiguousarray(camera_pps[unique_cameras]),
                          np.ascontiguousarray(camera_params[unique_cameras]),
                          np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points, track_keys,
-                         remaining, pp_indices)
+                         remaining, pp_indices, track_vals)
 
 
 def update(cameras, images, tracks, packed, camera_params, points_3d):
@@ -175,8 +216,12 @@ def update(cameras, images, tracks, packed, camera_params, points_3d):
     full[:, packed.pp_indices] = packed.camera_pps
     mats = _pose_matrices(full[:, :7])
     keys = packed.track_keys
-    for orig, xyz in zip(packed.unique_points.tolist(), pts):
-        tracks[keys[orig]].xyz = xyz
+    if _packx is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2:
+        _packx.assign_xyz(list(tracks.values()) if packed.track_vals is None else packed.track_vals,
+                          np.ascontiguousarray(packed.unique_points, np.int64), pts)
+    else:
+        for orig, xyz in zip(packed.unique_points.tolist(), pts):
+            tracks[keys[orig]].xyz = xyz
     last = {}
     for i, image_id in enumerate(packed.unique_cameras.tolist()):
         image = images[image_id]

@@ -35,14 +35,15 @@ def quat_equal_up_to_sign(a, b, tol):
     return np.all(np.minimum(np.abs(a - b).max(-1), np.abs(a + b).max(-1)) < tol)
 
 
+@pytest.mark.parametrize("native", [True, False])
 @pytest.mark.parametrize("name", ["packing_config1", "packing_edge", "packing_edge_points_only"])
-def test_pack_matches_reference(golden_dir, name):
+def test_pack_matches_reference(golden_dir, name, native):
     g = np.load(os.path.join(golden_dir, name + ".npz"))
     # rebuild the scene with the parameter types tools/gen_golden.py used for that fixture
     kind = "np64list" if name == "packing_config1" else "pyfloat"
     cams, imgs, tracks = scene_from_fixture(g, kind)
     opts = dict(OPTS, optimize_poses=bool(g["out_optimize_poses"]))
-    pk = pack(cams, imgs, tracks, opts)
+    pk = pack(cams, imgs, tracks, opts, native=native)
     np.testing.assert_array_equal(pk.points_2d, g["out_points_2d"])
     np.testing.assert_array_equal(pk.camera_indices, g["out_camera_indices"])
     np.testing.assert_array_equal(pk.point_indices, g["out_point_indices"])
@@ -94,3 +95,42 @@ def test_update_writes_back(golden_dir):
     last = max(i for i, image_id in enumerate(pk.unique_cameras) if imgs[image_id].cam_id == 0)
     assert cams[0].params[0] == cp[last, 7]
     assert cams[0].params[2] == pk.camera_pps[last, 0]  # principal point re-inserted
+
+
+def _fields(pk):
+    return [pk.points_2d, pk.camera_indices, pk.point_indices, pk.camera_pps, pk.camera_params, pk.points_3d,
+            pk.unique_cameras, pk.unique_points]
+
+
+def test_native_pack_is_built_and_matches_numpy_path():
+    """The C packer (csrc/packx.c) is what pack() runs, and it gives bit-identical arrays and dtypes to the numpy
+    path on a synthetic scene with unregistered images, short tracks, points behind cameras, int32 observations and
+    float32 xyz (the layouts the reference's DB reader and TrackEngine produce); Track attributes it does not take
+    (a Python list) fall back to the numpy path."""
+    from instantsfm_amd.processors import bundle_adjustment as BA
+    from instantsfm_amd.synth import make_problem, to_scene
+    assert BA._packx is not None, "instantsfm_amd/_lib/_packx*.so not built (instantsfm_amd.build.build_packx)"
+    prob = make_problem(30, 1500, seed=3)
+    cams, imgs, tracks = to_scene(prob)
+    rng = np.random.default_rng(0)
+    for i in rng.choice(len(imgs), 3, replace=False):
+        imgs[i].is_registered = False
+    keys = list(tracks)
+    for k in rng.choice(len(keys), 40, replace=False):       # length-1 tracks
+        tracks[keys[k]].observations = tracks[keys[k]].observations[:1]
+    for k in rng.choice(len(keys), 40, replace=False):       # points behind the cameras
+        tracks[keys[k]].xyz = tracks[keys[k]].xyz * -50.0
+    for k in rng.choice(len(keys), 100, replace=False):      # int32 observations, float32 xyz
+        tracks[keys[k]].observations = tracks[keys[k]].observations.astype(np.int32)
+        tracks[keys[k]].xyz = tracks[keys[k]].xyz.astype(np.float32)
+    a, b = pack(cams, imgs, tracks, OPTS, native=True), pack(cams, imgs, tracks, OPTS, native=False)
+    assert a.points_2d.shape[0] < prob.n_obs
+    for x, y in zip(_fields(a), _fields(b)):
+        assert x.dtype == y.dtype and x.shape == y.shape
+        np.testing.assert_array_equal(x, y)
+    assert BA._packx.collect(list(tracks.values()), 2) is not None
+    tracks[keys[0]].observations = tracks[keys[0]].observations.tolist()
+    assert BA._packx.collect(list(tracks.values()), 2) is None
+    c = pack(cams, imgs, tracks, OPTS)
+    for x, y in zip(_fields(c), _fields(b)):
+        np.testing.assert_array_equal(x, y)
