@@ -3414,6 +3414,23 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd(&tl.vc, cd))) return fail(rc, "");
         if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
         if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
+        {
+            // cluster reduction of the CG's row partials by the last-arriving row of each cluster in k_tl_pspmv
+            // (INSFM_PC_CLUSTER=1; off by default): measured on config 3, k_tl_pc 9.7 -> 7.0 us but k_tl_pspmv
+            // 13.5 -> 18.7 us -- every workgroup waits for its write-through stores and for its counter add to
+            // return, and all 1000 rows run in one round, so the launch grows by that round trip
+            static const bool pc_cluster = [] { const char* e = std::getenv("INSFM_PC_CLUSTER"); return e && std::atoi(e) != 0; }();
+            if ((rc = upload(h, &ip, lab.data(), lab.size()))) return fail(rc, "");
+            tl.clab = ip;
+            tl.ccnt = nullptr;
+            if (pc_cluster) {
+                if ((rc = dalloc(h, (void**)&tl.ccnt, sizeof(int) * (size_t)nc))) return fail(rc, "");
+                if (hipMemsetAsync(tl.ccnt, 0, sizeof(int) * (size_t)nc, h->stream) != hipSuccess)
+                    return fail(INSFM_BA_EHIP, "ccnt clear");
+            }
+            if ((rc = dd(&tl.Rcl, (size_t)m))) return fail(rc, "");
+            if ((rc = dd(&tl.gcl, 3 * (size_t)nc))) return fail(rc, "");
+        }
         if ((rc = dd(&tl.rowR, (size_t)C * MC + 2))) return fail(rc, "");  // +2: k_tl_pc reads it in 16-B pairs
         if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
         {

@@ -36,8 +36,13 @@ struct TlBufs {
     double* Ztc;         // [C][D][MC] the same rows in cluster-member order (cpos)
     double* vc;          // [C][D] the vector k_tl_pc reads (r0 at setup, w after), rows in cluster-member order
     double* Rc;          // [m]   (debug) restriction
-    double* gd;          // [3C]  row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2  (k_tl_pspmv)
+    double* gd;          // [3][C] row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2 (k_tl_pspmv), rows in cluster-member order
     double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
+    // cluster reduction in k_tl_pspmv (nullptr: k_tl_pc reduces the row partials itself): the last-arriving row of a
+    // cluster sums its members' partials (members in camera order) into
+    int* ccnt;           // [nc] arrival counters (reset to 0 by the last arriver)
+    double* Rcl;         // [nc][MC] restriction Z~^T w per cluster
+    double* gcl;         // [3][nc] the scalar partials per cluster
     double* Oseg;        // [nseg][MC][MC] per (row, neighbour cluster) sums of Z~_i^T S~_ij Z~_j
     double* E;           // [ldE][ldE] coarse matrix padded to whole kGB blocks (pad: identity), inverted in place
     double* Einv;        // [m][m] compact E^-1 (k_tl_pc reads its cluster's rows)
@@ -46,6 +51,7 @@ struct TlBufs {
     const int* cl_ptr;   // [nc+1]
     const int* cl_cams;  // cluster members, ascending camera id
     const int* cpos;     // [C] position of camera i in cl_cams
+    const int* clab;     // [C] cluster of camera i
     const int* alone;    // [C] camera is alone in its cluster -> basis [I_D | 0]
     const int* sperm;    // [n_nbr] neighbour slots of each row ordered by (cluster of the neighbour, slot)
     const int4* seg;     // [nseg] (cluster, sorted begin, sorted end, own-cluster flag) per (row, neighbour cluster)
@@ -54,6 +60,13 @@ struct TlBufs {
     const int* ered_seg; // segment ids of each cluster pair, rows ascending
     int nc, m, maxmem, ldE;
 };
+
+// Hand-off of the row partials to the cluster's last-arriving workgroup inside one k_tl_pspmv launch: every partial is
+// stored write-through (sc1), the storing wave waits for its stores (vmcnt(0)) before its one agent-scope counter add,
+// and the last arriver reads them with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1: no L2 write-back, no
+// acquire).  Relaxed agent-scope atomic load / store lower to global_load / global_store ... sc1 on gfx950.
+__device__ __forceinline__ void st_sc1(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ double ld_sc1(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // ---- setup ---------------------------------------------------------------------------------------------------
 // One thread per (camera i, coarse column k): column k of G_i at the linearization point and Z~_i[:,k] = L_i^T G_i[:,k].
@@ -502,24 +515,36 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     // issue order), so that reduction overlaps the E^-1 / restriction batch still in flight
     // the first GK partials per thread are held in registers and summed at the scalar phase (a summing loop here
     // would wait for them before the batch below is issued); rows past GK * kPcThreads are summed there too
+    // with the cluster reduction (tl.ccnt) k_tl_pspmv's last arrivers left one record per cluster: nc scalar partials
+    // and the full restriction (m values) instead of C and C * MC row partials
+    const bool usecl = tl.ccnt != nullptr && !setup;
+    const double* gsrc = usecl ? tl.gcl : tl.gd;
+    const int gn = usecl ? tl.nc : C;
     constexpr int GK = 2;
     double ga0[GK], ga1[GK], ga2[GK];
 #pragma unroll
     for (int r = 0; r < GK; ++r) {
-        const int k = min(t + r * kPcThreads, C - 1);
-        ga0[r] = tl.gd[k]; ga1[r] = tl.gd[C + k]; ga2[r] = tl.gd[2 * C + k];
+        const int k = min(t + r * kPcThreads, gn - 1);
+        ga0[r] = gsrc[k]; ga1[r] = gsrc[gn + k]; ga2[r] = gsrc[2 * gn + k];
     }
     const int ih = max(it - 1, 0);
     const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
     double ev[UE];
     double2 lrv[UR2];  // restriction partials in 16-B pairs (rowR is 16-B aligned and padded by 2)
+    constexpr int URC = (kCoarseMax + kPcThreads - 1) / kPcThreads;
+    double rcv[URC];   // the cluster restriction (usecl)
     // branch-free: indices past the end are clamped to the last valid element (a load under a divergent branch is
     // waited for at the branch's join, which would serialize the batch)
 #pragma unroll
     for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kPcThreads, MC * m - 1)];
+    if (usecl) {
 #pragma unroll
-    for (int u = 0; u < UR2; ++u)
-        lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kPcThreads, (nlr0 - 1) / 2)];
+        for (int u = 0; u < URC; ++u) rcv[u] = tl.Rcl[min(t + u * kPcThreads, m - 1)];
+    } else {
+#pragma unroll
+        for (int u = 0; u < UR2; ++u)
+            lrv[u] = reinterpret_cast<const double2*>(tl.rowR)[min(t + u * kPcThreads, (nlr0 - 1) / 2)];
+    }
     const int tc = min(t / MC, tl.nc - 1);
     const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
     const int ne = e1 - e0;
@@ -543,8 +568,8 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
         double g0 = 0.0, g1 = 0.0, g2 = 0.0;
 #pragma unroll
         for (int r = 0; r < GK; ++r)
-            if (t + r * kPcThreads < C) { g0 += ga0[r]; g1 += ga1[r]; g2 += ga2[r]; }
-        for (int k = t + GK * kPcThreads; k < C; k += kPcThreads) { g0 += tl.gd[k]; g1 += tl.gd[C + k]; g2 += tl.gd[2 * C + k]; }
+            if (t + r * kPcThreads < gn) { g0 += ga0[r]; g1 += ga1[r]; g2 += ga2[r]; }
+        for (int k = t + GK * kPcThreads; k < gn; k += kPcThreads) { g0 += gsrc[k]; g1 += gsrc[gn + k]; g2 += gsrc[2 * gn + k]; }
         g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
         if (lane == 0) { red[0][wv] = g0; red[1][wv] = g1; red[2][wv] = g2; }
         __syncthreads();
@@ -593,17 +618,25 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
             const int q = t + u * kPcThreads;
             if (q < MC * m) EL[q] = ev[u];
         }
+        if (usecl) {
 #pragma unroll
-        for (int u = 0; u < UR2; ++u) {
-            const int q = 2 * (t + u * kPcThreads);
-            if (q < nlr0) LR[q] = lrv[u].x;
-            if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
+            for (int u = 0; u < URC; ++u) {
+                const int q = t + u * kPcThreads;
+                if (q < m) Rs[q] = rcv[u];
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < UR2; ++u) {
+                const int q = 2 * (t + u * kPcThreads);
+                if (q < nlr0) LR[q] = lrv[u].x;
+                if (q + 1 < nlr0) LR[q + 1] = lrv[u].y;
+            }
+            if (nlr0 > UR * kPcThreads) stage_lds<kPcThreads, 16>(LR + UR * kPcThreads, tl.rowR + UR * kPcThreads,
+                                                                    nlr0 - UR * kPcThreads);
         }
-        if (nlr0 > UR * kPcThreads) stage_lds<kPcThreads, 16>(LR + UR * kPcThreads, tl.rowR + UR * kPcThreads,
-                                                                nlr0 - UR * kPcThreads);
     }
     PCT(2)
-    if (use) {
+    if (use && !usecl) {
         // full restriction: entry (c', k) sums the row partials of cluster c' in ascending camera order (from LDS)
         for (int pass = 0; pass < np; ++pass) {
             const int r0 = pass * prows, r1 = min(C, r0 + prows);
@@ -621,6 +654,8 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
                 Rs[e] = v;
             }
         }
+    }
+    if (use) {
         __syncthreads();
         PCT(3)
         constexpr int KPW = (MC + kPcWaves - 1) / kPcWaves, LPL = (kCoarseMax + 63) / 64;
@@ -806,6 +841,7 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     double g2 = 0.0, rr = 0.0;
+    const int cp = tl.cpos[row];
     if (lane < D) {  // (L r)_a for the true-residual norm
         double lr = 0.0;
 #pragma unroll
@@ -815,10 +851,33 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     } else if (lane < D + MC) {  // restriction of w: sum_a Z~[a][k] w_a
 #pragma unroll
         for (int a = 0; a < D; ++a) rr += tailop[a] * sv[1][a];
-        tl.rowR[(size_t)tl.cpos[row] * MC + (lane - D)] = rr;
+        st_sc1(tl.rowR + (size_t)cp * MC + (lane - D), rr);
     }
     g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
-    if (lane == 0) { tl.gd[row] = g0; tl.gd[C + row] = g1; tl.gd[2 * C + row] = g2; }
+    if (lane == 0) { st_sc1(tl.gd + cp, g0); st_sc1(tl.gd + C + cp, g1); st_sc1(tl.gd + 2 * C + cp, g2); }
+    if (tl.ccnt == nullptr) return;
+    // the cluster's last-arriving row reduces its members' partials (fixed order: members ascending)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int c = tl.clab[row], e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
+    int last = 0;
+    if (lane == 0)
+        last = __hip_atomic_fetch_add(tl.ccnt + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e1 - e0 - 1;
+    if (__builtin_amdgcn_readfirstlane(last) == 0) return;
+    if (lane < MC + 3) {
+        const double* src = lane < MC ? tl.rowR + lane : tl.gd + (size_t)(lane - MC) * C;
+        const int step = lane < MC ? MC : 1;
+        double v = 0.0;
+        int e = e0;
+        for (; e + 4 <= e1; e += 4) {  // loads four at a time, adds in member order
+            const double v0 = ld_sc1(src + (size_t)e * step), v1 = ld_sc1(src + (size_t)(e + 1) * step);
+            const double v2 = ld_sc1(src + (size_t)(e + 2) * step), v3 = ld_sc1(src + (size_t)(e + 3) * step);
+            v += v0; v += v1; v += v2; v += v3;
+        }
+        for (; e < e1; ++e) v += ld_sc1(src + (size_t)e * step);
+        if (lane < MC) tl.Rcl[(size_t)c * MC + lane] = v;
+        else tl.gcl[(size_t)(lane - MC) * tl.nc + c] = v;
+    }
+    if (lane == 0) __hip_atomic_store(tl.ccnt + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace insfm

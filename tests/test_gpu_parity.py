@@ -524,3 +524,24 @@ def test_coarse_inverse_matches_numpy(m):
         rc = L.insfm_ba_debug_spd_inverse(m, ctypes.c_void_p(dev(En).data_ptr()), ctypes.c_void_p(Xd.data_ptr()),
                                           None, 0, None)
         assert rc == 0
+
+
+@pytest.mark.timeout(300)
+def test_pc_cluster_reduction_parity():
+    """The opt-in cluster reduction of the CG's row partials (INSFM_PC_CLUSTER=1: the last-arriving row of each cluster
+    in k_tl_pspmv sums its members' partials through write-through stores and one agent-scope counter; k_tl_pc then
+    reads one record per cluster) against the oracle on config-2 LM steps: same PCG iterations and trials, loss
+    1e-10, parameters 1e-9.  The variable is read once per process, hence the subprocess."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pc_cluster_check.py")], capture_output=True,
+                       text=True, timeout=280, env=dict(os.environ, INSFM_PC_CLUSTER="1"), cwd=repo)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["env"] == "1"
+    for s in out["steps"]:
+        assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
+        assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s
