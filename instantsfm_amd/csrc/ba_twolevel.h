@@ -322,10 +322,105 @@ __device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __res
     }
 }
 
-// In-place scalar Gauss-Jordan inversion of the SPD block in M (LDS) by wave 0 (lane r & 31 = row r; the pivot row is
-// broadcast by readlane), result back into M; every thread of the workgroup must call it.  Returns (in wave 0)
-// whether a pivot was not positive.
+// In-place scalar Gauss-Jordan inversion of the SPD block in M (LDS) by wave 0 (lane r & 31 = row r), result back into
+// M; every thread of the workgroup must call it.  Returns (in wave 0) whether a pivot was not positive.
+// GJ_PINV 0: the pivot row is broadcast by readlane (2 x 32 v_readlane per pivot); 1: lane p stores its row in LDS and
+// every lane reads it back (one 16-B read per column pair, all lanes the same address); 2: timing only (no inversion,
+// results wrong); 3: all 256 threads, four entries each, the matrix ping-ponged through LDS.  0, 1 and 3 perform the
+// same arithmetic in the same order.
+#ifndef GJ_PINV
+#define GJ_PINV 3
+#endif
 __device__ bool gj_invert_block(double (*M)[kGS]) {
+#if GJ_PINV == 2
+    __syncthreads();
+    return false;
+#elif GJ_PINV == 3
+    // all 256 threads: thread t owns row t / 8, columns 4 (t % 8) .. +3, in registers; per pivot every thread reads the
+    // pivot row's entries of its columns and its row's pivot-column entry from the LDS copy of the previous step and
+    // writes its updated entries to the other copy (ping-pong, one barrier per pivot)
+    static_assert(kGB == 32 && (kGB & 1) == 0, "256 threads = 32 rows x 8 column quads; an even pivot count ends in M");
+    __shared__ double Mb[kGB][kGS];
+    __syncthreads();
+    const int t = threadIdx.x, r = t >> 3, c0 = (t & 7) * 4;
+    double a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = M[r][c0 + j];
+    double(*src)[kGS] = M;
+    double(*dst)[kGS] = Mb;
+    bool bad = false;
+    for (int p = 0; p < kGB; ++p) {
+        double piv = src[p][p];
+        const double aip = src[r][p];
+        double pr[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pr[j] = src[p][c0 + j];
+        if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+        const double inv = 1.0 / piv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (c0 + j == p) {
+                a[j] = (r == p) ? inv : -aip * inv;
+            } else {
+                const double rpc = pr[j] * inv;
+                a[j] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[j]);
+            }
+            dst[r][c0 + j] = a[j];
+        }
+        __syncthreads();
+        double(*tmp)[kGS] = src;
+        src = dst;
+        dst = tmp;
+    }
+    return bad;  // (the same pivots in every thread)
+#elif GJ_PINV == 1
+    __shared__ __attribute__((aligned(16))) double prow[kGB];
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x, r = lane & 31;
+        double a[kGB];
+#pragma unroll
+        for (int c = 0; c < kGB; ++c) a[c] = M[r][c];
+#pragma unroll
+        for (int p = 0; p < kGB; ++p) {
+            if (lane == p) {
+#pragma unroll
+                for (int c = 0; c < kGB; c += 2) *reinterpret_cast<double2*>(&prow[c]) = make_double2(a[c], a[c + 1]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double pr[kGB];
+#pragma unroll
+            for (int c = 0; c < kGB; c += 2) {
+                const double2 v = *reinterpret_cast<const double2*>(&prow[c]);
+                pr[c] = v.x;
+                pr[c + 1] = v.y;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double piv = pr[p];
+            if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+            const double inv = 1.0 / piv;
+            const double aip = a[p];
+#pragma unroll
+            for (int c = 0; c < kGB; ++c) {
+                if (c == p) continue;
+                const double rpc = pr[c] * inv;
+                a[c] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[c]);
+            }
+            a[p] = (r == p) ? inv : -aip * inv;
+        }
+        if (lane < kGB) {
+#pragma unroll
+            for (int c = 0; c < kGB; ++c) M[lane][c] = a[c];
+        }
+    }
+    __syncthreads();
+    return bad;
+#else
     __syncthreads();
     bool bad = false;
     if (threadIdx.x < 64) {
@@ -354,6 +449,7 @@ __device__ bool gj_invert_block(double (*M)[kGS]) {
     }
     __syncthreads();
     return bad;
+#endif
 }
 
 // P_0^-1 (one workgroup): the equilibrated first pivot block.
