@@ -1689,6 +1689,7 @@ struct insfm_ba {
     int *sfree = nullptr, *osrc = nullptr;
     double *scl_cur = nullptr, *scl_new = nullptr, *ds = nullptr;
     std::vector<int> osrc_host;
+    std::vector<std::pair<const char*, double>> hmarks;  // INSFM_HOST_TRACE=2
 };
 
 namespace {
@@ -1784,6 +1785,16 @@ int allreduce_async(insfm_ba* h, double* buf, int64_t n) {
 
 void rec(insfm_ba* h, int k) {
     if (h->timing) (void)hipEventRecord(h->ev[k], h->stream);
+}
+
+// INSFM_HOST_TRACE=2: host timestamps of one LM step's API calls (labels + microseconds since the step began),
+// printed to stderr when the step ends -- where the host, not the GPU, sets the pace
+int host_trace_level() {
+    static const int v = [] { const char* e = std::getenv("INSFM_HOST_TRACE"); return e ? std::atoi(e) : 0; }();
+    return v;
+}
+void hmark(insfm_ba* h, const char* what) {
+    if (host_trace_level() >= 2) h->hmarks.emplace_back(what, wall_seconds());
 }
 
 // after a stream sync: add the device time between events a and b to phase `slot`
@@ -2196,7 +2207,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         k_gp_prep_cams<<<h->C, kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
                                                                      h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->Up,
                                                                      h->gpc);
-    } else if (h->Pl > 0)
+    } else if (h->Pl > 0 && (hmark(h, "point_prep"), true))
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
                                                                        h->Vinv, h->y, h->flags, h->cg.status, pts_local,
                                                                        h->schur_rc ? h->ptrec : nullptr);
@@ -2224,7 +2235,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         } else {
             rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
             if (rc) return rc;
+            hmark(h, "schur");
             if ((rc = side_drain(h))) return rc;  // what remains of the previous solve's side chain
+            hmark(h, "side drained");
             rec(h, 7);
             rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
             if (rc) return rc;
@@ -2245,7 +2258,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             return launch_err(h, "k_cg_factor/scale");
         });
         if (rc) return rc;
+        hmark(h, "factor/scale");
         if (h->tlon && (rc = run_tl_setup(h, cams))) return rc;
+        hmark(h, "tl setup");
         const int maxit = h->d.pcg_max_iter;
         const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
         int it = 0;
@@ -2316,6 +2331,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // and cost (finish_cost), the rest after the next solve's k_schur is enqueued (run_solve) -- issuing it
             // here would hold back k_cg_finish by the host time of every remaining launch
             const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
+            hmark(h, "cg converged");
             if (erc) return erc;
             if (htrace)
                 std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
@@ -2390,6 +2406,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         });
         if (rc) return rc;
         dcp = h->dc;
+        hmark(h, "cg_finish");
     }
     rec(h, 3);
     if (gpk) {
@@ -2420,6 +2437,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         return launch_err(h, "k_backsub_rc");
     });
     if (rc) return rc;
+    hmark(h, "backsub");
     if (backsub_w) {
         rc = with_model(h->model, [&](auto mc) -> int {
             constexpr int M = decltype(mc)::value;
@@ -2457,7 +2475,9 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->pub_dev, seq, ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
                                                h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
     if (int rc = launch_err(h, "k_publish")) return rc;
+    hmark(h, "publish");
     if (int rc = side_issue_while_busy(h)) return rc;
+    hmark(h, "side while busy");
     const unsigned* w = reinterpret_cast<const unsigned*>(h->pub_host + 8);
     // bounded like the CG poll: a device that neither publishes nor reports an error ends the step with EHIP
     static const double stall_s = 6.0 * cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
@@ -2484,6 +2504,7 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
         __builtin_ia32_pause();
 #endif
     }
+    hmark(h, "published");
     const volatile double* pv = h->pub_host;
     for (int k = 0; k < 5; ++k) h->host_res[k] = pv[k];
     h->trial_copied = copy;
@@ -2535,8 +2556,11 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         h->have_loss = true;
     }
     const double last = h->loss;
+    h->hmarks.clear();
+    hmark(h, "step");
     rec(h, 0);
     if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
+    hmark(h, "linearize enqueued");
     if (h->timing && (rc = lin_join(h))) return rc;  // (the phase split times both linearization kernels)
     rec(h, 1);
     double f = 1.0;
@@ -2617,6 +2641,12 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         st->coarse_used = h->coarse_used;
     }
     h->timing = false;
+    if (host_trace_level() >= 2 && !h->hmarks.empty()) {
+        hmark(h, "step end");
+        std::string line = "[insfm host2]";
+        for (auto& m : h->hmarks) line += " " + std::string(m.first) + "=" + std::to_string((int)(1e6 * (m.second - h->hmarks[0].second)));
+        std::fprintf(stderr, "%s\n", line.c_str());
+    }
     return 0;
 }
 
