@@ -106,16 +106,16 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* sh /* >= NV *
 }
 
 // Sum n partial records of NV doubles (record-major) in a fixed order; every thread gets the result.
-template <int NV>
+template <int NV, int NT = kThreads>
 __device__ __forceinline__ void sum_partials(const double* __restrict__ part, int n, double (&out)[NV], double* sh) {
     double v[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) v[k] = 0.0;
 #pragma unroll 8
-    for (int i = threadIdx.x; i < n; i += kThreads)  // unrolled: 8 loads in flight, the adds in order
+    for (int i = threadIdx.x; i < n; i += NT)  // unrolled: 8 loads in flight, the adds in order
 #pragma unroll
         for (int k = 0; k < NV; ++k) v[k] += part[(size_t)i * NV + k];
-    block_sum<NV>(v, sh);
+    block_sum<NV, NT>(v, sh);
 #pragma unroll
     for (int k = 0; k < NV; ++k) out[k] = v[k];
 }
@@ -1474,16 +1474,19 @@ __global__ __launch_bounds__(kCostThreads) void k_cost(int Nl, const int* __rest
 
 // result[0..4] = {loss, sum ||r||^2, gain_points, gain_cams, #non-PD point blocks}; fixed-order sums of the partials.
 // All five are summed across ranks, so every rank takes the same accept / reject / fail branch.
-__global__ __launch_bounds__(kThreads) void k_final(const double* __restrict__ cost_part, int ncost,
+// one 1024-thread workgroup (16 waves: four times the loads in flight of a 256-thread one; 11 -> 5 us on config 3's
+// ~40k partials)
+constexpr int kFinalThreads = 1024;
+__global__ __launch_bounds__(kFinalThreads) void k_final(const double* __restrict__ cost_part, int ncost,
                                                     const double* __restrict__ gp_part, int ngp,
                                                     const double* __restrict__ gc_part, int ngc, int* __restrict__ flags,
                                                     double* __restrict__ result) {
-    __shared__ double red[2 * kThreads];
+    __shared__ double red[2 * kFinalThreads / 64];
     double c2[2];
-    sum_partials<2>(cost_part, ncost, c2, red);
+    sum_partials<2, kFinalThreads>(cost_part, ncost, c2, red);
     double a[1], b[1];
-    if (gp_part) sum_partials<1>(gp_part, ngp, a, red); else a[0] = 0.0;
-    if (gc_part) sum_partials<1>(gc_part, ngc, b, red); else b[0] = 0.0;
+    if (gp_part) sum_partials<1, kFinalThreads>(gp_part, ngp, a, red); else a[0] = 0.0;
+    if (gc_part) sum_partials<1, kFinalThreads>(gc_part, ngc, b, red); else b[0] = 0.0;
     if (threadIdx.x == 0) {
         result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0];
         result[4] = (double)flags[0];
@@ -2518,7 +2521,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
         if (h->Nl > 0)
             k_gp_cost<<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, cams, pts_local, scl,
                                                              h->d.huber_delta, h->part_cost);
-        k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
+        k_final<<<1, kFinalThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
                                                h->n_gp, nullptr, 0, h->flags, h->result);
         int rc = launch_err(h, "k_gp_cost/k_final");
         if (rc) return rc;
@@ -2532,7 +2535,7 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
         if (h->Nl > 0)
             k_cost<M><<<h->n_cost, kCostThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
                                                              h->d.huber_delta, h->part_cost);
-        k_final<<<1, kThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
+        k_final<<<1, kFinalThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
                                                h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result);
         return launch_err(h, "k_cost/k_final");
     });
