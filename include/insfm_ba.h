@@ -8,7 +8,10 @@
  *   - the residual model `ReprojNonBatched.forward` = `reproject_funcs[model](points_3d[pi], pose[ci], pp[ci]) - points_2d`
  *     (bundle_adjustment.py:51-64, cost_function.py:32-208) and its TrackingTensor sparse Jacobian
  *     (bae.autograd.function, un-vendored)  -> fused into the library's linearize kernels;
- *   - `bae.utils.pysolvers.PCG` and the cuDSS sparse solve (un-vendored)  -> Schur complement + block-Jacobi PCG kernels;
+ *   - `bae.utils.pysolvers.PCG` and the cuDSS sparse solve (un-vendored)  -> explicit Schur complement on the camera
+ *     blocks + PCG kernels with the same relative-residual stopping rule; preconditioner `desc.precond`: 1 (default)
+ *     two-level = block-Jacobi + a camera-cluster coarse correction (similarity + intrinsic modes per cluster, the
+ *     build's choice), 0 = block-Jacobi only (the closest restatement of PCG(tol=1e-5));
  *   - `model.loss(input)` (pypose RobustModel, Huber kernel)  -> insfm_ba_cost().
  * Creation corresponds to the LM/model construction at bundle_adjustment.py:115-119 (packed inputs of :98-113).
  *
@@ -149,8 +152,9 @@ int insfm_ba_debug_solve(insfm_ba* h, double f);
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
 /* Device time per launch (us, hipEvents on the library stream) of `reps` back-to-back launches of one kernel on the
  * data of the last solve: which = 0 k_cg_iter (one block-Jacobi CG iteration), 1 k_schur, 2 one two-level CG
- * iteration (k_tl_update + k_tl_coarse + k_tl_spmv), 3 k_tl_spmv alone, 4 the two-level setup (basis .. E^-1).
- * Overwrites CG scratch state. */
+ * iteration (k_tl_pc + k_tl_pspmv), 3 k_tl_pspmv alone, 4 the two-level setup (k_tl_basis, the E build k_tl_erow +
+ * k_tl_ereduce, the Gauss-Jordan inversion k_gj_pinv0 + k_gj_step), 5 k_lin_points at the last trial's parameters
+ * (BA with stored W records only).  Overwrites CG scratch state. */
 int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch);
 /* Camera cluster labels [C] of the two-level preconditioner's coarse space (HOST out); returns the cluster count. */
 int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);

@@ -11,7 +11,8 @@
  *     bundle_adjustment.py:115-119 (TrustRegion(1e4, 1e10, 2, 1/16), PCG(tol=1e-5), Huber(delta), reject=30):
  *       * Huber kernel + Triggs corrector: w = 1 if sqrt(s) < delta else delta/sqrt(s); r~ = sqrt(w) r, J~ = sqrt(w) J
  *       * A = J~^T J~ with diag clamped to [1e-6, 1e32]; per trial diag *= (1 + damping) (cumulative)
- *       * damped system solved by explicit Schur complement on the camera blocks + block-Jacobi PCG
+ *       * damped system solved by explicit Schur complement on the camera blocks + PCG, preconditioned by block-Jacobi
+ *         (precond 0) or the two-level block-Jacobi + camera-cluster coarse correction (precond 1, the default)
  *         (relative residual tol, x0 = 0); back-substitution for points
  *       * SE3 left retraction X <- Exp([rho, phi]) X (pypose se3 = [rho, phi]); intrinsics and points +=
  *       * gain ratio (last - new) / -((J~D)^T (2 r~ + J~D)) -> TrustRegion radius update; reject while
