@@ -25,6 +25,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_PEAK_TFS = 78.6   # MI355X dense FP64 (MFMA = vector rate on gfx950)
 
 
 def w_record_doubles(D):
@@ -732,6 +733,8 @@ def main():
     us_tl_iter = eng.debug_time_kernel(2, 50) if tl else None
     us_tl_setup = eng.debug_time_kernel(4, 10) if tl else None
     us_lin = eng.debug_time_kernel(5, 20)
+    us_gj = eng.debug_time_kernel(6, 10) if tl else None     # the coarse inverse (k_gj_pinv0 + nB k_gj_step)
+    us_erow = eng.debug_time_kernel(7, 10) if tl else None   # the E build (k_tl_erow + k_tl_ereduce)
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
@@ -774,6 +777,27 @@ def main():
                        "timing": "back-to-back launches (hipEvents): for k_lin_points that is the sustained rate of its "
                                  "384-MB W write; in the step its trace time is shorter (profiles/r2_v6/kernel_stats.csv)"
                                  if kname == "k_lin_points" else "back-to-back launches (hipEvents)"})
+
+    # the side chain of the two-level preconditioner (runs on the side stream, overlapping the CG): the Gauss-Jordan
+    # inversion of E against the FP64 matrix peak (2 m^3 flops; its tile products are v_mfma_f64_16x16x4f64), the E
+    # build against HBM (it streams the full-row S~ copy once plus Z~)
+    if tl:
+        m = eng.coarse_dim()
+        nb_gj = (m + 31) // 32
+        flops = 2.0 * m ** 3
+        tfs = flops / (us_gj * 1e-6) / 1e12 if us_gj else 0.0
+        others.append({"kernel": f"k_gj_pinv0 + {nb_gj} x k_gj_step (coarse inverse, m = {m})", "bound": "mfma",
+                       "achieved": round(tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                       "frac": round(tfs / FP64_PEAK_TFS, 4), "avg_launch_us": round(us_gj / (nb_gj + 1), 3),
+                       "chain_us": round(us_gj, 2), "algorithmic_flops_per_chain": int(flops),
+                       "timing": "back-to-back chains (hipEvents), main stream alone; in the step it overlaps the CG"})
+        nbe = 2 * (nnzb - C) * D * (D + (D & 1)) * 8 + C * D * (D + 1) * 8
+        ach = nbe / (us_erow * 1e-6) / 1e9 if us_erow else 0.0
+        others.append({"kernel": "k_tl_erow + k_tl_ereduce (E build)", "bound": "hbm", "achieved": round(ach, 2),
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                       "avg_launch_us": round(us_erow, 3), "algorithmic_bytes_per_launch": int(nbe),
+                       "timing": "back-to-back builds with the full grid on the main stream (hipEvents); in the step it "
+                                 "runs on the side stream with at most 256 workgroups"})
 
     out = {
         "metric": "LM-BA iterations/sec (+ final reprojection RMSE)",

@@ -154,7 +154,8 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
  * data of the last solve: which = 0 k_cg_iter (one block-Jacobi CG iteration), 1 k_schur, 2 one two-level CG
  * iteration (k_tl_pc + k_tl_pspmv), 3 k_tl_pspmv alone, 4 the two-level setup (k_tl_basis, the E build k_tl_erow +
  * k_tl_ereduce, the Gauss-Jordan inversion k_gj_pinv0 + k_gj_step), 5 k_lin_points at the last trial's parameters
- * (BA with stored W records only).  Overwrites CG scratch state. */
+ * (BA with stored W records only), 6 the coarse inverse alone (k_gj_pinv0 + one k_gj_step per 32-wide block of E),
+ * 7 the E build alone (k_tl_erow + k_tl_ereduce).  Overwrites CG scratch state. */
 int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch);
 /* Camera cluster labels [C] of the two-level preconditioner's coarse space (HOST out); returns the cluster count. */
 int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);

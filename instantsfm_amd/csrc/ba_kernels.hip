@@ -3463,6 +3463,18 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             }
             if ((rc = dd(&tl.Rcl, (size_t)m))) return fail(rc, "");
             if ((rc = dd(&tl.gcl, 3 * (size_t)nc))) return fail(rc, "");
+            // atomic cluster sums of the CG partials (INSFM_PC_ATOMIC=0 disables): single GPU, non-deterministic mode
+            // only -- the replicated multi-rank CG needs bitwise-equal inputs on every rank
+            static const bool pc_atomic = [] { const char* e = std::getenv("INSFM_PC_ATOMIC"); return !e || std::atoi(e) != 0; }();
+            tl.Racc = nullptr;
+            tl.Gacc = nullptr;
+            if (pc_atomic && !pc_cluster && !desc->deterministic && desc->world_size <= 1 && !desc->allreduce) {
+                if ((rc = dd(&tl.Racc, 2 * (size_t)m))) return fail(rc, "");
+                if ((rc = dd(&tl.Gacc, 2 * 3 * (size_t)nc))) return fail(rc, "");
+                if (hipMemsetAsync(tl.Racc, 0, sizeof(double) * 2 * (size_t)m, h->stream) != hipSuccess ||
+                    hipMemsetAsync(tl.Gacc, 0, sizeof(double) * 6 * (size_t)nc, h->stream) != hipSuccess)
+                    return fail(INSFM_BA_EHIP, "Racc clear");
+            }
         }
         if ((rc = dd(&tl.rowR, (size_t)C * MC + 2))) return fail(rc, "");  // +2: k_tl_pc reads it in 16-B pairs
         if ((rc = dd(&tl.Oseg, segs.size() * MC * MC))) return fail(rc, "");
@@ -3675,11 +3687,23 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     // 2: one two-level CG iteration  3: k_tl_pspmv  4: the two-level setup  5: k_lin_points (overwrites W / V / g_p)
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
-    if (which >= 2 && which <= 4 && !h->tlon) return INSFM_BA_EINVAL;
+    if (((which >= 2 && which <= 4) || which == 6 || which == 7) && !h->tlon) return INSFM_BA_EINVAL;
     if (which == 5 && (h->kind != 0 || !h->W)) return INSFM_BA_EINVAL;
-    if (which < 0 || which > 5) return INSFM_BA_EINVAL;
+    if (which < 0 || which > 7) return INSFM_BA_EINVAL;
     if (int rc0 = side_flush(h)) return rc0;  // its pending E build / factorization must not interleave
     if (int rc0 = lin_join(h)) return rc0;
+    if (which == 2 && h->tl.Racc) {
+        // atomic cluster sums: iteration 1's k_tl_pc reads buffer 1 every repetition (its k_tl_pspmv adds into buffer
+        // 0, which the next repetition clears), so fill buffer 1 once from a k_tl_pspmv of iteration 0
+        HIPCHK(hipMemsetAsync(h->tl.Racc + h->tl.m, 0, sizeof(double) * h->tl.m, h->stream));
+        HIPCHK(hipMemsetAsync(h->tl.Gacc + 3 * h->tl.nc, 0, sizeof(double) * 3 * h->tl.nc, h->stream));
+        with_D(h->D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(0, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn,
+                                                                 h->Lf, h->cg, h->tl);
+            return 0;
+        });
+    }
     HIPCHK(hipEventRecord(h->ev[10], h->stream));
     int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
@@ -3694,6 +3718,11 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 if (!rc2) rc2 = run_tl_build(h, 0, h->stream);
                 for (int u = 0; u <= gj_steps(h->tl.m) && !rc2; ++u) rc2 = run_tl_gj_unit(h, 0, u, h->stream);
                 if (rc2) return rc2;
+            } else if (which == 6) {  // the coarse inverse alone: k_gj_pinv0 + nB x k_gj_step on slot 0's E
+                for (int u = 1; u <= gj_steps(h->tl.m) + 1; ++u)
+                    if (int rc2 = run_tl_gj_unit(h, 0, u - 1, h->stream)) return rc2;
+            } else if (which == 7) {  // the E build alone: k_tl_erow + k_tl_ereduce
+                if (int rc2 = run_tl_build(h, 0, h->stream)) return rc2;
             } else if (which == 5 && h->kind == 0 && h->W) {  // k_lin_points at the last trial's parameters
                 with_model(h->model, [&](auto mc) -> int {
                     constexpr int M = decltype(mc)::value;

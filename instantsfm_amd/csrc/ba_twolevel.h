@@ -43,6 +43,11 @@ struct TlBufs {
     int* ccnt;           // [nc] arrival counters (reset to 0 by the last arriver)
     double* Rcl;         // [nc][MC] restriction Z~^T w per cluster
     double* gcl;         // [3][nc] the scalar partials per cluster
+    // atomic cluster sums (single GPU, non-deterministic mode; nullptr otherwise): k_tl_pspmv adds each row's
+    // restriction and scalar partials into its cluster's entries with no-return f64 atomics, double-buffered by
+    // iteration parity (k_tl_pc of iteration i reads buffer i & 1 and clears buffer (i + 1) & 1 for k_tl_pspmv)
+    double* Racc;        // [2][m]
+    double* Gacc;        // [2][3][nc]
     double* Oseg;        // [nseg][MC][MC] per (row, neighbour cluster) sums of Z~_i^T S~_ij Z~_j
     double* E;           // [ldE][ldE] coarse matrix padded to whole kGB blocks (pad: identity), inverted in place
     double* Einv;        // [m][m] compact E^-1 (k_tl_pc reads its cluster's rows)
@@ -613,9 +618,11 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     // would wait for them before the batch below is issued); rows past GK * kPcThreads are summed there too
     // with the cluster reduction (tl.ccnt) k_tl_pspmv's last arrivers left one record per cluster: nc scalar partials
     // and the full restriction (m values) instead of C and C * MC row partials
-    const bool usecl = tl.ccnt != nullptr && !setup;
-    const double* gsrc = usecl ? tl.gcl : tl.gd;
+    const bool usea = tl.Racc != nullptr && !setup;
+    const bool usecl = (tl.ccnt != nullptr || usea) && !setup;
+    const double* gsrc = usea ? tl.Gacc + (size_t)(it & 1) * 3 * tl.nc : (usecl ? tl.gcl : tl.gd);
     const int gn = usecl ? tl.nc : C;
+    const double* rsrc = usea ? tl.Racc + (size_t)(it & 1) * tl.m : tl.Rcl;
     constexpr int GK = 2;
     double ga0[GK], ga1[GK], ga2[GK];
 #pragma unroll
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     for (int u = 0; u < UE; ++u) ev[u] = Einv[(size_t)c * MC * m + min(t + u * kPcThreads, MC * m - 1)];
     if (usecl) {
 #pragma unroll
-        for (int u = 0; u < URC; ++u) rcv[u] = tl.Rcl[min(t + u * kPcThreads, m - 1)];
+        for (int u = 0; u < URC; ++u) rcv[u] = rsrc[min(t + u * kPcThreads, m - 1)];
     } else {
 #pragma unroll
         for (int u = 0; u < UR2; ++u)
@@ -644,6 +651,12 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     const int tc = min(t / MC, tl.nc - 1);
     const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
     const int ne = e1 - e0;
+    if (tl.Racc != nullptr && blockIdx.x == 0) {  // clear the buffer this iteration's k_tl_pspmv adds into
+        double* R = tl.Racc + (size_t)((it + 1) & 1) * m;
+        double* G = tl.Gacc + (size_t)((it + 1) & 1) * 3 * tl.nc;
+        for (int q = t; q < m; q += kPcThreads) R[q] = 0.0;
+        for (int q = t; q < 3 * tl.nc; q += kPcThreads) G[q] = 0.0;
+    }
     if (st0 != 0 || ne < 0) return;  // (ne < 0 never holds: it makes the branch wait for the range loads as well)
     const bool use = okv != 0;
     if (setup && c == 0 && t == 0) {
@@ -947,9 +960,21 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     } else if (lane < D + MC) {  // restriction of w: sum_a Z~[a][k] w_a
 #pragma unroll
         for (int a = 0; a < D; ++a) rr += tailop[a] * sv[1][a];
-        st_sc1(tl.rowR + (size_t)cp * MC + (lane - D), rr);
+        if (tl.Racc == nullptr) st_sc1(tl.rowR + (size_t)cp * MC + (lane - D), rr);
     }
     g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+    if (tl.Racc != nullptr) {  // cluster sums by atomics (order varies run to run; single GPU, non-deterministic)
+        const int c = tl.clab[row], bsel = (it + 1) & 1;
+        if (lane >= D && lane < D + MC)
+            unsafeAtomicAdd(tl.Racc + (size_t)bsel * tl.m + (size_t)c * MC + (lane - D), rr);
+        if (lane == 0) {
+            double* G = tl.Gacc + (size_t)bsel * 3 * tl.nc;
+            unsafeAtomicAdd(G + c, g0);
+            unsafeAtomicAdd(G + tl.nc + c, g1);
+            unsafeAtomicAdd(G + 2 * tl.nc + c, g2);
+        }
+        return;
+    }
     if (lane == 0) { st_sc1(tl.gd + cp, g0); st_sc1(tl.gd + C + cp, g1); st_sc1(tl.gd + 2 * C + cp, g2); }
     if (tl.ccnt == nullptr) return;
     // the cluster's last-arriving row reduces its members' partials (fixed order: members ascending)

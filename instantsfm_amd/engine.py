@@ -240,13 +240,18 @@ class BundleAdjuster:
 
     def debug_time_kernel(self, which, reps=50):
         """Average device time (us) of `reps` back-to-back launches: 0 k_cg_iter, 1 k_schur, 2 one two-level CG
-        iteration (3 launches), 3 k_tl_spmv, 4 the two-level setup (6 launches)."""
+        iteration (k_tl_pc + k_tl_pspmv), 3 k_tl_pspmv, 4 the two-level setup (basis, E build, E^-1), 5 k_lin_points,
+        6 the coarse inverse alone (k_gj_pinv0 + the k_gj_step chain), 7 the E build alone (include/insfm_ba.h)."""
         us = ctypes.c_double()
         _capi.check(self._h, _capi.load().insfm_ba_debug_time_kernel(self._h, int(which), int(reps), ctypes.byref(us)))
         return us.value
 
     def nnzb(self):
         return int(_capi.load().insfm_ba_nnzb(self._h))
+
+    def coarse_dim(self):
+        """Dimension m of the two-level preconditioner's coarse matrix E (clusters x (D + 1)); 0 when it is off."""
+        return self.clusters()[1] * (self.D + 1)
 
     def clusters(self):
         """Camera cluster labels of the two-level preconditioner and the cluster count (0 when it is off)."""
