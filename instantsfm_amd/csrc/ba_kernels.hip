@@ -2116,7 +2116,12 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
                                                               h->cg, h->tl);
     }
-    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl, h->tl.Einv);
+    static const bool pc_cl = [] { const char* e = std::getenv("INSFM_PC_CL"); return !e || std::atoi(e) != 0; }();
+    if (h->tl.Racc && pc_cl)
+        k_tl_pc_cl<D><<<h->tl.nc, kPcThreads, 0, h->stream>>>(it, h->C, maxit, tol2, h->cg, h->tl, h->tl.Einv);
+    else
+        k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
+                                                                   h->tl.Einv);
     k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
                                                           h->cg, h->tl);
 }

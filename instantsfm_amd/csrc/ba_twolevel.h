@@ -810,6 +810,117 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
 #undef PCT
 }
 
+// k_tl_pc for iterations it >= 0 when the row partials arrive as per-cluster sums (tl.Racc: atomic cluster sums):
+// every wave reduces the nc scalar partials itself (no workgroup barrier before the recurrence scalars), each wave
+// keeps its coarse rows of E^-1 in registers, loaded column-per-lane (no LDS staging), and multiplies them with the
+// restriction loaded the same way; one barrier publishes the MC entries of y before m = w + Z~ y.  Same arithmetic
+// as k_tl_pc's cluster path up to the order of the scalar sums (here: a butterfly over the clusters in every wave).
+template <int D>
+__global__ __launch_bounds__(kPcThreads) void k_tl_pc_cl(int it, int C, int maxit, double tol2_rel, CgBufs cg,
+                                                         TlBufs tl, const double* __restrict__ Einv) {
+    constexpr int MC = D + 1, NW = kPcWaves, KPW = (MC + NW - 1) / NW, LPL = (kCoarseMax + 63) / 64;
+    __shared__ double y[MC];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int c = blockIdx.x, m = tl.m, nc = tl.nc;
+    const int st0 = cg.status[0];
+    const int okv = tl.ok[0];
+    const int e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
+    const double* G = tl.Gacc + (size_t)(it & 1) * 3 * nc;
+    const double* Rv = tl.Racc + (size_t)(it & 1) * m;
+    // every load that does not depend on another is issued before the first wait: the scalar partials, history,
+    // E^-1 rows (row k = wv + NW kk, column l = lane + 64 q), the restriction, the cluster's source rows
+    double ga[3] = {0.0, 0.0, 0.0};
+    constexpr int LNC = (kCoarseMax / 3 + 63) / 64;  // clusters per lane (nc <= m / 3)
+    double gl[3][LNC];
+#pragma unroll
+    for (int q = 0; q < LNC; ++q) {
+        const int l = min(lane + 64 * q, nc - 1);
+        gl[0][q] = G[l]; gl[1][q] = G[nc + l]; gl[2][q] = G[2 * nc + l];
+    }
+    const int ih = max(it - 1, 0);
+    const double h_alpha = cg.hist[2 * ih], h_gam = cg.hist[2 * ih + 1], h_bb = cg.hist[2 * (maxit + 1)];
+    double ev[KPW][LPL], rv[LPL];
+#pragma unroll
+    for (int kk = 0; kk < KPW; ++kk) {
+        const int k = min(wv + NW * kk, MC - 1);
+#pragma unroll
+        for (int q = 0; q < LPL; ++q) ev[kk][q] = Einv[((size_t)c * MC + k) * m + min(lane + 64 * q, m - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < LPL; ++q) rv[q] = Rv[min(lane + 64 * q, m - 1)];
+    const int ne = e1 - e0;
+    if (blockIdx.x == 0) {  // clear the buffer this iteration's k_tl_pspmv adds into
+        double* Rn = tl.Racc + (size_t)((it + 1) & 1) * m;
+        double* Gn = tl.Gacc + (size_t)((it + 1) & 1) * 3 * nc;
+        for (int q = t; q < m; q += kPcThreads) Rn[q] = 0.0;
+        for (int q = t; q < 3 * nc; q += kPcThreads) Gn[q] = 0.0;
+    }
+    if (st0 != 0 || ne < 0) return;
+    const bool use = okv != 0;
+    // recurrence scalars, in every wave (the same butterfly, so the same doubles everywhere)
+#pragma unroll
+    for (int q = 0; q < LNC; ++q)
+        if (lane + 64 * q < nc) { ga[0] += gl[0][q]; ga[1] += gl[1][q]; ga[2] += gl[2][q]; }
+    const double gam = wave_sum(ga[0]), del = wave_sum(ga[1]), rho = wave_sum(ga[2]);
+    const int i = it;
+    const double bb = (i == 0) ? rho : h_bb;
+    int done = 0;
+    double alpha = 0.0;
+    if (rho <= tol2_rel * bb || i >= maxit) {
+        done = 1;
+    } else {
+        const double bev = (i == 0) ? 0.0 : gam / h_gam;
+        const double den = (i == 0) ? del : del - bev * gam / h_alpha;
+        if (!(den > 0.0)) done = 2;
+        else alpha = gam / den;
+    }
+    if (blockIdx.x == 0 && t == 0) {
+        if (done) {
+            cg.status[1] = i;
+            __threadfence();
+            cg.status[0] = done;
+        } else {
+            cg.hist[2 * i] = alpha;
+            cg.hist[2 * i + 1] = gam;
+            if (i == 0) cg.hist[2 * (maxit + 1)] = bb;
+        }
+        if (cg.prog) {
+            if (done) {
+                __hip_atomic_store(cg.prog + 2, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(cg.prog + 1, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                __hip_atomic_store(cg.prog + 0, i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    if (done) return;
+    if (use) {
+#pragma unroll
+        for (int kk = 0; kk < KPW; ++kk) {
+            double sy = 0.0;
+#pragma unroll
+            for (int q = 0; q < LPL; ++q)
+                if (lane + 64 * q < m) sy += ev[kk][q] * rv[q];
+            const double v = wave_sum(sy);
+            const int k = wv + NW * kk;
+            if (lane == 0 && k < MC) y[k] = v;
+        }
+    }
+    __syncthreads();
+    for (int e = t; e < ne * D; e += kPcThreads) {
+        const size_t idx = (size_t)tl.cl_cams[e0 + e / D] * D + e % D;
+        double v = tl.vc[(size_t)e0 * D + e];
+        if (use) {
+            const double* Z = tl.Ztc + ((size_t)e0 * D + e) * MC;
+            double sz = 0.0;
+#pragma unroll
+            for (int k = 0; k < MC; ++k) sz += Z[k] * y[k];
+            v += sz;
+        }
+        cg.s[1][idx] = v;
+    }
+}
+
 // One camera row per 512-thread workgroup: the product with S~ (row-contiguous Sn stream), the row's vector updates
 // and its partials for the next iteration (setup: w0 = S~ u0 and the partials of iteration 0).
 // NT threads per workgroup: at 256, the 1000 rows of config 3 (4 waves each) are all resident at once at <= 128 VGPRs.
