@@ -2053,13 +2053,15 @@ int side_drain(insfm_ba* h) {
     return rc;
 }
 
-// Side-chain schedule.  0 (default): a lagged solve's chain is issued from the CG poll loop while the host waits
-// (E build and inversion overlap the CG); what the CG leaves unissued is issued while the host waits for the trial
-// cost, the rest right after the next solve's k_schur is enqueued.  1: nothing is issued from the poll loop -- the
-// whole chain overlaps back-substitution, the cost, the next linearization and k_schur instead of the CG.  The lag rule is the same in
-// both (the next solve's k_cg_scale / k_tl_basis wait for the E build; its CG waits for the factorization).
-// Measured on config 3: the CG gets 10 % faster under 1, linearization and k_schur slower by about as much
-// (INSFM_SIDE_SCHED=1 selects it).
+// Side-chain schedule (INSFM_SIDE_SCHED).  0 (default, round 3): the whole chain of a lagged solve is issued at
+// its setup, right after the basis -- the host is then ~0.6 ms ahead of the GPU (k_schur has not even started), so
+// the ~20 launches cost the GPU nothing, the chain still starts when the basis is done and overlaps the CG, and the
+// CG poll loop has nothing but CG launches to issue (no extra iterations queued past convergence for it).
+// 2 (round 2's default): the chain is issued piecemeal from the CG poll loop while the host waits; what the CG leaves
+// unissued is issued while the host waits for the trial cost, the rest right after the next solve's k_schur.
+// 1: nothing is issued from the poll loop -- the whole chain overlaps back-substitution, the cost, the next
+// linearization and k_schur instead of the CG.  The lag rule is the same in all three (the next solve's
+// k_cg_scale / k_tl_basis wait for the E build; its CG waits for the factorization).
 int side_sched() {
     static const int v = [] { const char* e = std::getenv("INSFM_SIDE_SCHED"); return e ? std::atoi(e) : 0; }();
     return v;
@@ -2093,7 +2095,7 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
     h->tl_fresh = false;
     h->side_slot = slot;
     h->side_next = 0;
-    if (use == slot && (rc = side_drain(h))) return rc;
+    if ((use == slot || side_sched() == 0) && (rc = side_drain(h))) return rc;
     // a lagged solve's coarse inverse normally finished long ago: a completed event needs no wait marker in the main
     // queue (each one idles it a few us); INSFM_FACT_WAIT=1 always queues the wait
     static const bool always_wait = [] { const char* e = std::getenv("INSFM_FACT_WAIT"); return e && std::atoi(e) != 0; }();
@@ -2307,7 +2309,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             if ((rc = enqueue(0, enq))) return rc;
             CgPoll poll;
             poll.enq = enq;
-            poll.extra_ahead = (h->side_slot >= 0 && side_sched() == 0) ? kSideAhead : 0;
+            poll.extra_ahead = (h->side_slot >= 0 && side_sched() == 2) ? kSideAhead : 0;
             static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
             int erc = 0;
             const int pr = cg_poll(
@@ -2322,7 +2324,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                     // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax.  While
                     // side units remain, two more CG iterations are kept queued: a side launch can hold the host
                     // for longer than two iterations take on the GPU
-                    if (h->side_slot >= 0 && side_sched() == 0) {
+                    if (h->side_slot >= 0 && side_sched() == 2) {
                         const double t0 = htrace ? wall_seconds() : 0.0;
                         const int r = side_issue(h);
                         if (htrace) { const double dt = wall_seconds() - t0; t_side += dt; m_side = std::max(m_side, dt); ++n_side; }
