@@ -1,8 +1,11 @@
 """COLMAP database reader -- drop-in for ``instantsfm/controllers/data_reader.py:11-120`` (``PathInfo``, ``ReadData``,
 ``ReadColmapDatabase``).  Host code over sqlite3 (stdlib): the same query, the same filters (invalid match indices,
 NULL match blobs, invalid two-view configurations), the same id remapping to list indices and the same return value
-``(view_graph, cameras, images, feature_name)``.  Depth reading (``ReadDepths``) needs cv2 and is off the path.
+``(view_graph, cameras, images, feature_name)``.  ``ReadDepthsIntoFeatures`` / ``ReadDepths`` (:122-144) read
+ScanNet-style 16-bit depth PNGs with the framework's own PNG reader (``utils.png``; the reference uses cv2) and
+sample them at the features (``utils.depth_sample``).
 """
+import glob
 import os
 import time
 
@@ -11,6 +14,8 @@ import numpy as np
 from ..scene.defs import (Camera, CameraModelId, ConfigurationType, Ids2PairId, Image, ImagePair, PairId2IdsInversed,
                           ViewGraph)
 from ..utils.database import COLMAPDatabase, blob_to_array
+from ..utils.depth_sample import sample_depths
+from ..utils.png import read_png_gray
 
 _INVALID_CONFIGS = (ConfigurationType.UNDEFINED, ConfigurationType.DEGENERATE, ConfigurationType.WATERMARK,
                     ConfigurationType.MULTIPLE)
@@ -110,3 +115,26 @@ def ReadColmapDatabase(path):
     except Exception:
         feature_name = 'colmap'  # no (or an empty) feature_name table: a COLMAP-produced database
     return view_graph, cameras, images, feature_name
+
+
+def ReadDepthsIntoFeatures(path, cameras, images, depths=None):
+    """data_reader.py:122-134: the depth maps of ``path`` (``ReadDepths``), sampled at every feature of every image
+    (nearest, ``utils.depth_sample``) into ``image.depths`` (float32, 0 where the feature lies outside the image);
+    returns the [N, H, W] float32 maps, which ``SolveGlobalMapper(..., depths=...)`` takes.  Image i uses map i (the
+    sorted file order) and its camera's width / height.  ``depths``: maps already in memory (skips the file read).
+    One vectorized sample per image instead of the reference's per-feature loop; same values (tests/test_depth.py)."""
+    if depths is None:
+        depths = ReadDepths(path)
+    for image in images:
+        camera = cameras[image.cam_id]
+        feats = np.asarray(image.features).reshape(-1, 2)
+        d, _ = sample_depths(depths[image.id], feats, camera.width, camera.height)
+        image.depths = d.astype(np.float32)
+    return depths
+
+
+def ReadDepths(path):
+    """data_reader.py:136-144: every ``*.png`` of ``path`` in sorted order, 16-bit millimetres -> float32 metres,
+    stacked [N, H, W] (the maps must share one size, as ``np.array`` requires in the reference)."""
+    maps = [read_png_gray(f).astype(np.float32) / 1000.0 for f in sorted(glob.glob(os.path.join(path, '*.png')))]
+    return np.array(maps, dtype=np.float32)
