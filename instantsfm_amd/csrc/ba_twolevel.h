@@ -331,10 +331,11 @@ __device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __res
 // M; every thread of the workgroup must call it.  Returns (in wave 0) whether a pivot was not positive.
 // GJ_PINV 0: the pivot row is broadcast by readlane (2 x 32 v_readlane per pivot); 1: lane p stores its row in LDS and
 // every lane reads it back (one 16-B read per column pair, all lanes the same address); 2: timing only (no inversion,
-// results wrong); 3: all 256 threads, four entries each, the matrix ping-ponged through LDS.  0, 1 and 3 perform the
-// same arithmetic in the same order.
+// results wrong); 3: all 256 threads, four entries each, the matrix ping-ponged through LDS; 4: one wave, 16 entries
+// per lane, pivot row / column through LDS without a workgroup barrier.  0, 1, 3 and 4 perform the same arithmetic in
+// the same order.
 #ifndef GJ_PINV
-#define GJ_PINV 3
+#define GJ_PINV 4
 #endif
 __device__ bool gj_invert_block(double (*M)[kGS]) {
 #if GJ_PINV == 2
@@ -378,6 +379,59 @@ __device__ bool gj_invert_block(double (*M)[kGS]) {
         dst = tmp;
     }
     return bad;  // (the same pivots in every thread)
+#elif GJ_PINV == 4
+    // one wave: lane l holds row l & 31, columns 16 (l >> 5) .. +15 in registers.  Per pivot p the two lanes of row p
+    // publish it and every lane of the half holding column p publishes its column-p entry through LDS; the wave reads
+    // back what it needs.  LDS requests of one wave complete in order, so a wave-level fence replaces the workgroup
+    // barrier of variant 3 (the other three waves wait at the closing barrier); the pivot buffers alternate by parity.
+    static_assert(kGB == 32, "64 lanes = 32 rows x 2 column halves");
+    __shared__ __attribute__((aligned(16))) double prow[2][kGB];
+    __shared__ __attribute__((aligned(16))) double pcol[2][kGB];
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, r = l & 31, h = l >> 5, cb = 16 * h;
+        double a[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = M[r][cb + j];
+#pragma unroll
+        for (int p = 0; p < kGB; ++p) {
+            const int par = p & 1, hp = p >> 4, jp = p & 15;
+            if (r == p) {
+#pragma unroll
+                for (int j = 0; j < 16; j += 2)
+                    *reinterpret_cast<double2*>(&prow[par][cb + j]) = make_double2(a[j], a[j + 1]);
+            }
+            if (h == hp) pcol[par][r] = a[jp];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double pr[16];
+#pragma unroll
+            for (int j = 0; j < 16; j += 2) {
+                const double2 v = *reinterpret_cast<const double2*>(&prow[par][cb + j]);
+                pr[j] = v.x;
+                pr[j + 1] = v.y;
+            }
+            double piv = prow[par][p];
+            const double aip = pcol[par][r];
+            if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+            const double inv = 1.0 / piv;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (cb + j == p) {
+                    a[j] = (r == p) ? inv : -aip * inv;
+                } else {
+                    const double rpc = pr[j] * inv;
+                    a[j] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) M[r][cb + j] = a[j];
+    }
+    __syncthreads();
+    return bad;
 #elif GJ_PINV == 1
     __shared__ __attribute__((aligned(16))) double prow[kGB];
     __syncthreads();
@@ -478,9 +532,34 @@ __global__ __launch_bounds__(256) void k_gj_step(int k, int nB, int ld, int m, c
     const size_t k0 = (size_t)k * kGB, i0 = (size_t)i * kGB, j0 = (size_t)j * kGB;
     const int R = (w >> 1) * 16, Cc = (w & 1) * 16;
     const double* ds = first ? d : nullptr;   // equilibrate while reading E (step 0)
-    for (int e = t; e < kGB * kGB; e += 256) Ps[e / kGB][e % kGB] = Pin[e];
-    if (j != k) gj_stage(Bk, X, ld, k0, j0, ds);
-    if (i != k) gj_stage(Ci, X, ld, i0, k0, ds);
+    // Every load of the step is issued before the first one is used (P^-1, X_kj, X_ik: 4 entries each per thread at
+    // (row (t >> 5) + 8 q, column t & 31); X_ij: this lane's 4 accumulator entries), so the step waits for one global
+    // latency instead of one per staged entry (a load-then-store loop retires its loads one at a time).
+    const bool upd = i != k && j != k;
+    const int sr = t >> 5, sc = t & 31;
+    double pv[4], bv[4], cv[4], xv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        pv[q] = Pin[(sr + 8 * q) * kGB + sc];
+        bv[q] = j != k ? X[(k0 + sr + 8 * q) * ld + j0 + sc] : 0.0;
+        cv[q] = i != k ? X[(i0 + sr + 8 * q) * ld + k0 + sc] : 0.0;
+        xv[q] = upd ? X[(i0 + R + (lane >> 4) + 4 * q) * ld + j0 + Cc + (lane & 15)] : 0.0;
+    }
+    if (ds) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const size_t rk = k0 + sr + 8 * q, ri = i0 + sr + 8 * q;
+            bv[q] = bv[q] * ds[rk] * ds[j0 + sc];
+            cv[q] = cv[q] * ds[ri] * ds[k0 + sc];
+            xv[q] = xv[q] * ds[i0 + R + (lane >> 4) + 4 * q] * ds[j0 + Cc + (lane & 15)];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        Ps[sr + 8 * q][sc] = pv[q];
+        Bk[sr + 8 * q][sc] = bv[q];
+        Ci[sr + 8 * q][sc] = cv[q];
+    }
     __syncthreads();
     gj_acc_t acc = {0.0, 0.0, 0.0, 0.0};
     if (i == k && j == k) {
@@ -497,12 +576,7 @@ __global__ __launch_bounds__(256) void k_gj_step(int k, int nB, int ld, int m, c
         for (int q = 0; q < 4; ++q) Bk[R + (lane >> 4) + 4 * q][Cc + (lane & 15)] = acc[q];
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const size_t r = i0 + R + (lane >> 4) + 4 * q, cc = j0 + Cc + (lane & 15);
-            double v = X[r * ld + cc];
-            if (ds) v = v * ds[r] * ds[cc];
-            acc[q] = v;
-        }
+        for (int q = 0; q < 4; ++q) acc[q] = xv[q];
         acc = gj_tile_mfma(Ci, Bk, acc, -1.0, lane, w);               // ... Y_ij = X_ij - X_ik (P^-1 X_kj)
     }
     const bool last = k == nB - 1;
