@@ -23,6 +23,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <unordered_map>
 #include <string>
 #include <thread>
 #include <type_traits>
@@ -1527,6 +1530,59 @@ __global__ __launch_bounds__(kThreads) void k_derive_cm(int Nl, const int* __res
     }
 }
 
+// Upper block pattern of S and the co-visibility weights on the device (create, single rank; the host pass in create
+// is the multi-rank / INSFM_PATTERN_HOST=1 path and gives the same lists): one workgroup per camera row i counts, in
+// LDS, for every camera j the (observation of i, observation of j) pairs sharing a track, walking each own
+// observation's upper partners [ustart, track end) exactly like k_schur.  `off` null: cnt[i] = #{j > i with pairs};
+// else the j > i in increasing order and their pair counts go to nb / wt from off[i] (the second pass recounts).
+constexpr int kPatternMaxC = 16384;  // the row's counters in <= 64 KB of LDS
+__global__ __launch_bounds__(256) void k_pattern(int C, const int* __restrict__ cam_ptr, const int* __restrict__ cam_obs,
+                                                 const int* __restrict__ ustart, const int* __restrict__ ptl,
+                                                 const int* __restrict__ pt_ptr, const int* __restrict__ cam,
+                                                 int* __restrict__ cnt, const int* __restrict__ off, int* __restrict__ nb,
+                                                 int* __restrict__ wt) {
+    extern __shared__ int acc[];  // [C]
+    __shared__ int wsum[4];
+    const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int j = t; j < C; j += 256) acc[j] = 0;
+    __syncthreads();
+    for (int e = cam_ptr[i] + t; e < cam_ptr[i + 1]; e += 256) {
+        const int o = cam_obs[e];
+        const int q1 = pt_ptr[ptl[o] + 1];
+        for (int q = ustart[o]; q < q1; ++q) {
+            const int j = cam[q];
+            if (j != i) atomicAdd(&acc[j], 1);  // (the run of camera i itself: the observation and its duplicates)
+        }
+    }
+    __syncthreads();
+    if (!off) {
+        int c = 0;
+        for (int j = i + 1 + t; j < C; j += 256) c += acc[j] > 0;
+        for (int d = 32; d > 0; d >>= 1) c += __shfl_xor(c, d);
+        if (lane == 0) wsum[w] = c;
+        __syncthreads();
+        if (t == 0) cnt[i] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        return;
+    }
+    int base = off[i];
+    for (int j0 = i + 1; j0 < C; j0 += 256) {  // ordered compaction, 256 columns at a time
+        const int j = j0 + t;
+        const int v = j < C ? acc[j] : 0;
+        const unsigned long long bal = __ballot(v > 0);
+        if (lane == 0) wsum[w] = __popcll(bal);
+        __syncthreads();
+        int wo = 0;
+        for (int k = 0; k < w; ++k) wo += wsum[k];
+        if (v > 0) {
+            const int at = base + wo + __popcll(bal & ((1ull << lane) - 1));
+            nb[at] = j;
+            wt[at] = v;
+        }
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+}
+
 __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) {
     const int t = threadIdx.x;
     if (t < 4) flags[t] = 0;
@@ -1706,15 +1762,104 @@ namespace {
         }                                                                                         \
     } while (0)
 
+// Process-wide cache of the device buffers of destroyed handles.  TorchBA creates a handle per Solve (the mapper
+// solves 4-5 times per reconstruction), and freeing config 3's ~1 GB of buffers took ~7 ms per destroy (hipFree
+// synchronizes the device) plus the allocations of the next create.  insfm_ba_destroy waits for the handle's streams
+// and parks its buffers here; dalloc takes the smallest parked buffer of at least the requested size and at most
+// twice it.  Bounded by INSFM_DEVICE_CACHE_MB (default 16384; 0 disables it): beyond that, buffers are freed.
+struct DeviceCache {
+    std::mutex m;
+    std::multimap<size_t, void*> free;  // size -> pointer
+    size_t bytes = 0;
+    std::unordered_map<void*, size_t> size_of;  // every pointer dalloc handed out (cached or fresh)
+};
+DeviceCache& device_cache() {
+    static DeviceCache* c = new DeviceCache();  // (never destroyed: buffers may be parked until process exit)
+    return *c;
+}
+size_t device_cache_cap() {
+    static const size_t v = [] {
+        const char* e = std::getenv("INSFM_DEVICE_CACHE_MB");
+        return (size_t)(e ? std::max(0LL, std::atoll(e)) : 16384LL) << 20;
+    }();
+    return v;
+}
+
+// INSFM_DEVICE_POISON=1 (diagnostic): every buffer dalloc hands out is first filled with 0xff bytes (NaN doubles,
+// -1 ints), so a read of something never written shows up instead of reading a fresh allocation's zero pages.
+bool device_poison() {
+    static const bool v = [] { const char* e = std::getenv("INSFM_DEVICE_POISON"); return e && *e == '1'; }();
+    return v;
+}
+
 int dalloc(insfm_ba* h, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
+    bytes = (bytes + 255) & ~(size_t)255;
+    DeviceCache& c = device_cache();
+    bool hit = false;
+    {
+        std::lock_guard<std::mutex> lk(c.m);
+        auto it = c.free.lower_bound(bytes);
+        if (it != c.free.end() && it->first <= 2 * bytes) {
+            *p = it->second;
+            c.bytes -= it->first;
+            c.free.erase(it);
+            hit = true;
+        }
+    }
+    if (hit) {
+        h->allocs.push_back(*p);
+        if (device_poison()) (void)hipMemset(*p, 0xff, bytes);
+        return 0;
+    }
     hipError_t e = hipMalloc(p, bytes);
+    if (e == hipErrorOutOfMemory) {  // give the parked buffers back and try once more
+        std::vector<void*> drop;
+        {
+            std::lock_guard<std::mutex> lk(c.m);
+            for (auto& kv : c.free) drop.push_back(kv.second);
+            for (void* q : drop) c.size_of.erase(q);
+            c.free.clear();
+            c.bytes = 0;
+        }
+        for (void* q : drop) (void)hipFree(q);
+        (void)hipGetLastError();
+        e = hipMalloc(p, bytes);
+    }
     if (e != hipSuccess) {
         h->err = std::string("hipMalloc(") + std::to_string(bytes) + ") failed: " + hipGetErrorString(e);
         return INSFM_BA_ENOMEM;
     }
+    {
+        std::lock_guard<std::mutex> lk(c.m);
+        c.size_of[*p] = bytes;
+    }
     h->allocs.push_back(*p);
+    if (device_poison()) (void)hipMemset(*p, 0xff, bytes);
     return 0;
+}
+
+// the handle's buffers back to the cache (the caller has synchronized every stream that used them)
+void dfree_all(insfm_ba* h) {
+    DeviceCache& c = device_cache();
+    const size_t cap = device_cache_cap();
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> lk(c.m);
+        for (void* q : h->allocs) {
+            auto it = c.size_of.find(q);
+            const size_t sz = it == c.size_of.end() ? 0 : it->second;
+            if (sz == 0 || c.bytes + sz > cap) {
+                if (it != c.size_of.end()) c.size_of.erase(it);
+                drop.push_back(q);
+            } else {
+                c.free.emplace(sz, q);
+                c.bytes += sz;
+            }
+        }
+    }
+    for (void* q : drop) (void)hipFree(q);
+    h->allocs.clear();
 }
 
 template <typename T>
@@ -2691,7 +2836,11 @@ const char* insfm_ba_last_error(const insfm_ba* h) { return h ? h->err.c_str() :
 void insfm_ba_destroy(insfm_ba* h) {
     if (!h) return;
     if (h->side) (void)side_flush(h);
-    for (void* p : h->allocs) (void)hipFree(p);
+    // every stream that may still use the buffers, before they are parked for the next handle
+    for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux})
+        if (st) (void)hipStreamSynchronize(st);
+    if (!h->stream) (void)hipDeviceSynchronize();
+    dfree_all(h);
     if (h->host_res) (void)hipHostFree(h->host_res);
     if (h->prog_host) (void)hipHostFree(h->prog_host);
     if (h->pub_host) (void)hipHostFree(h->pub_host);
@@ -2840,14 +2989,118 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         pcount_sort(pool, Nl, C, byk.data(), [&](int o) { return lcam[o]; }, cobs, cptr);
     }
     tick("camera-major lists");
-    // global camera-major list (identical on every rank), then the co-visibility graph and the upper block pattern in
-    // one pass: per camera i, every other camera j sharing a track, with the number of (obs of i, obs of j) pairs
-    // sharing a track (the two-level clustering's weights); the pattern row of i is i, then the neighbours j > i
+    // the per-observation arrays go to the device now: the block pattern below is derived there (single rank)
+    int rc;
+    if (kind == 1) {
+        nivec<double> tl((size_t)3 * Nl);
+        nivec<int> sl(Nl);
+        pool.ranges(Nl, [&](int, long long a, long long b) {
+            for (long long o = a; o < b; ++o) {
+                for (int k = 0; k < 3; ++k) tl[3 * (size_t)o + k] = obs[3 * (size_t)lsrc[o] + k];
+                sl[o] = sfree_in ? (sfree_in[lsrc[o]] != 0) : 1;
+            }
+        });
+        if ((rc = upload(h, &h->trans, tl.data(), tl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->sfree, sl.data(), sl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->fcam, cpar, (size_t)C))) return fail(rc, "");
+        if ((rc = upload(h, &h->osrc, lsrc.data(), lsrc.size()))) return fail(rc, "");
+        h->osrc_host.assign(lsrc.begin(), lsrc.end());
+        auto dd1 = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
+        if ((rc = dd1(&h->gobs, (size_t)Nl * kGO))) return fail(rc, "");
+        if ((rc = dd1(&h->Up, (size_t)C * 9))) return fail(rc, "");
+        if ((rc = dd1(&h->VY, (size_t)std::max(Pl, 1) * kVY))) return fail(rc, "");
+        if ((rc = dd1(&h->gpc, (size_t)C * 3))) return fail(rc, "");
+        if ((rc = dd1(&h->scl_cur, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dd1(&h->scl_new, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dd1(&h->ds, (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    } else {
+        nivec<double> uvl((size_t)2 * Nl);
+        pool.ranges(Nl, [&](int, long long a, long long b) {
+            for (long long o = a; o < b; ++o) {
+                uvl[2 * (size_t)o] = obs[2 * (size_t)lsrc[o]];
+                uvl[2 * (size_t)o + 1] = obs[2 * (size_t)lsrc[o] + 1];
+            }
+        });
+        if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
+        if ((rc = upload(h, &h->pp, cpar, (size_t)2 * C))) return fail(rc, "");
+    }
+    if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->cam_ptr, cptr.data(), cptr.size()))) return fail(rc, "");
+    if ((rc = upload(h, &h->cam_obs, cobs.data(), cobs.size()))) return fail(rc, "");
+    // derived on the device from the four arrays above instead of uploaded (88 of 140 MB for config 3):
+    // per observation its track and the start of its upper partners; per camera-major entry the Schur descriptor and
+    // (BA) the linearization's point / uv gathers
+    if ((rc = dalloc(h, (void**)&h->ptl, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if ((rc = dalloc(h, (void**)&h->ustart, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if ((rc = dalloc(h, (void**)&h->sdesc, sizeof(int4) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    if (kind != 1) {
+        if ((rc = dalloc(h, (void**)&h->cm_pt, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+        if ((rc = dalloc(h, (void**)&h->cm_uv, sizeof(double) * 2 * (size_t)std::max(Nl, 1)))) return fail(rc, "");
+    }
+    if (Pl > 0) k_derive_tracks<<<cdiv(Pl, kThreads), kThreads, 0, h->stream>>>(Pl, h->pt_ptr, h->cam, h->ptl, h->ustart);
+    if (Nl > 0)
+        k_derive_cm<<<cdiv(Nl, kThreads), kThreads, 0, h->stream>>>(Nl, h->cam_obs, h->ptl, h->ustart, h->pt_ptr,
+                                                                    kind != 1 ? h->uv : nullptr, h->sdesc, h->cm_pt,
+                                                                    h->cm_uv);
+    if ((rc = launch_err(h, "k_derive"))) return fail(rc, "");
+    tick("uploads (observations)");
+    // The upper block pattern of S (row i: i, then the cameras j > i sharing a track) and the co-visibility graph (per
+    // camera every other camera sharing a track, weighted by the number of (obs of i, obs of j) pairs sharing one:
+    // the two-level clustering's weights).  Single rank: on the device (k_pattern, two passes), the lower half of the
+    // graph transposed from the upper on the host.  Multi-rank (every rank needs the global pattern, and holds only its
+    // shard's observations on the device) or INSFM_PATTERN_HOST=1: one host pass over the global camera-major list.
     std::vector<int> gcptr;
-    nivec<int> gcpt;  // the point of every observation, camera-major
-    pcount_sort(pool, N, C, nullptr, [&](int i) { return cam_idx[i]; }, gcpt, gcptr, [&](int i) { return pt_idx[i]; });
     CovisGraph g;
     std::vector<int> rptr(C + 1, 0), cols;
+    static const bool pattern_host = [] { const char* e = std::getenv("INSFM_PATTERN_HOST"); return e && *e == '1'; }();
+    const bool gpu_pattern = !pattern_host && Pl == P && o0 == 0 && Nl == N && C <= kPatternMaxC && Nl > 0;
+    std::vector<int> upw;  // (device pattern) the pair count of every upper block, indexed like cols
+    if (gpu_pattern) {
+        gcptr = cptr;  // (single rank: the local camera-major list is the global one)
+        // (scratch from dalloc: a hipFree here would synchronize the device; it goes back with the handle's buffers)
+        int *dcnt = nullptr, *doff = nullptr, *dnb = nullptr, *dwt = nullptr;
+        const size_t lds = sizeof(int) * (size_t)C;
+        std::vector<int> ulen(C), uoff(C + 1, 0);
+        if ((rc = dalloc(h, (void**)&dcnt, sizeof(int) * (size_t)C))) return fail(rc, "");
+        if ((rc = dalloc(h, (void**)&doff, sizeof(int) * (size_t)(C + 1)))) return fail(rc, "");
+        hipError_t e = hipSuccess;
+        {
+            k_pattern<<<C, 256, lds, h->stream>>>(C, h->cam_ptr, h->cam_obs, h->ustart, h->ptl, h->pt_ptr, h->cam, dcnt,
+                                                  nullptr, nullptr, nullptr);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(ulen.data(), dcnt, sizeof(int) * (size_t)C, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        for (int i = 0; i < C && e == hipSuccess; ++i) uoff[i + 1] = uoff[i] + ulen[i];
+        const int U = uoff[C];
+        std::vector<int> unb(std::max(U, 1)), uwt(std::max(U, 1));
+        if (e == hipSuccess && ((rc = dalloc(h, (void**)&dnb, sizeof(int) * (size_t)std::max(U, 1))) ||
+                                (rc = dalloc(h, (void**)&dwt, sizeof(int) * (size_t)std::max(U, 1)))))
+            return fail(rc, "");
+        if (e == hipSuccess) e = hipMemcpyAsync(doff, uoff.data(), sizeof(int) * (size_t)(C + 1), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) {
+            k_pattern<<<C, 256, lds, h->stream>>>(C, h->cam_ptr, h->cam_obs, h->ustart, h->ptl, h->pt_ptr, h->cam, nullptr,
+                                                  doff, dnb, dwt);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && U > 0) e = hipMemcpyAsync(unb.data(), dnb, sizeof(int) * (size_t)U, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess && U > 0) e = hipMemcpyAsync(uwt.data(), dwt, sizeof(int) * (size_t)U, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("k_pattern: ") + hipGetErrorString(e));
+        for (int i = 0; i < C; ++i) rptr[i + 1] = rptr[i] + 1 + ulen[i];
+        cols.resize(rptr[C]);
+        upw.assign(rptr[C], 0);
+        for (int i = 0; i < C; ++i) {
+            cols[rptr[i]] = i;
+            for (int k = 0; k < ulen[i]; ++k) {
+                cols[rptr[i] + 1 + k] = unb[uoff[i] + k];
+                upw[rptr[i] + 1 + k] = uwt[uoff[i] + k];
+            }
+        }
+    } else {
+    nivec<int> gcpt;  // the point of every observation, camera-major (global)
+    pcount_sort(pool, N, C, nullptr, [&](int i) { return cam_idx[i]; }, gcpt, gcptr, [&](int i) { return pt_idx[i]; });
     {
         const int T = pool.size();
         std::vector<std::vector<int>> pnb(T);
@@ -2895,6 +3148,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             }
         });
     }
+    }
     h->nnzb = rptr[C];
     std::vector<int> brow(h->nnzb);
     for (int i = 0; i < C; ++i)
@@ -2912,6 +3166,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 locol[k] = i;
                 loblk[k] = e;
             }
+    }
+    if (gpu_pattern) {  // the graph: per row the lower neighbours (transposed, ascending), then the upper ones
+        g.ptr.assign(C + 1, 0);
+        for (int i = 0; i < C; ++i) g.ptr[i + 1] = g.ptr[i] + (lop[i + 1] - lop[i]) + (rptr[i + 1] - rptr[i] - 1);
+        g.nb.resize(g.ptr[C]);
+        g.w.resize(g.ptr[C]);
+        for (int i = 0; i < C; ++i) {
+            int k = g.ptr[i];
+            for (int q = lop[i]; q < lop[i + 1]; ++q, ++k) { g.nb[k] = locol[q]; g.w[k] = upw[loblk[q]]; }
+            for (int e2 = rptr[i] + 1; e2 < rptr[i + 1]; ++e2, ++k) { g.nb[k] = cols[e2]; g.w[k] = upw[e2]; }
+        }
     }
     tick("block pattern + covisibility");
     // flattened CG neighbour list per row: upper blocks then lower (transposed) ones; pos_up/pos_lo give each upper
@@ -3125,60 +3390,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
     }
 
-    int rc;
-    if (kind == 1) {
-        nivec<double> tl((size_t)3 * Nl);
-        nivec<int> sl(Nl);
-        pool.ranges(Nl, [&](int, long long a, long long b) {
-            for (long long o = a; o < b; ++o) {
-                for (int k = 0; k < 3; ++k) tl[3 * (size_t)o + k] = obs[3 * (size_t)lsrc[o] + k];
-                sl[o] = sfree_in ? (sfree_in[lsrc[o]] != 0) : 1;
-            }
-        });
-        if ((rc = upload(h, &h->trans, tl.data(), tl.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->sfree, sl.data(), sl.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->fcam, cpar, (size_t)C))) return fail(rc, "");
-        if ((rc = upload(h, &h->osrc, lsrc.data(), lsrc.size()))) return fail(rc, "");
-        h->osrc_host.assign(lsrc.begin(), lsrc.end());
-        auto dd1 = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
-        if ((rc = dd1(&h->gobs, (size_t)Nl * kGO))) return fail(rc, "");
-        if ((rc = dd1(&h->Up, (size_t)C * 9))) return fail(rc, "");
-        if ((rc = dd1(&h->VY, (size_t)std::max(Pl, 1) * kVY))) return fail(rc, "");
-        if ((rc = dd1(&h->gpc, (size_t)C * 3))) return fail(rc, "");
-        if ((rc = dd1(&h->scl_cur, (size_t)std::max(Nl, 1)))) return fail(rc, "");
-        if ((rc = dd1(&h->scl_new, (size_t)std::max(Nl, 1)))) return fail(rc, "");
-        if ((rc = dd1(&h->ds, (size_t)std::max(Nl, 1)))) return fail(rc, "");
-    } else {
-        nivec<double> uvl((size_t)2 * Nl);
-        pool.ranges(Nl, [&](int, long long a, long long b) {
-            for (long long o = a; o < b; ++o) {
-                uvl[2 * (size_t)o] = obs[2 * (size_t)lsrc[o]];
-                uvl[2 * (size_t)o + 1] = obs[2 * (size_t)lsrc[o] + 1];
-            }
-        });
-        if ((rc = upload(h, &h->uv, uvl.data(), uvl.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->pp, cpar, (size_t)2 * C))) return fail(rc, "");
-    }
-    if ((rc = upload(h, &h->cam, lcam.data(), lcam.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->pt_ptr, lptr.data(), lptr.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->cam_ptr, cptr.data(), cptr.size()))) return fail(rc, "");
-    if ((rc = upload(h, &h->cam_obs, cobs.data(), cobs.size()))) return fail(rc, "");
-    // derived on the device from the four arrays above instead of uploaded (88 of 140 MB for config 3):
-    // per observation its track and the start of its upper partners; per camera-major entry the Schur descriptor and
-    // (BA) the linearization's point / uv gathers
-    if ((rc = dalloc(h, (void**)&h->ptl, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-    if ((rc = dalloc(h, (void**)&h->ustart, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-    if ((rc = dalloc(h, (void**)&h->sdesc, sizeof(int4) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-    if (kind != 1) {
-        if ((rc = dalloc(h, (void**)&h->cm_pt, sizeof(int) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-        if ((rc = dalloc(h, (void**)&h->cm_uv, sizeof(double) * 2 * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-    }
-    if (Pl > 0) k_derive_tracks<<<cdiv(Pl, kThreads), kThreads, 0, h->stream>>>(Pl, h->pt_ptr, h->cam, h->ptl, h->ustart);
-    if (Nl > 0)
-        k_derive_cm<<<cdiv(Nl, kThreads), kThreads, 0, h->stream>>>(Nl, h->cam_obs, h->ptl, h->ustart, h->pt_ptr,
-                                                                    kind != 1 ? h->uv : nullptr, h->sdesc, h->cm_pt,
-                                                                    h->cm_uv);
-    if ((rc = launch_err(h, "k_derive"))) return fail(rc, "");
     if (kind != 1) {
         std::vector<int> lb(1, 0);
         for (int p = 0; p < Pl; ++p)  // close the run before a track that would overflow it

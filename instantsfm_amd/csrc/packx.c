@@ -126,8 +126,9 @@ static int get_buf(PyObject* o, Py_buffer* b, Py_ssize_t itemsize, const char* w
 /* finish(obs int64[n,2], lengths int64[T], min_len, registered uint8[I], features float64[F,2], foff int64[I+1],
  *        points float64[T,3], poses float64[I,stride], stride)
  *   -> (points_2d float64[m,2], camera_indices int64[m], point_indices int64[m], unique_cameras int64[], unique_points
- *       int64[]) as bytearrays (writable): the observations of registered images whose point lies in front of the camera
- *       (bundle_adjustment.py:85-113). */
+ *       int64[], camera_indices int32[m], point_indices int32[m]) as bytearrays (writable): the observations of
+ *       registered images whose point lies in front of the camera (bundle_adjustment.py:85-113); the int32 copies are
+ *       what insfm_ba_create takes (written in the same pass instead of a numpy conversion per Solve). */
 static PyObject* finish(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *o_obs, *o_len, *o_reg, *o_feat, *o_foff, *o_pts, *o_pose;
@@ -221,10 +222,12 @@ static PyObject* finish(PyObject* self, PyObject* args) {
         PyObject *b2d = PyByteArray_FromStringAndSize(NULL, 16 * m), *bci = PyByteArray_FromStringAndSize(NULL, 8 * m);
         PyObject *bpi = PyByteArray_FromStringAndSize(NULL, 8 * m), *buc = PyByteArray_FromStringAndSize(NULL, 8 * nuc);
         PyObject* bup = PyByteArray_FromStringAndSize(NULL, 8 * nup);
+        PyObject *bc32 = PyByteArray_FromStringAndSize(NULL, 4 * m), *bp32 = PyByteArray_FromStringAndSize(NULL, 4 * m);
         int64_t* cmap = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(nI > 0 ? nI : 1));
         int64_t* pmap = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(nT > 0 ? nT : 1));
-        if (!b2d || !bci || !bpi || !buc || !bup || !cmap || !pmap) {
+        if (!b2d || !bci || !bpi || !buc || !bup || !bc32 || !bp32 || !cmap || !pmap) {
             Py_XDECREF(b2d); Py_XDECREF(bci); Py_XDECREF(bpi); Py_XDECREF(buc); Py_XDECREF(bup);
+            Py_XDECREF(bc32); Py_XDECREF(bp32);
             PyMem_Free(cmap); PyMem_Free(pmap); PyMem_Free(ok);
             if (!PyErr_Occurred()) PyErr_NoMemory();
             goto done;
@@ -236,6 +239,8 @@ static PyObject* finish(PyObject* self, PyObject* args) {
         double* o2d = (double*)PyByteArray_AS_STRING(b2d);
         int64_t* oci = (int64_t*)PyByteArray_AS_STRING(bci);
         int64_t* opi = (int64_t*)PyByteArray_AS_STRING(bpi);
+        int32_t* oc32 = (int32_t*)PyByteArray_AS_STRING(bc32);
+        int32_t* op32 = (int32_t*)PyByteArray_AS_STRING(bp32);
         #pragma omp parallel num_threads(nth)
         {
             const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
@@ -249,12 +254,15 @@ static PyObject* finish(PyObject* self, PyObject* args) {
                 o2d[2 * w + 1] = fp[1];
                 oci[w] = cmap[im];
                 opi[w] = pmap[tid[k]];
+                oc32[w] = (int32_t)cmap[im];
+                op32[w] = (int32_t)pmap[tid[k]];
                 ++w;
             }
         }
         PyMem_Free(cmap); PyMem_Free(pmap); PyMem_Free(ok);
-        res = PyTuple_Pack(5, b2d, bci, bpi, buc, bup);
+        res = PyTuple_Pack(7, b2d, bci, bpi, buc, bup, bc32, bp32);
         Py_DECREF(b2d); Py_DECREF(bci); Py_DECREF(bpi); Py_DECREF(buc); Py_DECREF(bup);
+        Py_DECREF(bc32); Py_DECREF(bp32);
     }
 done:
     PyMem_Free(tid); PyMem_Free(cnt); PyMem_Free(pc); PyMem_Free(pp);

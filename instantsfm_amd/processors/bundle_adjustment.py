@@ -96,7 +96,8 @@ class PackedProblem:
     """What TorchBA.Solve hands the LM (reference :98-126): compacted, track-major arrays + bookkeeping."""
 
     def __init__(self, model, points_2d, camera_indices, point_indices, camera_pps, camera_params, points_3d,
-                 unique_cameras, unique_points, track_keys, remaining_indices, pp_indices, track_vals=None):
+                 unique_cameras, unique_points, track_keys, remaining_indices, pp_indices, track_vals=None,
+                 indices_i32=None):
         self.model = model
         self.points_2d = points_2d
         self.camera_indices = camera_indices
@@ -110,6 +111,13 @@ class PackedProblem:
         self.remaining_indices = remaining_indices
         self.pp_indices = pp_indices
         self.track_vals = track_vals  # the Track objects in track_keys order (update() writes xyz through it)
+        # int32 copies of (camera_indices, point_indices) for insfm_ba_create (native pack), else made on demand
+        self.indices_i32 = indices_i32
+
+    def indices32(self):
+        if self.indices_i32 is None:
+            self.indices_i32 = (self.camera_indices.astype(np.int32), self.point_indices.astype(np.int32))
+        return self.indices_i32
 
 
 def pack(cameras, images, tracks, options, native=True):
@@ -165,7 +173,8 @@ def pack(cameras, images, tracks, options, native=True):
         return PackedProblem(model, points_2d, cam_inv, pt_inv, np.ascontiguousarray(camera_pps[unique_cameras]),
                              np.ascontiguousarray(camera_params[unique_cameras]),
                              np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points,
-                             track_keys, remaining, pp_indices, track_vals)
+                             track_keys, remaining, pp_indices, track_vals,
+                             (np.frombuffer(r[5], np.int32), np.frombuffer(r[6], np.int32)))
     try:
         points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
         if points_3d.shape[0] != len(xyz):
@@ -255,7 +264,8 @@ class TorchBA:
             return
         # the engine wants track-major observations: point_indices from np.unique are already nondecreasing because
         # observations were gathered track by track (reference :88-96), so no reordering is needed.
-        eng = BundleAdjuster(packed.model.value, packed.points_2d, packed.camera_indices, packed.point_indices,
+        cam32, pt32 = packed.indices32()
+        eng = BundleAdjuster(packed.model.value, packed.points_2d, cam32, pt32,
                              packed.camera_pps, packed.camera_params.shape[0], packed.points_3d.shape[0],
                              device=self.device, optimize_poses=opts['optimize_poses'],
                              huber_delta=opts['thres_loss_function'], deterministic=opts.get('deterministic', False),

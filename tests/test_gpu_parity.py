@@ -263,8 +263,8 @@ def test_two_level_step_with_coarse_active_and_fewer_iterations():
     assert abs(res[1][0] - res[0][0]) / res[0][0] < 1e-6, res
 
 
-@pytest.mark.parametrize("model", (2, 4, 6))
-def test_repeated_solves_lagged_coarse_inverse(model):
+@pytest.mark.parametrize("model,det", [(2, False), (4, False), (6, False), (6, True)])
+def test_repeated_solves_lagged_coarse_inverse(model, det):
     """Consecutive solves on one engine under the lag rule: the first solve after a linearization runs with the coarse
     inverse of the previous solve (factorized on the side stream while that CG ran), retries at the same
     linearization use their own.  Every solve matches the oracle's (same rule): iterations, and dc in residual space
@@ -277,13 +277,16 @@ def test_repeated_solves_lagged_coarse_inverse(model):
     the damping: cond(S) ~ 5e13, and a lagged solve's max-abs difference is set by rounding, not by the algorithm --
     the oracle against itself built with other rounding moves 4e-6 there while agreeing to 1.6e-11 in residual space
     (tests/test_oracle.py::test_pcg_rounding_sensitivity_lives_in_the_near_null_space).  So for D = 16 lagged solves
-    the residual-space and energy bounds are the parity check (max-abs is reported)."""
+    the residual-space and energy bounds are the parity check (max-abs is reported).  In the default mode the Schur
+    build's LDS-atomic order varies from run to run, and so does that residual: 27 runs of this test on the MI355X
+    (profiles/r3_v8/lag_*.log) gave 1e-10 .. 1.3e-8 for the lagged D = 16 solves (energy <= 1.2e-6), hence 5e-8
+    there; deterministic=1 (fixed-order sums) pins the same solves at the 1e-8 bound."""
     prob = make_problem(30, 800, seed=5, model=model)
     cams, pts = prob.cams_init.copy(), prob.points_init.copy()
     ref = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
     ref.linearize(cams, pts)
     for rep in range(3):
-        eng, ora = engines(prob, cluster_size=6)
+        eng, ora = engines(prob, cluster_size=6, deterministic=det)
         # (relinearize?, damping factor): LM-like sequences -- fresh trials change f by <= 16x, retries by more
         for k, (relin, f) in enumerate([(1, 1 + 1e-4), (1, 1 + 5e-5), (1, 1 + 8e-4), (0, 1 + 1.3e-2), (0, 1.2),
                                         (1, 1 + 6e-4)]):
@@ -299,9 +302,8 @@ def test_repeated_solves_lagged_coarse_inverse(model):
             print(f"model {model} rep {rep} solve {k}: {d}")
             lagged = relin and k > 0
             if lagged and eng.D == 16:
-                # round 3 on the MI355X: resid 2e-11 .. 5e-10, energy 3e-8 .. 2.3e-7 over 3 reps (k_schur's LDS-atomic
-                # order varies from run to run); the oracle against its own FMA-contracted build: 1.6e-11 / 2.6e-8
-                assert d["resid"] < 1e-8 and d["energy"] < 1e-5, (rep, k, d)
+                # the oracle against its own FMA-contracted build: 1.6e-11 / 2.6e-8 (see the docstring)
+                assert d["resid"] < (1e-8 if det else 5e-8) and d["energy"] < 1e-5, (rep, k, d)
             else:
                 assert d["resid"] < 1e-9 and d["energy"] < 1e-6, (rep, k, d)
             if not lagged:
@@ -527,6 +529,28 @@ def test_coarse_inverse_matches_numpy(m):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.timeout(300)
+def test_device_block_pattern_matches_host_pass():
+    """insfm_ba_create derives the Schur block pattern and the co-visibility graph on the device (k_pattern) on a
+    single rank; the host pass (multi-rank, INSFM_PATTERN_HOST=1) must give the same result: the same block count,
+    the same two-level clusters (which read the graph's weights) and bitwise the same deterministic LM steps, on
+    config 2, a scene with duplicated observations and one with a camera that sees nothing."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for host in ("0", "1"):
+        p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pattern_check.py")], capture_output=True,
+                           text=True, timeout=140, env=dict(os.environ, INSFM_PATTERN_HOST=host), cwd=repo)
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+        outs.append(json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]))
+    assert outs[0]["env"] == "0" and outs[1]["env"] == "1"
+    assert outs[0]["scenes"] == outs[1]["scenes"]
+    assert set(outs[0]["scenes"]) == {"config2", "duplicates", "empty_camera"}
+
+
 def test_pc_cluster_reduction_parity():
     """The opt-in cluster reduction of the CG's row partials (INSFM_PC_CLUSTER=1: the last-arriving row of each cluster
     in k_tl_pspmv sums its members' partials through write-through stores and one agent-scope counter; k_tl_pc then

@@ -128,6 +128,13 @@ def test_native_pack_is_built_and_matches_numpy_path():
     for x, y in zip(_fields(a), _fields(b)):
         assert x.dtype == y.dtype and x.shape == y.shape
         np.testing.assert_array_equal(x, y)
+    # the int32 index copies insfm_ba_create takes: written by the C packer, made on demand on the numpy path
+    assert a.indices_i32 is not None and b.indices_i32 is None
+    for x, y in zip(a.indices32(), b.indices32()):
+        assert x.dtype == np.int32 and y.dtype == np.int32
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(a.indices32()[0], a.camera_indices)
+    np.testing.assert_array_equal(a.indices32()[1], a.point_indices)
     assert BA._packx.collect(list(tracks.values()), 2) is not None
     tracks[keys[0]].observations = tracks[keys[0]].observations.tolist()
     assert BA._packx.collect(list(tracks.values()), 2) is None

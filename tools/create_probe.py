@@ -33,7 +33,8 @@ def main():
         t0 = time.perf_counter()
         pk = BA.pack(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)
         t1 = time.perf_counter()
-        eng = BundleAdjuster(pk.model.value, pk.points_2d, pk.camera_indices, pk.point_indices, pk.camera_pps,
+        cam32, pt32 = pk.indices32()
+        eng = BundleAdjuster(pk.model.value, pk.points_2d, cam32, pt32, pk.camera_pps,
                              pk.camera_params.shape[0], pk.points_3d.shape[0], device=dev)
         t2 = time.perf_counter()
         cams = torch.from_numpy(pk.camera_params).to(dev)
