@@ -3247,13 +3247,25 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->max_chunk = maxc;
     if (kind == 0 && desc->allreduce_async && (desc->world_size > 1 || desc->allreduce) && desc->exchange_chunks > 1 &&
         desc->optimize_poses) {
-        // chunk boundaries at rows with ~equal block counts, and the first work item of each boundary row
+        // chunk boundaries at rows where the block counts follow a geometric series (chunk c ~ ratio^c of the
+        // blocks, INSFM_XCHUNK_RATIO in (0, 4], default 1 = equal chunks; DESIGN.md section 5 for why decreasing
+        // chunks do not pay: the all-reduces run back to back on one stream), and the first work item of each
+        // boundary row
         const int K = std::min(desc->exchange_chunks, C);
+        static const double ratio = [] {
+            const char* e = std::getenv("INSFM_XCHUNK_RATIO");
+            const double v = e ? std::atof(e) : 1.0;
+            return (v > 0.0 && v <= 4.0) ? v : 1.0;
+        }();
+        double tot = 0.0;
+        for (int c = 0; c < K; ++c) tot += std::pow(ratio, c);
+        double cum = 0.0;
         h->rptr_host = rptr;
         h->xr.assign(1, 0);
         h->xw.assign(1, 0);
         for (int c = 1; c < K; ++c) {
-            const int64_t target = (int64_t)rptr[C] * c / K;
+            cum += std::pow(ratio, c - 1);
+            const int64_t target = (int64_t)((double)rptr[C] * cum / tot);
             const int r = (int)(std::upper_bound(rptr.begin(), rptr.end(), (int)target) - rptr.begin()) - 1;
             if (r <= h->xr.back() || r >= C) continue;
             int w = h->xw.back();
