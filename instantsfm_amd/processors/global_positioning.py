@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 from ..engine import GlobalPositioner
+from .bundle_adjustment import _packx
 
 
 class PackedGP:
@@ -21,21 +22,47 @@ class PackedGP:
         self.__dict__.update(kw)
 
 
-def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
+def pack_gp(cameras, images, tracks, depths, options, depth_only=False, native=True):
     """Vectorized restatement of global_positioning.py:85-152.  Mutates ``tracks`` (drops short tracks) and
-    ``images[*].is_registered`` (images left without tracks) exactly like the reference."""
-    short = [k for k, t in tracks.items() if t.observations.shape[0] < options['min_num_view_per_track']]
-    for track_id in short:                                                                      # :86-89
-        del tracks[track_id]
-    track_list = list(tracks.values())
-    raw = [t.observations for t in track_list]
-    if raw and all(isinstance(o, np.ndarray) and o.ndim == 2 for o in raw):  # one concatenation over the arrays
-        counts = np.fromiter((o.shape[0] for o in raw), dtype=np.int64, count=len(raw))
-        obs = np.concatenate(raw).astype(np.int64, copy=False).reshape(-1, 2)
+    ``images[*].is_registered`` (images left without tracks) exactly like the reference.  With the native extension
+    (csrc/packx.c ``collect``, as in the BA pack) every Track's observations and xyz are read in one C loop; Track
+    attributes that are not plain ndarrays (or ``native=False``) take the numpy path, which gives the same arrays."""
+    min_len = options['min_num_view_per_track']
+    keys, vals = list(tracks.keys()), list(tracks.values())
+    got = _packx.collect(vals, 0) if (native and _packx is not None) else None
+    if got is not None:
+        lengths = np.frombuffer(got[0], np.int64)
+        short = lengths < min_len
+        for k in np.flatnonzero(short).tolist():                                                # :86-89
+            del tracks[keys[k]]
+        obs = np.frombuffer(got[1], np.int64).reshape(-1, 2)
+        xyz_all = np.frombuffer(got[2], np.float64).reshape(-1, 3)
+        if short.any():
+            track_list = [v for v, sh in zip(vals, short.tolist()) if not sh]
+            obs = obs[np.repeat(~short, lengths)]
+            counts, points_3d = lengths[~short], np.ascontiguousarray(xyz_all[~short])
+        else:
+            track_list, counts, points_3d = vals, lengths, xyz_all
     else:
-        obs = [np.asarray(o, dtype=np.int64).reshape(-1, 2) for o in raw]
-        counts = np.fromiter(map(len, obs), dtype=np.int64, count=len(obs))
-        obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
+        short = [k for k, t in tracks.items() if t.observations.shape[0] < min_len]
+        for track_id in short:                                                                  # :86-89
+            del tracks[track_id]
+        track_list = list(tracks.values())
+        raw = [t.observations for t in track_list]
+        if raw and all(isinstance(o, np.ndarray) and o.ndim == 2 for o in raw):  # one concatenation over the arrays
+            counts = np.fromiter((o.shape[0] for o in raw), dtype=np.int64, count=len(raw))
+            obs = np.concatenate(raw).astype(np.int64, copy=False).reshape(-1, 2)
+        else:
+            obs = [np.asarray(o, dtype=np.int64).reshape(-1, 2) for o in raw]
+            counts = np.fromiter(map(len, obs), dtype=np.int64, count=len(obs))
+            obs = np.concatenate(obs) if obs else np.zeros((0, 2), np.int64)
+        xyz = [t.xyz for t in track_list]                                                       # :110-111
+        try:
+            points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
+            if points_3d.shape[0] != len(xyz):
+                raise ValueError
+        except ValueError:
+            points_3d = np.stack([np.asarray(x, dtype=np.float64).reshape(3) for x in xyz])
     image_used = np.zeros(len(images), dtype=bool)                                              # :91-99
     image_used[obs[:, 0]] = True  # the union over all tracks (the reference's early exit does not change it)
     for image_id, image in enumerate(images):
@@ -48,13 +75,6 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False):
     image_id2idx[image_idx2id] = np.arange(image_idx2id.size)
     w2c = np.array([np.asarray(im.world2cam, dtype=np.float64) for im in images]).reshape(-1, 4, 4)
     camera_translations = np.ascontiguousarray(w2c[image_idx2id, :3, 3])                        # :108-109
-    xyz = [t.xyz for t in track_list]                                                           # :110-111
-    try:
-        points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
-        if points_3d.shape[0] != len(xyz):
-            raise ValueError
-    except ValueError:
-        points_3d = np.stack([np.asarray(x, dtype=np.float64).reshape(3) for x in xyz])
 
     tid = np.repeat(np.arange(len(track_list)), counts)                                         # :120-138
     img_id, feat_id = obs[:, 0], obs[:, 1]
@@ -114,8 +134,16 @@ class TorchGP:
                 scene_scale = np.mean(valid_depths) * 4.0
         for image in images:
             image.world2cam[:3, 3] = scene_scale * np.random.uniform(-1, 1, 3)
-        for track in tracks.values():
-            track.xyz = scene_scale * np.random.uniform(-1, 1, 3)
+        # the tracks' draws in one call: the legacy global RNG yields the same doubles in the same order as one
+        # uniform(-1, 1, 3) per track (tests/test_gp_packing.py), and each track gets its own row
+        vals = list(tracks.values())
+        xyz = scene_scale * np.random.uniform(-1, 1, 3 * len(vals)).reshape(-1, 3)
+        if _packx is not None and xyz.dtype == np.float64 and vals:
+            _packx.assign_xyz(vals, np.arange(len(vals), dtype=np.int64), np.ascontiguousarray(xyz))
+        else:
+            for track, row in zip(vals, xyz):
+                track.xyz = row
+        for track in vals:
             track.is_initialized = True
         if self.visualizer:
             self.visualizer.add_step(cameras, images, tracks)
@@ -187,7 +215,10 @@ class TorchGP:
     def _write_back(images, pk, pos_t, pts_t):
         pts = pts_t.detach().cpu().numpy()
         pos = pos_t.detach().cpu().numpy()
-        for track, xyz in zip(pk.track_list, pts):
-            track.xyz = xyz
+        if _packx is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2 and len(pts):
+            _packx.assign_xyz(pk.track_list, np.arange(len(pk.track_list), dtype=np.int64), pts)
+        else:
+            for track, xyz in zip(pk.track_list, pts):
+                track.xyz = xyz
         for idx, image_id in enumerate(pk.image_idx2id.tolist()):
             images[image_id].world2cam[:3, 3] = pos[idx]

@@ -80,3 +80,50 @@ def test_convert_results_and_random_init():
     c = imgs[1].world2cam[:3, 3].copy()
     gp.ConvertResults(imgs)
     np.testing.assert_allclose(imgs[1].world2cam[:3, 3], -imgs[1].world2cam[:3, :3] @ c)
+
+
+def test_random_init_matches_per_track_draws():
+    """InitializeRandomPositions draws all tracks' positions in one call of the global RNG: the same doubles, in the
+    same order, as the reference's uniform(-1, 1, 3) per image then per track (global_positioning.py:23-39)."""
+    rng = np.random.default_rng(1)
+    imgs = [Image(id=i, world2cam=np.eye(4)) for i in range(7)]
+    tracks = {int(k): Track(id=int(k)) for k in rng.permutation(5000)[:600]}
+    gp = TorchGP(device="cpu")
+    np.random.seed(3)
+    gp.InitializeRandomPositions([], imgs, tracks)
+    np.random.seed(3)
+    exp_img = [100 * np.random.uniform(-1, 1, 3) for _ in imgs]
+    exp_trk = [100 * np.random.uniform(-1, 1, 3) for _ in tracks]
+    for im, e in zip(imgs, exp_img):
+        np.testing.assert_array_equal(im.world2cam[:3, 3], e)
+    for t, e in zip(tracks.values(), exp_trk):
+        assert t.xyz.shape == (3,) and t.xyz.dtype == np.float64 and t.is_initialized
+        np.testing.assert_array_equal(t.xyz, e)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_gp_pack_native_matches_numpy_path(golden_dir, name):
+    """The C collect path of pack_gp (observations and xyz read in one loop) gives the numpy path's arrays and the
+    same scene mutations, also when one Track's observations are an array layout collect does not take (int16,
+    Fortran order: the numpy path for the whole call)."""
+    from instantsfm_amd.processors.bundle_adjustment import _packx
+    assert _packx is not None
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    outs = []
+    for native in (True, False):
+        cams, imgs, tracks, depths = scene_from_fixture(g)
+        pk = pack_gp(cams, imgs, tracks, depths, OPTS, depth_only=bool(g["out_depth_only"]), native=native)
+        outs.append((pk, list(tracks.keys()), [im.is_registered for im in imgs]))
+    (a, ka, ra), (b, kb, rb) = outs
+    assert ka == kb and ra == rb
+    for f in ("translations", "camera_indices", "point_indices", "is_calibrated", "camera_translations", "points_3d",
+              "scales", "scale_free", "image_idx2id"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert x.dtype == y.dtype and x.shape == y.shape, f
+        np.testing.assert_array_equal(x, y)
+    assert [t.id for t in a.track_list] == [t.id for t in b.track_list]
+    cams, imgs, tracks, depths = scene_from_fixture(g)
+    k0 = next(iter(tracks))
+    tracks[k0].observations = np.asfortranarray(tracks[k0].observations.astype(np.int16))  # numpy path for the call
+    c = pack_gp(cams, imgs, tracks, depths, OPTS, depth_only=bool(g["out_depth_only"]))
+    np.testing.assert_array_equal(c.point_indices, b.point_indices)
