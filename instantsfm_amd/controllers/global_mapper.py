@@ -21,12 +21,15 @@ from ..processors.image_undistortion import UndistortImages
 from ..processors.reconstruction_normalizer import NormalizeReconstruction
 from ..processors.track_establishment import TrackEngine
 from ..processors.track_filter import (FilterTracksByAngle, FilterTracksByReprojectionNormalized,
-                                       FilterTracksTriangulationAngle)
+                                       FilterTracksTriangulationAngle, collect_tracks)
 from ..processors.track_retriangulation import RetriangulateTracks
 from .config import OUT_OF_SCOPE_STAGES
 
 
 def _n_obs(tracks):
+    got = collect_tracks(tracks, with_obs=False)  # (the per-track lengths in one C loop when the tracks allow it)
+    if got is not None:
+        return int(got[0].sum())
     return int(sum(len(t.observations) for t in tracks.values()))
 
 

@@ -9,17 +9,37 @@ FilterTracksByReprojectionNormalized's counter, which the reference computes on 
 import numpy as np
 
 from .. import passes
+from .bundle_adjustment import _packx
 
 EPSILON = 1e-10
 
 
+def collect_tracks(tracks, with_obs=True):
+    """(per-track counts int64, observations [X,2] int64 in dict order, xyz [T,3] float64) read in one C loop by the
+    native pack extension (csrc/packx.c ``collect``), or None when it is missing or a Track's attributes are not the
+    plain (n, 2) integer / (3,) float arrays it takes.  ``with_obs=False`` skips copying the observations."""
+    if _packx is None or not tracks:
+        return None
+    got = _packx.collect(list(tracks.values()), 0 if with_obs else (1 << 62))
+    if got is None:
+        return None
+    return (np.frombuffer(got[0], np.int64), np.frombuffer(got[1], np.int64).reshape(-1, 2),
+            np.frombuffer(got[2], np.float64).reshape(-1, 3))
+
+
 def _gather_obs(tracks):
-    """All observations of all tracks in dict order: (the per-track arrays, [X,2] int64, per-track counts, track row
-    of each observation).  One concatenation over the tracks' own arrays; tracks whose observations are not (n, 2)
-    arrays (lists, empty 1-D arrays) go through the per-track reshape."""
-    raw = [t.observations for t in tracks.values()]
-    if not raw:
+    """All observations of all tracks in dict order: (the per-track arrays or None, [X,2] int64, per-track counts,
+    track row of each observation, -, the tracks' xyz or None).  Natively when collect_tracks takes the tracks, else
+    one concatenation over the tracks' own arrays; tracks whose observations are not (n, 2) arrays (lists, empty 1-D
+    arrays) go through the per-track reshape."""
+    if not tracks:
         raise ValueError("need at least one array to concatenate")  # what the reference's np.concatenate raises
+    got = collect_tracks(tracks)
+    if got is not None:
+        counts, allobs, xyz = got
+        trow = np.repeat(np.arange(counts.size, dtype=np.int64), counts)
+        return None, allobs, counts, trow, None, xyz
+    raw = [t.observations for t in tracks.values()]
     try:
         if not all(isinstance(o, np.ndarray) and o.ndim == 2 for o in raw):
             raise ValueError
@@ -50,21 +70,23 @@ def _apply_mask(tracks, valid, counts):
 
 def _gather(images, tracks):
     """Observations of all tracks in dict order -> (obs [X,2], per-track counts, track rows, global feature row of each
-    observation into the concatenated features_undist, the rays themselves)."""
-    obs, allobs, counts, trow, _, _ = _gather_obs(tracks)
+    observation into the concatenated features_undist, the rays themselves, the tracks' xyz or None)."""
+    obs, allobs, counts, trow, _, xyz = _gather_obs(tracks)
     fu = [np.asarray(im.features_undist, dtype=np.float64).reshape(-1, 3) if len(im.features_undist) else np.zeros((0, 3))
           for im in images]
     foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in fu])]).astype(np.int64)
     rays = np.concatenate(fu) if fu else np.zeros((0, 3))
     ray_row = foff[allobs[:, 0]] + allobs[:, 1]
-    return obs, allobs, counts, trow, ray_row, rays
+    return obs, allobs, counts, trow, ray_row, rays, xyz
 
 
 def _world2cams(images):
     return np.array([np.asarray(im.world2cam, dtype=np.float64) for im in images]).reshape(-1, 16)
 
 
-def _xyz(tracks):
+def _xyz(tracks, xyz=None):
+    if xyz is not None:  # (already read by collect_tracks: the same float64 values)
+        return xyz
     return np.array([t.xyz for t in tracks.values()], dtype=np.float64).reshape(-1, 3)
 
 
@@ -80,8 +102,8 @@ def quirk_counter(valid, counts):
 
 def FilterTracksByReprojectionNormalized(cameras, images, tracks, max_reprojection_error, device="cuda:0"):
     """track_filter.py:26-66."""
-    obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
-    valid = passes.filter_reproj_normalized(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays,
+    obs, allobs, counts, trow, ray_row, rays, xyz = _gather(images, tracks)
+    valid = passes.filter_reproj_normalized(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks, xyz), rays,
                                             max_reprojection_error, device)
     _apply_mask(tracks, valid, counts)
     counter = quirk_counter(valid, counts)
@@ -102,12 +124,12 @@ def _features(images):
 
 def FilterTracksByReprojection(cameras, images, tracks, max_reprojection_error, device="cuda:0"):
     """track_filter.py:68-113: pixel reprojection error through each image's Camera.cam2img."""
-    obs, allobs, counts, trow, _, _ = _gather_obs(tracks)
+    obs, allobs, counts, trow, _, xyz = _gather_obs(tracks)
     feats, foff = _features(images)
     img_cam = np.array([im.cam_id for im in images], dtype=np.int32)
     valid = passes.filter_reproj_pixel(allobs[:, 0], trow, foff[allobs[:, 0]] + allobs[:, 1], feats, img_cam,
                                        [cam.model_id.value for cam in cameras], [cam.params for cam in cameras],
-                                       _world2cams(images), _xyz(tracks), max_reprojection_error, device)
+                                       _world2cams(images), _xyz(tracks, xyz), max_reprojection_error, device)
     _apply_mask(tracks, valid, counts)
     counter = quirk_counter(valid, counts)
     print(f'Filtered {counter} / {len(tracks)} tracks by reprojection error')
@@ -117,8 +139,9 @@ def FilterTracksByReprojection(cameras, images, tracks, max_reprojection_error, 
 def FilterTracksByAngle(cameras, images, tracks, max_angle_error, device="cuda:0"):
     """track_filter.py:5-24."""
     thres = np.cos(np.deg2rad(max_angle_error))
-    obs, allobs, counts, trow, ray_row, rays = _gather(images, tracks)
-    valid = passes.filter_angle(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks), rays, thres, device)
+    obs, allobs, counts, trow, ray_row, rays, xyz = _gather(images, tracks)
+    valid = passes.filter_angle(allobs[:, 0], trow, ray_row, _world2cams(images), _xyz(tracks, xyz), rays, thres,
+                                device)
     starts = np.concatenate([[0], np.cumsum(counts)])
     bad = np.concatenate([[0], np.cumsum(~valid)])
     touched = np.flatnonzero(bad[starts[1:]] - bad[starts[:-1]] > 0)  # the tracks with a failing observation
@@ -136,11 +159,17 @@ def FilterTracksTriangulationAngle(cameras, images, tracks, min_angle, device="c
     thres = np.cos(np.deg2rad(min_angle))
     centers = np.array([np.asarray(im.center(), dtype=np.float64) for im in images]).reshape(-1, 3)
     keys = list(tracks.keys())
-    obs = [np.asarray(tracks[k].observations).reshape(-1, 2) for k in keys]
-    counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+    got = collect_tracks(tracks)
+    if got is not None:
+        counts, allobs, xyz = got
+        img = allobs[:, 0].astype(np.int32)
+    else:
+        obs = [np.asarray(tracks[k].observations).reshape(-1, 2) for k in keys]
+        counts = np.array([o.shape[0] for o in obs], dtype=np.int64)
+        img = np.concatenate([o[:, 0] for o in obs]).astype(np.int32) if obs else np.zeros(0, np.int32)
+        xyz = None
     ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-    img = np.concatenate([o[:, 0] for o in obs]).astype(np.int32) if obs else np.zeros(0, np.int32)
-    remove = passes.filter_tri_angle(ptr, img, centers, _xyz(tracks), thres, device) if keys else np.zeros(0, bool)
+    remove = passes.filter_tri_angle(ptr, img, centers, _xyz(tracks, xyz), thres, device) if keys else np.zeros(0, bool)
     counter = 0
     for k, r in zip(keys, remove.tolist()):
         if r:
