@@ -2978,11 +2978,31 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     });
     const int kmax = *std::max_element(kmax_t.begin(), kmax_t.end());
     tick("local track order");
-    // camera-major lists; within a camera, observations with more upper partners first (stable), which balances the
-    // Schur groups: two stable counting sorts, by descending partner count, then by camera
+    // camera-major lists.  Default (INSFM_SCHUR_ORDER=1): within a camera the observations in point order, cut into
+    // chunks of four k_schur rounds (4 x 64 own observations for D = 8; INSFM_SCHUR_CHUNK rounds), each chunk sorted
+    // by descending upper-partner count (stable; balances the Schur groups of a wave: 2.8 % more wave partner slots
+    // than the global count sort, 10.8 % with one-round chunks).  Every k_schur row then walks the points in the same
+    // global order at about the same pace, so rows running together read a shared track's partner W records close
+    // together in time.  Config 3, k_schur: 491 us (count sort) -> 467 us (chunks of 4 rounds; 1 / 2 / 8 / 16 rounds:
+    // 541 / 499 / 471 / 483 us -- the wave partner slots cost more than the locality buys below 4).
+    // INSFM_SCHUR_ORDER=0: descending partner count over the whole camera (stable counting sorts: count, camera).
     std::vector<int> cptr;
     nivec<int> cobs;
-    {
+    static const int schur_order = [] { const char* e = std::getenv("INSFM_SCHUR_ORDER"); return e ? std::atoi(e) : 1; }();
+    if (schur_order == 1) {
+        // observations are track-major (point order), so a stable counting sort by camera leaves each list in point
+        // order; then a stable sort of each chunk by descending partner count
+        pcount_sort(pool, Nl, C, nullptr, [&](int o) { return lcam[o]; }, cobs, cptr);
+        static const int rounds = [] { const char* e = std::getenv("INSFM_SCHUR_CHUNK"); const int v = e ? std::atoi(e) : 4; return v > 0 ? v : 4; }();
+        const int K = rounds * kSchurWaves * (64 / D);
+        pool.ranges(C, [&](int, long long i0, long long i1) {
+            for (long long i = i0; i < i1; ++i)
+                for (int a = cptr[i]; a < cptr[i + 1]; a += K) {
+                    const int e = std::min(a + K, cptr[i + 1]);
+                    std::stable_sort(cobs.data() + a, cobs.data() + e, [&](int x, int y) { return key[x] > key[y]; });
+                }
+        });
+    } else {
         nivec<int> byk;
         std::vector<int> kptr;
         pcount_sort(pool, Nl, kmax + 1, nullptr, [&](int o) { return kmax - key[o]; }, byk, kptr);
@@ -3241,8 +3261,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             maxc = std::max(maxc, ke - kb);
         }
     }
-    // Row order is kept: measured against heaviest-first (LPT) and XCD-contiguous orders it is the fastest
-    // (651 vs 667 / 688 us on config 3): neighbouring rows launched together share partner W records in L2/MALL.
     h->nwork = (int)work.size();
     h->max_chunk = maxc;
     if (kind == 0 && desc->allreduce_async && (desc->world_size > 1 || desc->allreduce) && desc->exchange_chunks > 1 &&
@@ -3279,6 +3297,31 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_x, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_xdone, hipEventDisableTiming);
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("exchange stream: ") + hipGetErrorString(e));
+    }
+    // Work order: natural (row order), so the 256 rows running at once are 256 consecutive cameras that share tracks
+    // in the Infinity Cache.  INSFM_SCHUR_XCD=B (with the point-order chunks) deals runs of B consecutive items to one
+    // XCD instead (workgroups go round-robin over the 8 XCDs): measured on config 3 (tools/order_probe.sh,
+    // profiles/r3_v10/): B = 1 / 2 / 4 / 16 / 125 -> k_schur 467 / 469 / 471 / 491 / 515 us -- the whole-XCD runs lift the
+    // L2 hit rate from 4 to 54 % and cut the average L1->L2 read latency 562 -> 402 cycles, yet the kernel is slower:
+    // it is not bound by that latency.
+    {
+        static const int xcd = [] { const char* e = std::getenv("INSFM_SCHUR_XCD"); return e ? std::atoi(e) : 0; }();
+        const int nw = (int)work.size();
+        if (xcd >= 1 && schur_order == 1 && nw >= 16 && h->xw.empty()) {  // (the chunked exchange needs row order)
+            // natural item k goes to XCD (k / xcd) % 8: runs of `xcd` consecutive items per XCD; position 8 j + x
+            // takes the j-th item of XCD x (leftovers of unequal lists at the end)
+            std::vector<std::vector<int>> lx(8);
+            for (int k = 0; k < nw; ++k) lx[(k / xcd) % 8].push_back(k);
+            std::vector<int4> w2;
+            w2.reserve(nw);
+            size_t mn = lx[0].size();
+            for (int x = 1; x < 8; ++x) mn = std::min(mn, lx[x].size());
+            for (size_t j = 0; j < mn; ++j)
+                for (int x = 0; x < 8; ++x) w2.push_back(work[lx[x][j]]);
+            for (int x = 0; x < 8; ++x)
+                for (size_t j = mn; j < lx[x].size(); ++j) w2.push_back(work[lx[x][j]]);
+            work.swap(w2);
+        }
     }
     h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D + 12) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
