@@ -2994,12 +2994,27 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         // order; then a stable sort of each chunk by descending partner count
         pcount_sort(pool, Nl, C, nullptr, [&](int o) { return lcam[o]; }, cobs, cptr);
         static const int rounds = [] { const char* e = std::getenv("INSFM_SCHUR_CHUNK"); const int v = e ? std::atoi(e) : 4; return v > 0 ? v : 4; }();
-        const int K = rounds * kSchurWaves * (64 / D);
+        // INSFM_SCHUR_SNAKE=1: after the sort of a chunk the slices of round r go to the waves in snake order (r even:
+        // wave w <- sorted slice r W + w; r odd: r W + W - 1 - w), so no wave always gets the heaviest slice of every
+        // round (k_schur's waves run their slices w * NG + r * R independently; the row ends with its slowest wave).
+        // A model of config 3 gives critical wave / ideal work 1.26 -> 1.06, but k_schur measured 473-475 us without
+        // it and 480-484 with it (profiles/r3_v10/snake_probe.log), so it is off by default.
+        static const bool snake = [] { const char* e = std::getenv("INSFM_SCHUR_SNAKE"); return e && *e == '1'; }();
+        const int NG = 64 / D, R = kSchurWaves * NG, K = rounds * R;
         pool.ranges(C, [&](int, long long i0, long long i1) {
+            std::vector<int> tmp(K);
             for (long long i = i0; i < i1; ++i)
                 for (int a = cptr[i]; a < cptr[i + 1]; a += K) {
-                    const int e = std::min(a + K, cptr[i + 1]);
-                    std::stable_sort(cobs.data() + a, cobs.data() + e, [&](int x, int y) { return key[x] > key[y]; });
+                    const int e = std::min(a + K, cptr[i + 1]), m = e - a;
+                    int* c = cobs.data() + a;
+                    std::stable_sort(c, c + m, [&](int x, int y) { return key[x] > key[y]; });
+                    if (m < K || !snake) continue;  // (a row's short last chunk stays in sorted order)
+                    std::copy(c, c + m, tmp.begin());
+                    for (int r = 0; r < rounds; ++r)
+                        for (int w = 0; w < kSchurWaves; ++w) {
+                            const int src = r * kSchurWaves + ((r & 1) ? kSchurWaves - 1 - w : w);
+                            std::copy(tmp.begin() + src * NG, tmp.begin() + src * NG + NG, c + (r * kSchurWaves + w) * NG);
+                        }
                 }
         });
     } else {
