@@ -69,7 +69,7 @@ typedef struct {
     int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
                               plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
                               Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
-    int32_t cluster_size;  /* target cameras per coarse cluster (default 16; doubled until nclust*(D+1) <= 768) */
+    int32_t cluster_size;  /* target cameras per coarse cluster (default 14; grown until nclust*(D+1) <= 768) */
     int32_t schur_variant; /* reduced-system build (BA, deterministic = 0): 0 (default) reads the stored camera-point
                               blocks W; 1 re-derives them per pair, LDS-atomic row accumulation; 2 re-derives them,
                               MFMA register accumulation (D <= 8, else 1).  1 and 2 never form W (no 192 B/obs write).

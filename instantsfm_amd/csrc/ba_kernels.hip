@@ -1484,12 +1484,21 @@ __global__ __launch_bounds__(kFinalThreads) void k_final(const double* __restric
                                                     const double* __restrict__ gp_part, int ngp,
                                                     const double* __restrict__ gc_part, int ngc, int* __restrict__ flags,
                                                     double* __restrict__ result) {
-    __shared__ double red[2 * kFinalThreads / 64];
-    double c2[2];
-    sum_partials<2, kFinalThreads>(cost_part, ncost, c2, red);
-    double a[1], b[1];
-    if (gp_part) sum_partials<1, kFinalThreads>(gp_part, ngp, a, red); else a[0] = 0.0;
-    if (gc_part) sum_partials<1, kFinalThreads>(gc_part, ngc, b, red); else b[0] = 0.0;
+    // the three partial arrays in one pass (every load of a round in flight together), each array still summed by
+    // each thread in index order and then by the same butterfly and wave order: bitwise the sums of three separate
+    // sum_partials passes, with one latency chain instead of three
+    __shared__ double red[4 * kFinalThreads / 64];
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    const int ng1 = gp_part ? ngp : 0, ng2 = gc_part ? ngc : 0;
+    const int nmax = max(ncost, max(ng1, ng2));
+#pragma unroll 4
+    for (int i = threadIdx.x; i < nmax; i += kFinalThreads) {
+        if (i < ncost) { v[0] += cost_part[2 * (size_t)i]; v[1] += cost_part[2 * (size_t)i + 1]; }
+        if (i < ng1) v[2] += gp_part[i];
+        if (i < ng2) v[3] += gc_part[i];
+    }
+    block_sum<4, kFinalThreads>(v, red);
+    const double c2[2] = {v[0], v[1]}, a[1] = {v[2]}, b[1] = {v[3]};
     if (threadIdx.x == 0) {
         result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0];
         result[4] = (double)flags[0];
@@ -2827,7 +2836,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->world_size = 1; d->rank = 0;
     d->shard_point_begin = 0; d->shard_point_end = -1;
     d->precond = 1;
-    d->cluster_size = 16;
+    d->cluster_size = 14;
     d->exchange_chunks = 4;
 }
 
@@ -3618,11 +3627,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (desc->precond == 1 && h->d.optimize_poses) {
         // ---- two-level preconditioner: clusters, source lists of E, buffers ----
         const int MC = D + 1;
-        int K = desc->cluster_size > 0 ? desc->cluster_size : 16;
+        // target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
+        // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
+        // While the coarse dimension exceeds kCoarseMax the target grows in proportion to the excess (at least by
+        // one), rounded up to even (aggregates below K / 2 are dissolved: an odd K would keep singletons):
+        // K' = max(K + 1, ceil(K nc MC / kCoarseMax)) rounded up to even -- the oracle's ora_cluster_cameras
+        int K = desc->cluster_size > 0 ? desc->cluster_size : 14;
         std::vector<int>& lab = h->clab_host;
         int nc = aggregate(g, C, K, lab);
         while (nc * MC > kCoarseMax) {
-            K *= 2;
+            K = std::max(K + 1, (int)(((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));
+            K += K & 1;
             nc = aggregate(g, C, K, lab);
         }
         const int m = nc * MC;

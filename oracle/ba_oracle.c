@@ -345,12 +345,17 @@ static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *
  * aggregate id).  Labels are renumbered in order of first appearance by camera id. */
 static int ora_aggregate(ora_t* h, int K);
 /* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU's k_tl_pc keeps a cluster's rows of E^-1
- * in registers; csrc/ba_twolevel.h COARSE_MAX_DIM): while the aggregation yields more clusters, it is redone with
- * twice the target size. */
+ * in registers; csrc/ba_twolevel.h COARSE_MAX_DIM): while the aggregation yields more clusters, it is redone with the
+ * target size grown in proportion to the excess, K' = max(K + 1, ceil(K nclust (D + 1) / COARSE_MAX)) rounded up to
+ * even (aggregates below K / 2 are dissolved, so an odd K would keep singletons). */
 #define COARSE_MAX 768
 static void ora_cluster_cameras(ora_t* h) {
-    int K = h->cluster_size;
-    while (ora_aggregate(h, K) * (h->D + 1) > COARSE_MAX) K *= 2;
+    int K = h->cluster_size, nc;
+    while ((nc = ora_aggregate(h, K)) * (h->D + 1) > COARSE_MAX) {
+        const long g = ((long)K * nc * (h->D + 1) + COARSE_MAX - 1) / COARSE_MAX;
+        K = g > K + 1 ? (int)g : K + 1;
+        K += K & 1;
+    }
 }
 
 static int ora_aggregate(ora_t* h, int K) {
@@ -506,7 +511,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     h->down0 = dopt[5]; h->factor = dopt[6]; h->high = dopt[7]; h->low = dopt[8]; h->cmin = dopt[9];
     h->cmax = dopt[10]; h->pcg_tol = dopt[11];
     h->max_rejects = iopt[0]; h->pcg_max_iter = iopt[1]; h->optimize_poses = iopt[2];
-    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 16;
+    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 14;
 #ifdef _OPENMP
     if (iopt[3] > 0) omp_set_num_threads(iopt[3]);
 #endif

@@ -30,7 +30,7 @@ def engines(prob, **kw):
                          **kw)
     ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                      optimize_poses=int(kw.get("optimize_poses", True)), precond=kw.get("precond", 1),
-                     cluster_size=kw.get("cluster_size", 16))
+                     cluster_size=kw.get("cluster_size", 14))
     return eng, ora
 
 

@@ -166,7 +166,7 @@ def _shuffled(prob, seed=1):
 @pytest.mark.parametrize("K", (2, 4, 8, 32))
 def test_clusters_partition_and_cap(K):
     """Every camera gets a label 0..nc-1, no degenerate singleton clusters on a connected scene, and the coarse
-    dimension nc*(D+1) stays within the 768 cap (cluster size doubled as needed)."""
+    dimension nc*(D+1) stays within the 768 cap (cluster size grown as needed)."""
     prob = make_problem(200, 4000, seed=1)
     cam_idx, _, pp = _shuffled(prob)
     ba = O.OracleBA(prob.model, prob.uv, cam_idx, prob.pt_idx, pp, prob.n_cams, prob.n_points, cluster_size=K)
