@@ -25,6 +25,7 @@ struct CgBufs {
     double* scal;     // [4]: alpha, beta, flag of the current recurrence step (written by k_cg_dots)
     int* status;      // [0] 0 running / 1 converged / 2 breakdown ; [1] iterations
     int* prog;        // host-mapped (two-level path): [0] iterations started, [1] status, [2] iterations, [3] coarse
+                      // used, [4] sequence of the last k_cg_gate that saw its status (CG-stream path)
 };
 
 

@@ -1598,6 +1598,27 @@ __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) 
     else if (t < 8) status[t - 4] = 0;
 }
 
+// Main-stream gate of a CG running on its own stream: one thread waits (s_sleep between system-scope loads of the
+// host-mapped status word, which the converging k_tl_pc(_cl) publishes with a system-scope release after its final
+// iterate is complete) until the status is non-zero, then records it in *code for k_publish.  Bounded: after
+// `limit` ticks of the 100-MHz real-time counter it gives up with code -1 (the host reports the CG error itself and
+// releases the gate by writing the status word on every error path).
+// On exit it stores `seq` into prog[4] (system scope): the host resets the status word for the next solve only after
+// that acknowledgement, so a gate can never miss its own status.
+__global__ void k_cg_gate(int* prog, int* __restrict__ code, long long limit, int seq) {
+    if (threadIdx.x != 0) return;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    int v = 0;
+    for (;;) {
+        v = __hip_atomic_load(prog + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v != 0) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > limit) { v = -1; break; }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    *code = v;
+    __hip_atomic_store(prog + 4, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // After k_final (and the cross-rank sum): result[0..4] into host-mapped memory for the host's spin-wait, then
 // sequence word `seq` (system-scope release), so the host reads the trial's cost without a stream synchronization or a
 // copy launch.  With `cams_cur` set (insfm_ba_step: the caller's buffers hold the current parameters) the accepted
@@ -1608,9 +1629,10 @@ __global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__
                                                       int can_reject, const double* __restrict__ cams_new,
                                                       double* __restrict__ cams_cur, long long ncam,
                                                       const double* __restrict__ pts_new, double* __restrict__ pts_cur,
-                                                      long long npts) {
+                                                      long long npts, const int* __restrict__ gate) {
     const double loss = result[0];
-    const bool acc = result[4] == 0.0 && !(last < loss && can_reject);
+    // (gate: the CG status its gate saw -- anything but a converged CG is never accepted)
+    const bool acc = result[4] == 0.0 && !(last < loss && can_reject) && (gate == nullptr || *gate == 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int k = 0; k < 5; ++k) pub[k] = result[k];
         pub[5] = acc ? 1.0 : 0.0;
@@ -1705,6 +1727,16 @@ struct insfm_ba {
     int* flags = nullptr;
     double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
     int* prog_host = nullptr;    // pinned, device-mapped: progress of the two-level CG (CgBufs::prog)
+    // CG on its own stream (single rank, two-level; opt-in, INSFM_CG_STREAM=1): the iterations go to `cgs` behind
+    // one event of the main stream, and the main stream continues at once with k_cg_gate (spins on the published
+    // status word) and the post-CG kernels, so they start as soon as the CG converges instead of after the host has
+    // seen the status and after the iterations queued past convergence.  ev_cgtail: the last iteration queued on cgs
+    // (the next solve's status reset waits for it); gate_dev: the status the gate saw (k_publish accepts only 1).
+    hipStream_t cgs = nullptr;
+    hipEvent_t ev_cg0 = nullptr, ev_cgtail = nullptr;
+    bool cgtail_pending = false, gate_used = false;
+    int gate_seq = 0;  // sequence of the last gate queued (acknowledged in prog_host[4])
+    int* gate_dev = nullptr;
     double* pub_host = nullptr;  // pinned, device-mapped: k_publish's result[0..4], decision, sequence word (double 8)
     double* pub_dev = nullptr;
     unsigned pub_seq = 0;
@@ -2348,6 +2380,13 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
+    // the previous solve's iterations queued past convergence on the CG stream exit at the status word this solve
+    // resets: they must have run first (normally long done: then no wait marker is queued)
+    if (h->cgtail_pending) {
+        if (hipEventQuery(h->ev_cgtail) != hipSuccess) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_cgtail, 0));
+        h->cgtail_pending = false;
+    }
+    h->gate_used = false;
     // The non-PD flag is cleared by the k_final that consumed it and the CG status word by k_point_prep; one tiny
     // launch clears both only when that chain is broken (a solve not followed by a cost, or no local points).
     if (h->flags_dirty || h->Pl == 0 || h->kind == 1) {
@@ -2435,6 +2474,21 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // loop ends when the status word turns non-zero.  The few iterations enqueued past convergence exit at the
             // device status flag.
             volatile int* pg = h->prog_host;
+            if (h->gate_seq != 0 && pg[4] != h->gate_seq) {
+                // the last solve's gate has not acknowledged yet (it exits once it has seen that solve's status, which
+                // is non-zero by now): wait for it before the status word is reset under it
+                const double tg = wall_seconds();
+                static const double gate_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
+                while (pg[4] != h->gate_seq) {
+                    if (wall_seconds() - tg > gate_s) {
+                        h->err = "PCG: the previous solve's CG gate did not finish";
+                        return INSFM_BA_EHIP;
+                    }
+#if defined(__x86_64__)
+                    __builtin_ia32_pause();
+#endif
+                }
+            }
             pg[0] = pg[1] = pg[2] = pg[3] = 0;
             std::atomic_thread_fence(std::memory_order_seq_cst);
             // INSFM_HOST_TRACE=1: per solve, host microseconds spent enqueueing CG iterations / issuing side units, and
@@ -2442,13 +2496,20 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             static const bool htrace = [] { const char* e = std::getenv("INSFM_HOST_TRACE"); return e && *e == '1'; }();
             double t_enq = 0.0, t_side = 0.0, m_enq = 0.0, m_side = 0.0, t_sol0 = htrace ? wall_seconds() : 0.0;
             int n_enq = 0, n_side = 0;
+            // CG stream (see insfm_ba::cgs): not with the instrumented replay (its phase events are on the main stream)
+            // or multi-rank runs (their CG waits for the exchange; cgs is created single-rank only)
+            const bool on_cgs = h->cgs != nullptr && !h->timing;
+            hipStream_t cg_stream = on_cgs ? h->cgs : h->stream;
             auto enqueue = [&](int from, int to) -> int {
                 const double t0 = htrace ? wall_seconds() : 0.0;
+                hipStream_t main_stream = h->stream;
+                h->stream = cg_stream;  // (launch_tl_iter launches on h->stream)
                 const int r = with_D(D, [&](auto dc_) -> int {
                     constexpr int DV = decltype(dc_)::value;
                     for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
                     return launch_err(h, "k_tl_pc/k_tl_pspmv");
                 });
+                h->stream = main_stream;
                 if (htrace) { const double dt = wall_seconds() - t0; t_enq += dt; m_enq = std::max(m_enq, dt / std::max(1, to - from)); n_enq += to - from; }
                 return r;
             };
@@ -2460,7 +2521,25 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step);
             // the loop below tops up one iteration at a time
             int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
+            if (on_cgs) {  // the CG stream starts behind everything queued so far on the main stream
+                HIPCHK(hipEventRecord(h->ev_cg0, h->stream));
+                HIPCHK(hipStreamWaitEvent(h->cgs, h->ev_cg0, 0));
+            }
             if ((rc = enqueue(0, enq))) return rc;
+            if (on_cgs) {
+                // the main stream: the gate, then the post-CG kernels (k_cg_finish here, the back-substitution and the
+                // cost after the poll loop) -- they run as soon as the status word turns non-zero
+                if (++h->gate_seq == 0) h->gate_seq = 1;
+                k_cg_gate<<<1, 64, 0, h->stream>>>(h->cg.prog, h->gate_dev, 6000000000LL, h->gate_seq);
+                rc = with_D(D, [&](auto dc_) -> int {
+                    constexpr int DV = decltype(dc_)::value;
+                    k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
+                                                                                                  h->dc);
+                    return launch_err(h, "k_cg_gate/k_cg_finish");
+                });
+                if (rc) { pg[1] = 3; return rc; }
+                h->gate_used = true;
+            }
             CgPoll poll;
             poll.enq = enq;
             poll.extra_ahead = (h->side_slot >= 0 && side_sched() == 2) ? kSideAhead : 0;
@@ -2469,7 +2548,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             const int pr = cg_poll(
                 poll, maxit + 2, kCgAhead, stall_s, [&] { return (int)pg[1]; }, [&] { return (int)pg[0]; }, enqueue,
                 [&] {
-                    const hipError_t q = hipStreamQuery(h->stream);
+                    const hipError_t q = hipStreamQuery(cg_stream);
                     if (q == hipSuccess) { std::atomic_thread_fence(std::memory_order_seq_cst); return 0; }
                     return q == hipErrorNotReady ? 1 : -1;
                 },
@@ -2496,6 +2575,12 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // here would hold back k_cg_finish by the host time of every remaining launch
             const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
             hmark(h, "cg converged");
+            if (on_cgs) {
+                HIPCHK(hipEventRecord(h->ev_cgtail, h->cgs));
+                h->cgtail_pending = true;
+                // on any error the gate is released here (status 3: never accepted by k_publish)
+                if (pr != CgPoll::kDone || erc) { std::atomic_thread_fence(std::memory_order_seq_cst); pg[1] = 3; }
+            }
             if (erc) return erc;
             if (htrace)
                 std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
@@ -2505,7 +2590,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             enq = poll.enq;
             if (pr == CgPoll::kEnqueueError) return erc;
             if (pr == CgPoll::kStreamError) {
-                h->err = std::string("PCG: ") + hipGetErrorString(hipStreamQuery(h->stream));
+                h->err = std::string("PCG: ") + hipGetErrorString(hipStreamQuery(cg_stream));
                 return INSFM_BA_EHIP;
             }
             if (pr == CgPoll::kStalled) {
@@ -2563,12 +2648,15 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         iters = st[1];
         h->coarse_used = h->tlon ? st[2] : 0;
         h->last_cg_iters = iters;
-        rc = with_D(D, [&](auto dc_) -> int {
-            constexpr int DV = decltype(dc_)::value;
-            k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x, h->dc);
-            return launch_err(h, "k_cg_finish");
-        });
-        if (rc) return rc;
+        if (!h->gate_used) {  // (on the CG-stream path k_cg_finish is already queued behind the gate)
+            rc = with_D(D, [&](auto dc_) -> int {
+                constexpr int DV = decltype(dc_)::value;
+                k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
+                                                                                                h->dc);
+                return launch_err(h, "k_cg_finish");
+            });
+            if (rc) return rc;
+        }
         dcp = h->dc;
         hmark(h, "cg_finish");
     }
@@ -2637,7 +2725,8 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     const long long ncam = copy ? (long long)h->C * h->stride : 0, npts = copy ? (long long)h->Pl * 3 : 0;
     const int grid = copy ? std::max(1, std::min(1024, cdiv(std::max(ncam, npts / 2 + 1), kThreads))) : 1;
     k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->pub_dev, seq, ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
-                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
+                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts,
+                                               (ta && h->gate_used) ? h->gate_dev : nullptr);
     if (int rc = launch_err(h, "k_publish")) return rc;
     hmark(h, "publish");
     if (int rc = side_issue_while_busy(h)) return rc;
@@ -2846,7 +2935,7 @@ void insfm_ba_destroy(insfm_ba* h) {
     if (!h) return;
     if (h->side) (void)side_flush(h);
     // every stream that may still use the buffers, before they are parked for the next handle
-    for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux})
+    for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux, h->cgs})
         if (st) (void)hipStreamSynchronize(st);
     if (!h->stream) (void)hipDeviceSynchronize();
     dfree_all(h);
@@ -2867,6 +2956,12 @@ void insfm_ba_destroy(insfm_ba* h) {
         (void)hipStreamSynchronize(h->aux);
         (void)hipStreamDestroy(h->aux);
     }
+    if (h->cgs) {
+        (void)hipStreamSynchronize(h->cgs);
+        (void)hipStreamDestroy(h->cgs);
+    }
+    if (h->ev_cg0) (void)hipEventDestroy(h->ev_cg0);
+    if (h->ev_cgtail) (void)hipEventDestroy(h->ev_cgtail);
     if (h->ev_lin0) (void)hipEventDestroy(h->ev_lin0);
     if (h->ev_lc) (void)hipEventDestroy(h->ev_lc);
     if (h->ev_x) (void)hipEventDestroy(h->ev_x);
@@ -3831,11 +3926,22 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         });
         h->tlon = true;
         void* pm = nullptr;
-        if (hipHostMalloc(&pm, sizeof(int) * 4, hipHostMallocMapped) == hipSuccess) {
+        if (hipHostMalloc(&pm, sizeof(int) * 8, hipHostMallocMapped) == hipSuccess) {
             h->prog_host = static_cast<int*>(pm);
             void* dp = nullptr;
             if (hipHostGetDevicePointer(&dp, pm, 0) == hipSuccess) h->cg.prog = static_cast<int*>(dp);
             else { (void)hipHostFree(pm); h->prog_host = nullptr; }
+        }
+        // opt-in (INSFM_CG_STREAM=1): measured slower on config 3 -- 659-672 vs 709-726 LM it/s on one box
+        // (profiles/r3_v11/cg_stream_ab.log); the iterations behind a cross-queue event and the gated tail cost more
+        // than the host round trip and the launches past convergence they remove
+        static const bool cg_stream = [] { const char* e = std::getenv("INSFM_CG_STREAM"); return e && *e == '1'; }();
+        if (cg_stream && h->prog_host && kind == 0 && desc->world_size <= 1 && !desc->allreduce) {
+            hipError_t e2 = hipStreamCreateWithFlags(&h->cgs, hipStreamNonBlocking);
+            if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&h->ev_cg0, hipEventDisableTiming);
+            if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&h->ev_cgtail, hipEventDisableTiming);
+            if (e2 != hipSuccess) return fail(INSFM_BA_EHIP, std::string("CG stream: ") + hipGetErrorString(e2));
+            if ((rc = dalloc(h, (void**)&h->gate_dev, sizeof(int)))) return fail(rc, "");
         }
     }
     tick("two-level setup (end)");
@@ -3922,7 +4028,7 @@ int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts)
     int rc = run_linearize(h, h->cams_cur, h->pts_cur);
     if (!rc) rc = lin_join(h);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
     return 0;
 }
 
@@ -3931,7 +4037,7 @@ int insfm_ba_debug_solve(insfm_ba* h, double f) {
     h->keep_S = 1;
     // solves around the parameters last passed to insfm_ba_debug_linearize
     int it = run_solve(h, f, h->cams_cur, h->pts_cur);
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
     return it;
 }
 
@@ -3988,6 +4094,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     // re-run one kernel `reps` times back to back on the data of the last solve; the CG state it overwrites is
     // scratch once the solve has finished (dc already extracted).  0: k_cg_iter  1: k_schur (damping factor 1)
     // 2: one two-level CG iteration  3: k_tl_pspmv  4: the two-level setup  5: k_lin_points (overwrites W / V / g_p)
+    if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));  // (iterations queued past convergence read the status word)
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
     if (((which >= 2 && which <= 4) || which == 6 || which == 7) && !h->tlon) return INSFM_BA_EINVAL;
@@ -4115,7 +4222,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     if (int rc0 = side_flush(h)) return rc0;
     if (int rc0 = lin_join(h)) return rc0;
     if (n) HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
     return (int64_t)n;
 }
 

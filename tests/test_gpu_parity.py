@@ -569,3 +569,22 @@ def test_pc_cluster_reduction_parity():
     for s in out["steps"]:
         assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
         assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s
+
+
+def test_cg_stream_parity():
+    """The opt-in CG stream (INSFM_CG_STREAM=1: iterations on their own stream behind one event, the main stream gated
+    by k_cg_gate on the published status word, k_publish accepting only a converged CG) against the oracle on config-2
+    LM steps: same PCG iterations and trials, loss 1e-10, parameters 1e-9.  Read once per process: a subprocess."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pc_cluster_check.py"), "INSFM_CG_STREAM"],
+                       capture_output=True, text=True, timeout=280, env=dict(os.environ, INSFM_CG_STREAM="1"), cwd=repo)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["env"] == "1"
+    for s in out["steps"]:
+        assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
+        assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s

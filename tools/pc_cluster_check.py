@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""Parity of the opt-in cluster reduction of the CG's row partials (INSFM_PC_CLUSTER=1, read once per process):
+"""Parity of an opt-in CG path switched by an environment variable read once per process (argv[1], default
+INSFM_PC_CLUSTER: the cluster reduction of the CG's row partials; INSFM_CG_STREAM: the CG on its own stream):
 config-2 LM steps on the GPU vs the oracle, same PCG iterations and trials, parameters to 1e-9.  Prints one JSON line.
-Run by tests/test_gpu_parity.py::test_pc_cluster_reduction_parity in a subprocess with the variable set."""
+Run by tests/test_gpu_parity.py (test_pc_cluster_reduction_parity, test_cg_stream_parity) in a subprocess with the
+variable set."""
 import json
 import os
 import sys
@@ -23,7 +25,8 @@ def main():
     ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
     cg, pg = torch.from_numpy(prob.cams_init.copy()).to(dev), torch.from_numpy(prob.points_init.copy()).to(dev)
     co, po = prob.cams_init.copy(), prob.points_init.copy()
-    out = dict(env=os.environ.get("INSFM_PC_CLUSTER"), steps=[])
+    var = sys.argv[1] if len(sys.argv) > 1 else "INSFM_PC_CLUSTER"
+    out = dict(env=os.environ.get(var), steps=[])
     for _ in range(3):
         lg, st = eng.step(cg, pg)
         lo = ora.step(co, po)
