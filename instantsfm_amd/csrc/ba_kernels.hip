@@ -2189,8 +2189,11 @@ int run_tl_gj_unit(insfm_ba* h, int slot, int u, hipStream_t stream) {
 // solve when this is the first solve after a linearization (it starts right away), otherwise at its own (it waits
 // for the factorization) -- the oracle's lag rule (ora_pcg).  The next solve's k_cg_scale / k_tl_basis overwrite
 // S~ / Z~, so they wait for ev_built (run_solve).
+// CG iterations the host keeps queued ahead of the device: 1 since late round 3 (config 3, same box, 3 runs each:
+// 2 / 1 / 0 -> 714-721 / 722-726 / 720-727 LM it/s; every queued iteration a converged CG still runs costs ~9 us;
+// profiles/r3_v12/cg_ahead_ab.log)
 #ifndef CG_AHEAD
-#define CG_AHEAD 2
+#define CG_AHEAD 1
 #endif
 #ifndef CG_INIT_BACK
 #define CG_INIT_BACK 2
