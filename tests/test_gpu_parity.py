@@ -588,3 +588,19 @@ def test_cg_stream_parity():
     for s in out["steps"]:
         assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
         assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s
+
+
+@pytest.mark.parametrize("K", (2, 3))
+def test_clusters_match_oracle_when_the_cap_grows_the_target(K):
+    """FULL_OPENCV (D = 16, 17 coarse columns per cluster) on 150 cameras: a target of K = 2 or 3 gives more than
+    768 / 17 clusters, so both sides grow the target in proportion to the excess (rounded up to even) and must arrive
+    at the same clusters, within the cap."""
+    prob = make_problem(150, 6000, seed=8, model=6)
+    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=DEV,
+                         cluster_size=K)
+    ora = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, cluster_size=K)
+    lg, ng = eng.clusters()
+    lo, no = ora.clusters()
+    assert ng == no and np.array_equal(lg, lo)
+    assert ng * 17 <= 768 and np.bincount(lo).min() >= 2
+    eng.close()
