@@ -465,7 +465,8 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
 // group owns column b.  The group forms W^_o = W_o V_p^-1 (row b per lane, shared through LDS), then walks the
 // upper partners q of track p -- tracks are sorted by camera at create, so they are exactly [ustart[o], end) --
 // and adds column b of -W^_o W_q^T into slot(cam[q]) with LDS f64 atomics (ds_add_f64).  Each camera's
-// observation list is sorted by partner count so the groups of a wave stay balanced.  The kernel is bound by the
+// observation list is in point order cut into chunks sorted by partner count (create: the groups of a wave stay
+// balanced, and the rows walk the tracks in step).  The kernel is bound by the
 // chain of dependent loads per round, not by bytes (cache-resident partner data: no faster): every own-observation
 // index comes from one descriptor {o, p, partner range} prefetched a round ahead.  Measured and rejected: a
 // precomputed per-pair block position (36 MB streamed per trial, slower than cam[] from cache + an LDS lookup).
@@ -3483,7 +3484,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         });
     }
     // MFMA-accumulating variant for D <= 8 (ba_schur_mf.h): rows in chunks of <= 64 blocks; each chunk's own
-    // observations in batches of 64 taken round-robin from the camera's list (sorted by partner count), so every batch
+    // observations in batches of 64 taken round-robin from the camera's list (partner-count-sorted chunks), so every batch
     // carries about the average number of pairs; every pair's staging position groups the batch's pairs by
     // destination block (own order, then partner order, inside a block).
     const bool no_mf = schur_kind != "mf";
