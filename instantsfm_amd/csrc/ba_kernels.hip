@@ -136,13 +136,45 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // as one contiguous segment in k_schur); each track reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~.
 constexpr int kLinThreads = 128;  // k_lin_points workgroup (LDS: W staging + V/g terms of its observations)
 
+// The first trial's point preparation fused into k_lin_points (the damping factor of a step's first trial is known
+// when the linearization is enqueued: f = 1 + damping): per track the damped V_p (diagonal clamped, times f), its
+// 3x3 inverse and y = V_p^-1 g_p from the same doubles k_point_prep would read back -- bitwise its result -- and the
+// CG status words cleared.  Vinv null: no fusion (retrials, the re-deriving Schur, global positioning).
+struct PointPrep {
+    double f = 1.0, cmin = 0.0, cmax = 0.0;
+    double* Vinv = nullptr;
+    double* y = nullptr;
+    int* flags = nullptr;
+    int* status = nullptr;
+};
+__device__ __forceinline__ void point_prep_one(int p, const double V[6], const double g[3], const PointPrep& a) {
+    double s[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) s[k] = V[k];
+    s[0] = clampd(s[0], a.cmin, a.cmax) * a.f;
+    s[3] = clampd(s[3], a.cmin, a.cmax) * a.f;
+    s[5] = clampd(s[5], a.cmin, a.cmax) * a.f;
+    double o[6];
+    if (!spd3_inverse(s, o)) {
+        atomicOr(a.flags, 1);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) o[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a.Vinv[6 * (size_t)p + k] = o[k];
+    a.y[3 * (size_t)p + 0] = o[0] * g[0] + o[1] * g[1] + o[2] * g[2];
+    a.y[3 * (size_t)p + 1] = o[1] * g[0] + o[3] * g[1] + o[4] * g[2];
+    a.y[3 * (size_t)p + 2] = o[2] * g[0] + o[4] * g[1] + o[5] * g[2];
+}
+
 template <int M, bool STORE_W = true, bool CW = false>
 __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
                                                          const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
                                                          double delta, double* __restrict__ W, double* __restrict__ V,
-                                                         double* __restrict__ gp, double2* __restrict__ obrec) {
+                                                         double* __restrict__ gp, double2* __restrict__ obrec,
+                                                         PointPrep pp1 = PointPrep{}) {
     // STORE_W = false (the re-deriving Schur, ba_schur_rc.h): no W records; each observation's {sqrt(w), camera}
     // goes to obrec instead (16 B, coalesced).
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
@@ -242,7 +274,9 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
         for (int k = 0; k < 6; ++k) V[6 * (size_t)tr + k] = Vs[k];
 #pragma unroll
         for (int k = 0; k < 3; ++k) gp[3 * (size_t)tr + k] = g[k];
+        if (pp1.Vinv) point_prep_one(tr, Vs, g, pp1);  // the first trial's k_point_prep, on the same doubles
     }
+    if (pp1.Vinv && blockIdx.x == 0 && threadIdx.x < 4) pp1.status[threadIdx.x] = 0;  // (k_point_prep's status clear)
 }
 
 // One workgroup per camera: 256 observations at a time are evaluated (one per thread) into an LDS batch
@@ -1737,6 +1771,9 @@ struct insfm_ba {
     hipEvent_t ev_cg0 = nullptr, ev_cgtail = nullptr;
     bool cgtail_pending = false, gate_used = false;
     int gate_seq = 0;  // sequence of the last gate queued (acknowledged in prog_host[4])
+    // the last linearization already prepared the points (Vinv, y, status) for damping factor prep_f (PointPrep)
+    bool prep_valid = false;
+    double prep_f = 0.0;
     int* gate_dev = nullptr;
     double* pub_host = nullptr;  // pinned, device-mapped: k_publish's result[0..4], decision, sequence word (double 8)
     double* pub_dev = nullptr;
@@ -2076,14 +2113,23 @@ int lin_join(insfm_ba* h) {
 
 // k_lin_points writing W in the handle's record format (compact or [3][D]).
 template <int M>
-void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local) {
+void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local, PointPrep pp1 = PointPrep{}) {
     if (h->w_compact)
         k_lin_points<M, true, true><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv,
                                                                            h->pp, cams, pts_local, h->d.huber_delta, h->W,
-                                                                           h->V, h->gp, nullptr);
+                                                                           h->V, h->gp, nullptr, pp1);
     else
         k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
-                                                             pts_local, h->d.huber_delta, h->W, h->V, h->gp, nullptr);
+                                                             pts_local, h->d.huber_delta, h->W, h->V, h->gp, nullptr, pp1);
+}
+
+// The previous solve's CG iterations queued past convergence on the CG stream (INSFM_CG_STREAM=1) exit at the status
+// word the next solve resets: they must have run first (normally long done: then no wait marker is queued).
+int cgtail_join(insfm_ba* h) {
+    if (!h->cgtail_pending) return 0;
+    if (hipEventQuery(h->ev_cgtail) != hipSuccess) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_cgtail, 0));
+    h->cgtail_pending = false;
+    return 0;
 }
 
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
@@ -2100,13 +2146,35 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
     }
     if (int rc0 = lin_join(h)) return rc0;  // (the previous linearization's U / g_c writes come first)
+    if (int rc0 = cgtail_join(h)) return rc0;  // (the fused point preparation below clears the CG status words)
+    // The first trial's point preparation rides along with k_lin_points (W paths; the re-deriving Schur needs its
+    // per-point records from k_point_prep): lm_step's first trial runs at f = 1 + damping.
+    PointPrep pp1;
+    h->prep_valid = false;
+    static const bool fuse_prep = [] { const char* e = std::getenv("INSFM_PREP_FUSE"); return e && *e == '1'; }();
+    if (fuse_prep && h->kind == 0 && !h->schur_rc && h->Pl > 0) {
+        if (h->flags_dirty) {  // a solve without a cost left the flags / status set: clear them first (k_zero_words)
+            k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
+            if (int e = launch_err(h, "k_zero_words")) return e;
+            h->flags_dirty = false;
+        }
+        pp1.f = 1.0 + h->damping;
+        pp1.cmin = h->d.clamp_min;
+        pp1.cmax = h->d.clamp_max;
+        pp1.Vinv = h->Vinv;
+        pp1.y = h->y;
+        pp1.flags = h->flags;
+        pp1.status = h->cg.status;
+        h->prep_valid = true;
+        h->prep_f = pp1.f;
+    }
     hipStream_t cst = h->aux;
     int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int D = kD<M>;
         // k_lin_cams (compute-bound) forks after k_lin_points (HBM-bound) so that it overlaps k_schur (bound by
         // gather latency) instead of competing with k_lin_points for bandwidth
-        if (h->u_late && h->Pl > 0) launch_lin_points_w<M>(h, cams, pts_local);
+        if (h->u_late && h->Pl > 0) launch_lin_points_w<M>(h, cams, pts_local, pp1);
         if (h->u_late) {
             HIPCHK(hipEventRecord(h->ev_lin0, h->stream));
             HIPCHK(hipStreamWaitEvent(h->aux, h->ev_lin0, 0));
@@ -2129,7 +2197,7 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
                     h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, pts_local, h->d.huber_delta, nullptr, h->V,
                     h->gp, h->obrec);
             else
-                launch_lin_points_w<M>(h, cams, pts_local);
+                launch_lin_points_w<M>(h, cams, pts_local, pp1);
         }
         static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
         if constexpr (D <= 9) {
@@ -2384,13 +2452,11 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
-    // the previous solve's iterations queued past convergence on the CG stream exit at the status word this solve
-    // resets: they must have run first (normally long done: then no wait marker is queued)
-    if (h->cgtail_pending) {
-        if (hipEventQuery(h->ev_cgtail) != hipSuccess) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_cgtail, 0));
-        h->cgtail_pending = false;
-    }
+    if (int rc0 = cgtail_join(h)) return rc0;
     h->gate_used = false;
+    // the point preparation of the linearization covers this solve when it runs at the prepared damping factor
+    const bool prepared = h->prep_valid && h->prep_f == f && h->kind == 0;
+    h->prep_valid = false;
     // The non-PD flag is cleared by the k_final that consumed it and the CG status word by k_point_prep; one tiny
     // launch clears both only when that chain is broken (a solve not followed by a cost, or no local points).
     if (h->flags_dirty || h->Pl == 0 || h->kind == 1) {
@@ -2414,7 +2480,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         k_gp_prep_cams<<<h->C, kThreads, 0, h->stream>>>(h->C, h->cam_ptr, h->cam_obs, h->gobs, h->U, h->gc, f,
                                                                      h->d.clamp_min, h->d.clamp_max, h->d.rank == 0, h->Up,
                                                                      h->gpc);
-    } else if (h->Pl > 0 && (hmark(h, "point_prep"), true))
+    } else if (h->Pl > 0 && !prepared && (hmark(h, "point_prep"), true))
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
                                                                        h->Vinv, h->y, h->flags, h->cg.status, pts_local,
                                                                        h->schur_rc ? h->ptrec : nullptr);
