@@ -2151,7 +2151,9 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     // per-point records from k_point_prep): lm_step's first trial runs at f = 1 + damping.
     PointPrep pp1;
     h->prep_valid = false;
-    static const bool fuse_prep = [] { const char* e = std::getenv("INSFM_PREP_FUSE"); return e && *e == '1'; }();
+    // (config 3, same box, 3 runs each: 725 / 722 / 701 -> 733 / 725 / 734 LM it/s; profiles/r3_v13/prep_fuse_ab.log;
+    // INSFM_PREP_FUSE=0 keeps the separate k_point_prep launch)
+    static const bool fuse_prep = [] { const char* e = std::getenv("INSFM_PREP_FUSE"); return !(e && *e == '0'); }();
     if (fuse_prep && h->kind == 0 && !h->schur_rc && h->Pl > 0) {
         if (h->flags_dirty) {  // a solve without a cost left the flags / status set: clear them first (k_zero_words)
             k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
