@@ -29,16 +29,14 @@ FP64_PEAK_TFS = 78.6   # MI355X dense FP64 (MFMA = vector rate on gfx950; SURVEY
 
 
 def w_record_doubles(D):
-    """Doubles per stored W record: [3][D], or the compact {H, Wi} record under INSFM_SCHUR=cw."""
-    return 6 + 3 * (D - 6) if os.environ.get("INSFM_SCHUR") == "cw" else 3 * D
+    """Doubles per stored W record: [3][D]."""
+    return 3 * D
 
 
 def algorithmic_bytes(kernel, C, P, N, D, nnzb):
     """Compulsory HBM bytes of one launch (every input byte read once, every output byte written once)."""
     if kernel == "k_schur":
-        cw = os.environ.get("INSFM_SCHUR") == "cw"
         return (N * w_record_doubles(D) * 8  # W_o records
-                + (P * 3 * 8 + C * (D + 1) * 8 if cw else 0)  # points and camera rows (compact records)
                 + N * 4 * 3            # cam_obs, ptl, cam
                 + (P + 1) * 4          # pt_ptr
                 + P * 9 * 8            # V^-1 (6) + y (3)

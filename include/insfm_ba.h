@@ -70,12 +70,9 @@ typedef struct {
                               plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
                               Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
     int32_t cluster_size;  /* target cameras per coarse cluster (default 14; grown until nclust*(D+1) <= 768) */
-    int32_t schur_variant; /* reduced-system build (BA, deterministic = 0): 0 (default) reads the stored camera-point
-                              blocks W; 1 re-derives them per pair, LDS-atomic row accumulation; 2 re-derives them,
-                              MFMA register accumulation (D <= 8, else 1).  1 and 2 never form W (no 192 B/obs write).
-                              3 stores compact W records {J~p^T J~p, J~c,intr^T J~p} (96 B/obs for D = 8) and applies
-                              each camera's rotation and centre per block (any deterministic setting).
-                              The environment variable INSFM_SCHUR=w|rc|mf|cw overrides it. */
+    int32_t schur_variant; /* reduced-system build: must be 0 (EINVAL otherwise).  Kept for the struct layout: the
+                              round-2/3 variants 1-3 (re-derived or compact camera-point blocks) were measured slower
+                              or even and removed. */
     insfm_ba_allreduce_async_fn allreduce_async; /* optional (see above); uses allreduce_ctx */
     int32_t exchange_chunks;  /* row chunks of the [S | b] exchange overlapped with the Schur build when allreduce_async
                                  is set (default 4; 1 = one all-reduce after the whole build) */
@@ -136,8 +133,13 @@ int insfm_ba_cost(insfm_ba* h, const double* cam_params, const double* points, d
 int64_t insfm_ba_exchange_count(const insfm_ba* h);
 int insfm_ba_set_exchange(insfm_ba* h, double* dev_buf, int64_t count);
 
-/* Forget the cached loss/damping state (a fresh LM, as TorchBA builds one per Solve). */
+/* A fresh LM on the same problem, as TorchBA builds one per Solve: forgets the cached loss, the damping / TrustRegion
+ * state and the lagged coarse inverse of the two-level preconditioner (the next solve factorizes its own). */
 int insfm_ba_reset(insfm_ba* h);
+
+/* Free the device buffers that destroyed handles parked for reuse (process-wide cache, at most
+ * INSFM_DEVICE_CACHE_MB, default 4096 MB; invisible to PyTorch's caching allocator).  Returns the bytes released. */
+int64_t insfm_ba_release_cache(void);
 
 void insfm_ba_destroy(insfm_ba* h);
 const char* insfm_ba_last_error(const insfm_ba* h);

@@ -60,6 +60,7 @@ SYMBOLS = ("insfm_build_info", "insfm_ba_default_desc", "insfm_ba_create", "insf
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
            "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters", "insfm_ba_debug_spd_inverse",
+           "insfm_ba_release_cache",
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
            "insfm_gp_debug_get_ds",
            "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
@@ -98,7 +99,7 @@ def _check_provenance(L, path):
 
 def load(path=None):
     """Load the HIP library (no GPU needed to load it).  Raises if it was not built.  ``INSFM_LIB`` names another
-    build of the same library (tools/schur_variants.sh compiles kernel variants for timing)."""
+    build of the same library (A/B timing of kernel variants on one box; its provenance is not checked)."""
     global _lib
     if _lib is not None:
         return _lib
@@ -144,6 +145,8 @@ def load(path=None):
     L.insfm_ba_debug_clusters.restype = ctypes.c_int32
     L.insfm_ba_debug_spd_inverse.argtypes = [ctypes.c_int32, vp, vp, vp, ctypes.c_int32, dp]
     L.insfm_ba_debug_spd_inverse.restype = ctypes.c_int
+    L.insfm_ba_release_cache.argtypes = []
+    L.insfm_ba_release_cache.restype = ctypes.c_int64
     ip = ctypes.POINTER(ctypes.c_int32)
     L.insfm_gp_default_desc.argtypes = [ctypes.POINTER(Desc)]
     L.insfm_gp_default_desc.restype = None
@@ -184,6 +187,12 @@ def gp_default_desc():
     d = Desc()
     load().insfm_gp_default_desc(ctypes.byref(d))
     return d
+
+
+def release_device_cache():
+    """Free the device buffers destroyed handles parked for reuse (insfm_ba_release_cache); returns the bytes freed.
+    Those buffers are invisible to PyTorch's caching allocator: call this before large torch allocations."""
+    return int(load().insfm_ba_release_cache())
 
 
 def check(h, rc):

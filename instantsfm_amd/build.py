@@ -61,8 +61,15 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def packx_hash():
+    """SHA-256 (first 16 hex digits) of csrc/packx.c: compiled into the extension as _packx.SRC_HASH and compared at
+    import (processors/bundle_adjustment.py), like the main library's provenance check."""
+    with open(PACKX_SRC, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def needs_build():
-    return _stale(OUT, SRCS + HEADERS)
+    return _stale(OUT, SRCS + HEADERS) or _stale(PACKX_OUT, [PACKX_SRC])
 
 
 def build(force=False, verbose=True):
@@ -105,7 +112,8 @@ def build_packx(force=False, verbose=True):
     if not (force or _stale(PACKX_OUT, [PACKX_SRC])):
         return PACKX_OUT
     cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-std=c99",
-           "-Wall", f"-I{sysconfig.get_paths()['include']}", f"-I{_numpy_include()}", "-o", PACKX_OUT + ".tmp", PACKX_SRC]
+           "-Wall", f'-DPACKX_SRC_HASH="{packx_hash()}"', f"-I{sysconfig.get_paths()['include']}",
+           f"-I{_numpy_include()}", "-o", PACKX_OUT + ".tmp", PACKX_SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -296,7 +296,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur_gp(const int4* __restrict_
                                                          const double* __restrict__ W, const double* __restrict__ VY,
                                                          const double* __restrict__ Up,
                                                          const double* __restrict__ gpc, double* __restrict__ S,
-                                                         double* __restrict__ b, int probe) {
+                                                         double* __restrict__ b) {
     constexpr int NT = WAVES * 64, BS = 9, NGW = NT / G;
     static_assert(64 % G == 0, "lane groups must tile a wave");
     extern __shared__ __attribute__((aligned(16))) double sh[];
@@ -333,7 +333,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur_gp(const int4* __restrict_
         w.cq = -1;
         if (q < d.w) { w.q = Wr[q]; w.cq = cam[q]; }
     };
-    const int eend = probe == 4 ? ob : oe;
+    const int eend = oe;
     int4 dcur = make_int4(0, 0, 0, 0), dnext = make_int4(0, 0, 0, 0);
     Own cur, nxt;
     if (ob + g < eend) { dcur = sdesc[ob + g]; load_own(dcur, cur); }
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur_gp(const int4* __restrict_
 #pragma unroll
             for (int k = 0; k < 3; ++k) br[k] -= w[k][0] * yv[0] + w[k][1] * yv[1] + w[k][2] * yv[2];
         }
-        for (int q = dcur.z + l; q < (probe == 3 ? dcur.z : dcur.w); q += G) {
+        for (int q = dcur.z + l; q < dcur.w; q += G) {
             const bool first = q == dcur.z + l;
             const double4 rq = first ? cur.q : Wr[q];
             const int sl = slot[first ? cur.cq : cam[q]];
@@ -375,9 +375,7 @@ __global__ __launch_bounds__(WAVES * 64) void k_schur_gp(const int4* __restrict_
 #pragma unroll
                 for (int m = 0; m < 3; ++m) {
                     const double val = rq.w * (wh[k][m] - wu * uq[m]);
-                    if (probe == 0) atomicAdd(dst + k * 3 + m, val);
-                    else if (probe == 1) dst[k * 3 + m] += val;  // timing probe only (racy)
-                    else if (val == 1.2345e-300) dst[0] = val;    // timing probe only (no accumulation)
+                    atomicAdd(dst + k * 3 + m, val);
                 }
             }
         }

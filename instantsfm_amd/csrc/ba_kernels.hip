@@ -8,8 +8,8 @@
 //                          k_cg_factor / k_cg_scale : S_ii = L L^T, S~ = L^-1 S L^-T, r0 = L^-1 b
 //                          k_cg_iter x k : Chronopoulos-Gear CG on S~, ONE launch per iteration
 //                          k_cg_finish   : dc = L^-T x~
-//                          k_backsub     : dp = V^-1 (g_p - W^T dc), trial points, gain terms
-//                          k_update_cams : SE3 left retraction, intrinsics +=, gain terms
+//                          k_backsub_rc  : dp = V^-1 (g_p - W^T dc), trial points, gain terms; its last blocks the
+//                                          SE3 left retraction of the cameras, intrinsics +=, gain terms
 //                          k_cost        : Huber loss + sum ||r||^2 at the trial parameters
 //                          k_final       : fixed-order reduction of all partials -> 64 B to the host
 // Every cross-workgroup reduction is a fixed-order partial sum (no float atomics in global memory), so a step is
@@ -38,8 +38,6 @@
 #include "ba_twolevel.h"
 #include "ba_gp.h"
 #include "cg_poll.h"
-#include "ba_schur_rc.h"
-#include "ba_schur_mf.h"
 #include "create_host.h"
 
 using namespace insfm;
@@ -55,6 +53,7 @@ constexpr int kLdsTarget = SCHUR_LDS_KB * 1024;
 #define INSFM_SCHUR_WAVES 8
 #endif
 constexpr int kSchurWaves = INSFM_SCHUR_WAVES;  // waves per k_schur workgroup (non-deterministic mode)
+constexpr int kSchurChunk = 4;  // k_schur rounds per chunk of a camera's observation list (create)
 #ifndef LIN_CAMS_NT
 #define LIN_CAMS_NT 128  // k_lin_cams_reg threads per camera (measured 128 / 192 / 256 / 320: 0.156 / 0.161 / 0.167 / 0.194 ms linearize)
 #endif
@@ -67,20 +66,6 @@ constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 /
 #endif
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
-#endif
-#ifndef SCHUR_UP_C
-#define SCHUR_UP_C 5  // partners in flight per group with the compact W record (6 values per lane each)
-#endif
-#ifndef SCHUR_CW_VEC
-#define SCHUR_CW_VEC 0  // 1: compact records of even length read in 16-B pieces (measured: k_schur 556 -> 755 us)
-#endif
-#ifndef SCHUR_CW_TAB
-#define SCHUR_CW_TAB 1  // k_schur's row write-out: each block's column camera {R, c} formed once into LDS
-#endif
-// doubles per compact W record {H (6), Wi [ni][3]} for camera block dimension D = 6 + ni (see k_schur)
-__host__ __device__ constexpr int wrec_len(int D) { return 6 + 3 * (D - 6); }
-#ifndef SCHUR_RC_WAVES
-#define SCHUR_RC_WAVES 4  // waves per k_schur_rc workgroup
 #endif
 
 // ------------------------------------------------------------------------------------------------------------
@@ -167,23 +152,19 @@ __device__ __forceinline__ void point_prep_one(int p, const double V[6], const d
     a.y[3 * (size_t)p + 2] = o[2] * g[0] + o[4] * g[1] + o[5] * g[2];
 }
 
-template <int M, bool STORE_W = true, bool CW = false>
+template <int M>
 __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
                                                          const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
                                                          double delta, double* __restrict__ W, double* __restrict__ V,
-                                                         double* __restrict__ gp, double2* __restrict__ obrec,
-                                                         PointPrep pp1 = PointPrep{}) {
-    // STORE_W = false (the re-deriving Schur, ba_schur_rc.h): no W records; each observation's {sqrt(w), camera}
-    // goes to obrec instead (16 B, coalesced).
+                                                         double* __restrict__ gp, PointPrep pp1 = PointPrep{}) {
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
     // is longer), one thread per observation: coalesced uv / cam / point loads and 192-B W records written by
     // consecutive lanes (16 B per lane).  Each observation's V / g_p terms go to LDS and one thread per track adds them
     // in observation order -- the same sequence of additions as a thread walking its track.  The terms reuse the W
     // staging area once the records are stored (one 25.6-KB LDS buffer: 6 workgroups per CU instead of 4).
-    // CW: the compact record {H, Wi} (wrec_len) instead of W_o [3][D]
-    constexpr int D = kD<M>, ST = kStride<M>, WR = CW ? wrec_len(D) : 3 * D, WRP = WR | 1;  // odd LDS row stride
+    constexpr int D = kD<M>, ST = kStride<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride
     static_assert(WRP >= 9, "the V / g terms reuse a W staging row");
     __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here; then the V / g terms
     const int t = threadIdx.x;
@@ -204,7 +185,6 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             double r[2], Jc[2][D], Jp[2][3];
             eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
             const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
-            if (obrec) obrec[o] = make_double2(sw, (double)c);
             r[0] *= sw; r[1] *= sw;
 #pragma unroll
             for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
@@ -216,15 +196,7 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             cv[3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
             cv[4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
             cv[5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
-            if constexpr (STORE_W && CW) {
-                double* Wo = wst + (size_t)t * WRP;
-#pragma unroll
-                for (int k = 0; k < 6; ++k) Wo[k] = cv[k];
-#pragma unroll
-                for (int a = 6; a < D; ++a)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) Wo[6 + 3 * (a - 6) + k] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
-            } else if constexpr (STORE_W) {
+            {
                 double* Wo = wst + (size_t)t * WRP;
 #pragma unroll
                 for (int a = 0; a < D; ++a)
@@ -235,8 +207,7 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
             for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
         }
         const int n = min(kLinThreads, oe - base);
-        if constexpr (!STORE_W) {
-        } else if constexpr ((WR & 1) == 0) {
+        if constexpr ((WR & 1) == 0) {
             __syncthreads();
             // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive
             // 16-B pairs (WR even: a pair never crosses a record, and every record starts 16-B aligned)
@@ -455,9 +426,7 @@ __global__ __launch_bounds__(NT) void k_lin_cams_reg(const int* __restrict__ cam
 __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* __restrict__ V, const double* __restrict__ gp,
                                                          double f, double cmin, double cmax, double* __restrict__ Vinv,
                                                          double* __restrict__ y, int* __restrict__ flags,
-                                                         int* __restrict__ status, const double* __restrict__ pts,
-                                                         double* __restrict__ ptrec) {
-    // ptrec (the re-deriving Schur): per point {V^-1 (6), y (3), X (3)} in one 96-B record
+                                                         int* __restrict__ status) {
     const int p = blockIdx.x * kThreads + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0;  // the CG status word of this solve
     if (p >= Pl) return;
@@ -482,15 +451,6 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
     y[3 * (size_t)p + 0] = y0;
     y[3 * (size_t)p + 1] = y1;
     y[3 * (size_t)p + 2] = y2;
-    if (ptrec) {
-        double2* r = reinterpret_cast<double2*>(ptrec + 12 * (size_t)p);
-        r[0] = make_double2(o[0], o[1]);
-        r[1] = make_double2(o[2], o[3]);
-        r[2] = make_double2(o[4], o[5]);
-        r[3] = make_double2(y0, y1);
-        r[4] = make_double2(y2, pts[3 * (size_t)p]);
-        r[5] = make_double2(pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]);
-    }
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -528,127 +488,7 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
     }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// Compact W record (BA, D = 6 + ni; the default): 96 B instead of 192 B per observation for D = 8.
-// With the pose tangent under left perturbation (ba_device.h) and R the camera's rotation matrix,
-//   J~p = A R,  J~c = [A | -A [p_c]x | J~c,intr],  p_c = R X + t = R (X - c),  c = -R^T t (camera centre), so
-//   W_o = J~c^T J~p = [R H ; R [X - c]x H ; Wi],  H = J~p^T J~p (3x3 symmetric),  Wi = J~c,intr^T J~p (ni x 3).
-// The record stores {H packed [xx xy xz yy yz zz], Wi [ni][3]}; every camera-dependent factor is applied where the
-// camera is known: the own observation's rows are rebuilt with camera i's R and the point (row of the workgroup), and
-// for a partner q on camera j the products against W_q^T factor as
-//   W^_o W_q^T = [T R_j^T | -(T [X - c_i]x + T [c_i - c_j]x) R_j^T | W^_o Wi_q^T],  T = W^_o H_q,
-// so k_schur accumulates A1 = sum T, A2 = sum T [X - c_i]x (the point is the own observation's, so X - c_i is fixed
-// over its partners) and A3 = sum W^_o Wi_q^T per block -- the same D x D slots and the same LDS adds as the full
-// record -- and applies R_j, c_j once per block when the row is written.  Assumes unit quaternions, like the analytic
-// pose Jacobian itself (dp_c/dphi = -[p_c]x holds only for a rotation).
-// ------------------------------------------------------------------------------------------------------------
-
-// Rotation matrix of a stored pose [t, q_xyzw] (the matrix eval_obs applies: I + 2w[q]x + 2[q]x^2) and the camera
-// centre c = -R^T t: out = {R row-major (9), c (3)}.
-__device__ __forceinline__ void pose_rc(const double* __restrict__ cam, double out[12]) {
-    const double qx = cam[3], qy = cam[4], qz = cam[5], qw = cam[6];
-    const double K[3][3] = {{0.0, -qz, qy}, {qz, 0.0, -qx}, {-qy, qx, 0.0}};
-#pragma unroll
-    for (int a = 0; a < 3; ++a)
-#pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const double kk = K[a][0] * K[0][b] + K[a][1] * K[1][b] + K[a][2] * K[2][b];
-            out[3 * a + b] = (a == b ? 1.0 : 0.0) + 2.0 * qw * K[a][b] + 2.0 * kk;
-        }
-#pragma unroll
-    for (int b = 0; b < 3; ++b) out[9 + b] = -(out[b] * cam[0] + out[3 + b] * cam[1] + out[6 + b] * cam[2]);
-}
-
-// Lane cb's view of compact record o: cb < 6 -> x = H (packed); cb >= 6 -> x = {row cb - 6 of Wi, 0, 0, 0}.  Every
-// lane then forms its column as v = H u (hmul) with a per-lane u: a Wi row comes out of the same product with u = e0.
-template <int D>
-__device__ __forceinline__ void load_crec(const double* __restrict__ W, int o, int cb, double x[6]) {
-    constexpr int R = wrec_len(D);
-    const int s = cb < 6 ? 0 : 6 + 3 * (cb - 6);  // first value of this lane's part of the record
-    if constexpr (SCHUR_CW_VEC && R % 2 == 0) {
-        // even record length: every record starts 16-B aligned, so the lane's values come in 16-B pieces from the
-        // aligned start at or below s (a Wi row at an odd offset takes the upper half of the first piece; the W
-        // allocation is padded so the last record's last piece stays inside it)
-        const double2* p = reinterpret_cast<const double2*>(W + (size_t)o * R + (s & ~1));
-        const double2 l0 = p[0], l1 = p[1];
-        const double2 l2 = cb < 6 ? p[2] : make_double2(0.0, 0.0);
-        if (cb < 6) {
-            x[0] = l0.x; x[1] = l0.y; x[2] = l1.x; x[3] = l1.y; x[4] = l2.x; x[5] = l2.y;
-        } else {
-            const bool odd = s & 1;
-            x[0] = odd ? l0.y : l0.x; x[1] = odd ? l1.x : l0.y; x[2] = odd ? l1.y : l1.x;
-            x[3] = 0.0; x[4] = 0.0; x[5] = 0.0;
-        }
-    } else {
-        const double* r = W + (size_t)o * R + s;
-        x[0] = r[0]; x[1] = r[1]; x[2] = r[2];
-        x[3] = 0.0; x[4] = 0.0; x[5] = 0.0;
-        if (cb < 6) { x[3] = r[3]; x[4] = r[4]; x[5] = r[5]; }
-    }
-}
-__device__ __forceinline__ void hmul(const double x[6], const double u[3], double& v0, double& v1, double& v2) {
-    v0 = x[0] * u[0] + x[1] * u[1] + x[2] * u[2];
-    v1 = x[1] * u[0] + x[3] * u[1] + x[4] * u[2];
-    v2 = x[2] * u[0] + x[4] * u[1] + x[5] * u[2];
-}
-// The per-lane vectors of one own observation (point X, row camera {R, c} in rc):
-//   own (row cb of W_o = (H uo)^T): cb < 3 -> row cb of R; cb 3..5 -> row k of R [d]x = R[k] x d; else e0;
-//   partner (column cb of the accumulated slot = W^_o H_q up):  cb < 3 -> e_cb;  cb 3..5 -> d x e_k;  else e0;
-// with d = X - c and k = cb - 3.
-__device__ __forceinline__ void crec_u(int cb, const double* rc, const double X[3], double uo[3], double up[3]) {
-    const double d0 = X[0] - rc[9], d1 = X[1] - rc[10], d2 = X[2] - rc[11];
-    uo[0] = 1.0; uo[1] = 0.0; uo[2] = 0.0;
-    up[0] = 1.0; up[1] = 0.0; up[2] = 0.0;
-    if (cb < 3) {
-        uo[0] = rc[3 * cb]; uo[1] = rc[3 * cb + 1]; uo[2] = rc[3 * cb + 2];
-        up[0] = cb == 0 ? 1.0 : 0.0; up[1] = cb == 1 ? 1.0 : 0.0; up[2] = cb == 2 ? 1.0 : 0.0;
-    } else if (cb < 6) {
-        const int k = cb - 3;
-        const double r0 = rc[3 * k], r1 = rc[3 * k + 1], r2 = rc[3 * k + 2];
-        uo[0] = r1 * d2 - r2 * d1; uo[1] = r2 * d0 - r0 * d2; uo[2] = r0 * d1 - r1 * d0;
-        // d x e_k
-        up[0] = k == 0 ? 0.0 : (k == 1 ? -d2 : d1);
-        up[1] = k == 0 ? d2 : (k == 1 ? 0.0 : -d0);
-        up[2] = k == 0 ? -d1 : (k == 1 ? d0 : 0.0);
-    }
-}
-// Entry (a, b) of the written block for column camera j from the accumulated slot row ab = acc row a (see above):
-// b < 3: A1_a . R_j[b];  b in 3..5: -(A2_a + A1_a x (c_i - c_j)) . R_j[b - 3];  else A3_a,b.
-__device__ __forceinline__ double crec_out(const double* ab, int b, const double* rj, const double* ci) {
-    if (b < 3) return ab[0] * rj[3 * b] + ab[1] * rj[3 * b + 1] + ab[2] * rj[3 * b + 2];
-    if (b < 6) {
-        const int k = b - 3;
-        const double e0 = ci[0] - rj[9], e1 = ci[1] - rj[10], e2 = ci[2] - rj[11];
-        const double s0 = ab[3] + (ab[1] * e2 - ab[2] * e1);
-        const double s1 = ab[4] + (ab[2] * e0 - ab[0] * e2);
-        const double s2 = ab[5] + (ab[0] * e1 - ab[1] * e0);
-        return -(s0 * rj[3 * k] + s1 * rj[3 * k + 1] + s2 * rj[3 * k + 2]);
-    }
-    return ab[b];
-}
-
-// Debug getter: the full W_o [3][D] of every observation rebuilt from its compact record (the own-row path of k_schur).
-template <int D>
-__global__ __launch_bounds__(kThreads) void k_w_expand(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
-                                                       const double* __restrict__ camsl, const double* __restrict__ ptsl,
-                                                       const double* __restrict__ W, double* __restrict__ out) {
-    const int o = blockIdx.x * kThreads + threadIdx.x;
-    if (o >= Nl) return;
-    double rc[12];
-    pose_rc(camsl + (size_t)cam[o] * (D + 1), rc);
-    const double* xp = ptsl + 3 * (size_t)ptl[o];
-    const double X[3] = {xp[0], xp[1], xp[2]};
-    for (int cb = 0; cb < D; ++cb) {
-        double x[6], uo[3], up[3], w0, w1, w2;
-        load_crec<D>(W, o, cb, x);
-        crec_u(cb, rc, X, uo, up);
-        hmul(x, uo, w0, w1, w2);
-        double* wo = out + (size_t)o * 3 * D + cb;
-        wo[0] = w0; wo[D] = w1; wo[2 * D] = w2;
-    }
-}
-
-template <int D, int WAVES, bool GPW = false, bool CW = false>
+template <int D, int WAVES, bool GPW = false>
 __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
@@ -658,35 +498,23 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                                                       const double* __restrict__ Vinv, const double* __restrict__ y,
                                                       const double* __restrict__ U, const double* __restrict__ gc, double f,
                                                       double cmin, double cmax, int add_diag, double* __restrict__ S,
-                                                      double* __restrict__ b, const double* __restrict__ camsl = nullptr,
-                                                      const double* __restrict__ ptsl = nullptr) {
-    // CW: compact W records (see wrec_len); camsl / ptsl = cameras and points of the linearization
+                                                      double* __restrict__ b) {
     constexpr int DD = D * D;
     constexpr int BS = schur_bs(D);  // LDS stride of an accumulated block (padded off the 64-bank period)
     constexpr int WS = schur_ws(D);  // LDS stride of a group's W^ staging
     constexpr int NG = 64 / D;  // observation groups per wave
     constexpr int NT = WAVES * 64;
-    constexpr int XN = CW ? 6 : 3;  // values per lane of a partner record
     extern __shared__ __attribute__((aligned(16))) double sh[];
     const int4 wk = work[blockIdx.x];
     const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
     double* acc = sh;
     double* wsh = acc + (size_t)nb * BS;           // [WAVES][NG][WS]  W^ rows ([D][4], padded group stride)
     double* bacc = wsh + (size_t)WAVES * NG * WS;  // [D]
-    double* rci = bacc + D;                        // [12] row camera {R, c} (CW)
-    int* slot = reinterpret_cast<int*>(rci + 12);  // [C]
+    int* slot = reinterpret_cast<int*>(bacc + D + 12);  // [C]
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     for (int k = t; k < nb * BS; k += NT) acc[k] = 0.0;
     for (int k = t; k < C; k += NT) slot[k] = -1;
     if (t < D) bacc[t] = 0.0;
-    if constexpr (CW) {
-        if (t == 0) {
-            double rc[12];
-            pose_rc(camsl + (size_t)i * (D + 1), rc);
-#pragma unroll
-            for (int k = 0; k < 12; ++k) rci[k] = rc[k];
-        }
-    }
     __syncthreads();
     for (int e = kb + t; e < ke; e += NT) slot[col[e]] = e - kb;
     __syncthreads();
@@ -711,42 +539,25 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             const int en = e + WAVES * NG;
             if (active && en < oe) dnext = sdesc[en];
         }
-        constexpr int UP = CW ? SCHUR_UP_C : SCHUR_UP;  // partners in flight per group
+        constexpr int UP = SCHUR_UP;  // partners in flight per group
         const int qs = has ? dcur.z : 0, qe = has ? dcur.w : 0;
         const int n = qe - qs;
         // issue order = wait order (vmcnt retires in order): the own record first, then the first UP partner records,
         // so the W^ staging waits only for the own record while the partner loads stay in flight
         double w0 = 0.0, w1 = 0.0, w2 = 0.0, v00 = 0.0, v01 = 0.0, v02 = 0.0, v11 = 0.0, v12 = 0.0, v22 = 0.0;
-        double xo[XN];
-        double up[3] = {1.0, 0.0, 0.0};
-        double X[3] = {0.0, 0.0, 0.0};
         if (has) {
             const double* vi = Vinv + 6 * (size_t)dcur.y;
             v00 = vi[0]; v01 = vi[1]; v02 = vi[2]; v11 = vi[3]; v12 = vi[4]; v22 = vi[5];
-            if constexpr (CW) {
-                load_crec<D>(W, dcur.x, cb, xo);
-                const double* xp = ptsl + 3 * (size_t)dcur.y;
-                X[0] = xp[0]; X[1] = xp[1]; X[2] = xp[2];
-            } else {
-                load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
-            }
+            load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
         }
-        double x[UP][XN];
+        double x[UP][3];
         int cj[UP];
 #pragma unroll
         for (int u = 0; u < UP; ++u) {
             cj[u] = -1;
             if (u < n) {
-                if constexpr (CW) load_crec<D>(W, qs + u, cb, x[u]);
-                else load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
+                load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
                 cj[u] = cam[qs + u];
-            }
-        }
-        if constexpr (CW) {
-            if (has) {  // own row cb of W_o from the record, the row camera and the point
-                double uo[3];
-                crec_u(cb, rci, X, uo, up);
-                hmul(xo, uo, w0, w1, w2);
             }
         }
         if (has) {
@@ -779,8 +590,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     cj[u] = -1;
                     if (k0 + u < n) {
                         const int q = qs + k0 + u;
-                        if constexpr (CW) load_crec<D>(W, q, cb, x[u]);
-                        else load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
+                        load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
                         cj[u] = cam[q];
                     }
                 }
@@ -791,9 +601,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     const int sl = slot[cj[u]];
                     if (sl >= 0) {
                         double* dst = acc + (size_t)sl * BS + cb;
-                        double y0, y1, y2;
-                        if constexpr (CW) hmul(x[u], up, y0, y1, y2);
-                        else { y0 = x[u][0]; y1 = x[u][1]; y2 = x[u][2]; }
+                        const double y0 = x[u][0], y1 = x[u][1], y2 = x[u][2];
 #pragma unroll
                         for (int a2 = 0; a2 < D; ++a2)
                             atomicAdd(dst + a2 * D, -(wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2));
@@ -805,40 +613,10 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
     }
     if (diag_chunk && active) atomicAdd(bacc + cb, breg);
     __syncthreads();
-    // CW: the blocks' column cameras {R, c}, formed once per block into the (now free) W^ staging area when it fits
-    const bool ctab = CW && SCHUR_CW_TAB && nb * 12 <= WAVES * NG * WS;
-    if constexpr (CW) {
-        if (ctab) {
-            for (int bk = t; bk < nb; bk += NT) {
-                double rj[12];
-                pose_rc(camsl + (size_t)col[kb + bk] * (D + 1), rj);
-#pragma unroll
-                for (int q = 0; q < 12; ++q) wsh[12 * bk + q] = rj[q];
-            }
-            __syncthreads();
-        }
-    }
     double* Sout = S + (size_t)kb * DD;
     const double* Ui = U + (size_t)i * DD;
     for (int k = t; k < nb * DD; k += NT) {
-        double v;
-        if constexpr (CW) {  // camera j's rotation and centre applied to the block's accumulated [A1 | A2 | A3]
-            const int bk = k / DD, e2 = k - bk * DD, a2 = e2 / D, bb = e2 - a2 * D;
-            const double* ab = acc + (size_t)bk * BS + a2 * D;
-            if (bb < 6) {
-                if (ctab) {
-                    v = crec_out(ab, bb, wsh + 12 * bk, rci + 9);
-                } else {
-                    double rj[12];
-                    pose_rc(camsl + (size_t)col[kb + bk] * (D + 1), rj);
-                    v = crec_out(ab, bb, rj, rci + 9);
-                }
-            } else {
-                v = ab[bb];
-            }
-        } else {
-            v = acc[(k / DD) * BS + k % DD];
-        }
+        double v = acc[(k / DD) * BS + k % DD];
         if (diag_chunk && add_diag && k < DD) {
             const int a2 = k / D, bb = k % D;
             double u = Ui[k];
@@ -1107,7 +885,7 @@ template <int D>
 __global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit, double tol2_rel,
                                                         const int* __restrict__ nbr_ptr, const int* __restrict__ nbr_j,
                                                         const double* __restrict__ Sn, const double* __restrict__ Lf,
-                                                        CgBufs cg, int probe) {
+                                                        CgBufs cg) {
     using G = CgGeom<D>;
     constexpr int DD = D * D;
     constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = G::BPR;
@@ -1125,8 +903,8 @@ __global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit
     const bool lane_on = (PPB <= 64) ? (bw < BPW) : true;
     const int slot = wv * BPW + bw;                  // block slot within the round
     // ======== phase 1: loads independent of alpha / beta ========
-    const int status = (probe & 8) ? 0 : cg.status[0];
-    const int n0 = nbr_ptr[row], n1 = (probe & 2) ? nbr_ptr[row] : nbr_ptr[row + 1];
+    const int status = cg.status[0];
+    const int n0 = nbr_ptr[row], n1 = nbr_ptr[row + 1];
     double acc[PPL];
 #pragma unroll
     for (int m = 0; m < PPL; ++m) acc[m] = 0.0;
@@ -1179,7 +957,7 @@ __global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit
     // recurrence scalars published by k_cg_dots (uniform loads)
     double alpha = 0.0, beta = 0.0;
     if (it > 0) {
-        if ((probe & 8) == 0 && cg.scal[2] != 0.0) return;
+        if (cg.scal[2] != 0.0) return;
         alpha = cg.scal[0];
         beta = cg.scal[1];
     }
@@ -1269,91 +1047,6 @@ __global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __r
 // ------------------------------------------------------------------------------------------------------------
 // back-substitution, parameter update, cost
 // ------------------------------------------------------------------------------------------------------------
-// dp = V^-1 (g_p - sum_o W_o^T dc_c(o)); trial points; gain part  2 t.dp - dp^T V dp  (block partial).
-// dp = V^-1 (g_p - sum_o W_o^T dc_cam(o)) per track, trial points, gain part 2 g_p.dp - dp^T V dp.  Same runs of whole
-// tracks as k_lin_points.  Per chunk of the run's observations: the W records (contiguous in HBM) are copied to LDS by
-// consecutive lanes and every thread loads its observation's camera step; thread o forms q_o = W_o^T dc (a = 0..D-1 in
-// order) from LDS, and one thread per track subtracts its q_o in observation order -- the arithmetic of a thread
-// walking its track, without a dependent global load per observation.
-template <int D>
-__global__ __launch_bounds__(kLinThreads) void k_backsub(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
-                                                         const int* __restrict__ cam, const double* __restrict__ W,
-                                                         const double* __restrict__ dc, const double* __restrict__ V,
-                                                         const double* __restrict__ Vinv, const double* __restrict__ gp,
-                                                         const double* __restrict__ pts, double* __restrict__ dp,
-                                                         double* __restrict__ pts_new, double* __restrict__ part) {
-    constexpr int WR = 3 * D, WRP = WR | 1;
-    __shared__ double red[kLinThreads];
-    __shared__ double wst[kLinThreads * WRP];
-    __shared__ double q[kLinThreads][3];
-    const int t = threadIdx.x;
-    const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
-    const int p = tb + t;
-    const bool own = p < te;
-    double gain[1] = {0.0};
-    double t0 = 0.0, t1 = 0.0, t2 = 0.0;
-    if (own) { t0 = gp[3 * (size_t)p]; t1 = gp[3 * (size_t)p + 1]; t2 = gp[3 * (size_t)p + 2]; }
-    if (dc) {
-        const int ob = pt_ptr[tb], oe = pt_ptr[te];
-        const int lo = own ? pt_ptr[p] : 0, hi = own ? pt_ptr[p + 1] : 0;
-        for (int base = ob; base < oe; base += kLinThreads) {
-            const int n = min(kLinThreads, oe - base);
-            const double* src = W + (size_t)base * WR;
-            double buf[WR];  // thread t holds doubles t, t + kLinThreads, ... of the chunk: every load issued first
-#pragma unroll
-            for (int j = 0; j < WR; ++j) {
-                const int k = t + j * kLinThreads;
-                if (k < n * WR) buf[j] = src[k];
-            }
-#pragma unroll
-            for (int j = 0; j < WR; ++j) {
-                const int k = t + j * kLinThreads;
-                if (k < n * WR) wst[(k / WR) * WRP + k % WR] = buf[j];
-            }
-            double d[D];
-            if (t < n) {
-                const double* dr = dc + (size_t)cam[base + t] * D;
-#pragma unroll
-                for (int a = 0; a < D; ++a) d[a] = dr[a];
-            }
-            __syncthreads();
-            if (t < n) {
-                const double* Wo = wst + (size_t)t * WRP;
-                double s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-                for (int a = 0; a < D; ++a) {
-                    s0 += Wo[a] * d[a];
-                    s1 += Wo[D + a] * d[a];
-                    s2 += Wo[2 * D + a] * d[a];
-                }
-                q[t][0] = s0; q[t][1] = s1; q[t][2] = s2;
-            }
-            __syncthreads();
-            for (int o = max(lo, base); o < min(hi, base + n); ++o) {
-                t0 -= q[o - base][0]; t1 -= q[o - base][1]; t2 -= q[o - base][2];
-            }
-            __syncthreads();
-        }
-    }
-    if (own) {
-        const double* vi = Vinv + 6 * (size_t)p;
-        const double d0 = vi[0] * t0 + vi[1] * t1 + vi[2] * t2;
-        const double d1 = vi[1] * t0 + vi[3] * t1 + vi[4] * t2;
-        const double d2 = vi[2] * t0 + vi[4] * t1 + vi[5] * t2;
-        dp[3 * (size_t)p] = d0; dp[3 * (size_t)p + 1] = d1; dp[3 * (size_t)p + 2] = d2;
-        pts_new[3 * (size_t)p] = pts[3 * (size_t)p] + d0;
-        pts_new[3 * (size_t)p + 1] = pts[3 * (size_t)p + 1] + d1;
-        pts_new[3 * (size_t)p + 2] = pts[3 * (size_t)p + 2] + d2;
-        const double* v = V + 6 * (size_t)p;
-        const double Vd0 = v[0] * d0 + v[1] * d1 + v[2] * d2;
-        const double Vd1 = v[1] * d0 + v[3] * d1 + v[4] * d2;
-        const double Vd2 = v[2] * d0 + v[4] * d1 + v[5] * d2;
-        gain[0] = 2.0 * (t0 * d0 + t1 * d1 + t2 * d2) - (d0 * Vd0 + d1 * Vd1 + d2 * Vd2);
-    }
-    block_sum<1, kLinThreads>(gain, red);
-    if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
-}
-
 // Cameras: X <- Exp(dc_pose) X, intrinsics += dc_intr; gain part 2 g_c.dc - dc^T U dc (rank 0 only).  One block of NT
 // cameras per call; the block's gain partial goes to part[blk].
 template <int M, int NT>
@@ -1393,10 +1086,12 @@ __device__ __forceinline__ void update_cams_block(int blk, int C, const double* 
     if (threadIdx.x == 0) part[blk] = gain[0];
 }
 
-// The same back-substitution with W_o^T dc re-derived from the observation instead of read from W: J~ is evaluated
-// again at the linearization point exactly as k_lin_points does (same inputs, same code: the same J~c, J~p) and
-// q_o = J~p^T (J~c dc).  It reads ~50 B per observation (uv, camera / point index, the run's points) instead of the
-// 192-B W record, and the evaluation costs less than the record's HBM time.
+// Back-substitution: dp = V^-1 (g_p - sum_o W_o^T dc_cam(o)) per track, trial points, gain part 2 g_p.dp - dp^T V dp
+// (block partial).  Same runs of whole tracks as k_lin_points, one thread per observation; W_o^T dc is re-derived
+// instead of read from W: J~ is evaluated again at the linearization point exactly as k_lin_points does (same inputs,
+// same code: the same J~c, J~p) and q_o = J~p^T (J~c dc); one thread per track subtracts its q_o in observation order.
+// It reads ~50 B per observation (uv, camera / point index, the run's points) instead of the 192-B W record, and the
+// evaluation costs less than the record's HBM time (the W-reading form measured 107 vs 64 us on config 3).
 template <int M>
 __global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restrict__ blk, const int* __restrict__ pt_ptr,
                                                             const int* __restrict__ cam, const int* __restrict__ ptl,
@@ -1472,15 +1167,6 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restric
     }
     block_sum<1, kLinThreads>(gain, red);
     if (threadIdx.x == 0) part[blockIdx.x] = gain[0];
-}
-
-template <int M>
-__global__ __launch_bounds__(kLinThreads) void k_update_cams(int C, const double* __restrict__ cams, const double* __restrict__ dc,
-                                                             const double* __restrict__ U, const double* __restrict__ gc,
-                                                             int with_gain, double* __restrict__ cams_new,
-                                                             double* __restrict__ part) {
-    __shared__ double red[kLinThreads / 64];
-    update_cams_block<M, kLinThreads>(blockIdx.x, C, cams, dc, U, gc, with_gain, cams_new, part, red);
 }
 
 // Huber loss and sum ||r||^2 (block partials).  (Measured: 4 observations per thread, loads hoisted, ran 25 -> 33 us.)
@@ -1575,7 +1261,7 @@ __global__ __launch_bounds__(kThreads) void k_derive_cm(int Nl, const int* __res
 }
 
 // Upper block pattern of S and the co-visibility weights on the device (create, single rank; the host pass in create
-// is the multi-rank / INSFM_PATTERN_HOST=1 path and gives the same lists): one workgroup per camera row i counts, in
+// is the multi-rank / INSFM_DIAG=pattern_host path and gives the same lists): one workgroup per camera row i counts, in
 // LDS, for every camera j the (observation of i, observation of j) pairs sharing a track, walking each own
 // observation's upper partners [ustart, track end) exactly like k_schur.  `off` null: cnt[i] = #{j > i with pairs};
 // else the j > i in increasing order and their pair counts go to nb / wt from off[i] (the second pass recounts).
@@ -1633,27 +1319,6 @@ __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) 
     else if (t < 8) status[t - 4] = 0;
 }
 
-// Main-stream gate of a CG running on its own stream: one thread waits (s_sleep between system-scope loads of the
-// host-mapped status word, which the converging k_tl_pc(_cl) publishes with a system-scope release after its final
-// iterate is complete) until the status is non-zero, then records it in *code for k_publish.  Bounded: after
-// `limit` ticks of the 100-MHz real-time counter it gives up with code -1 (the host reports the CG error itself and
-// releases the gate by writing the status word on every error path).
-// On exit it stores `seq` into prog[4] (system scope): the host resets the status word for the next solve only after
-// that acknowledgement, so a gate can never miss its own status.
-__global__ void k_cg_gate(int* prog, int* __restrict__ code, long long limit, int seq) {
-    if (threadIdx.x != 0) return;
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    int v = 0;
-    for (;;) {
-        v = __hip_atomic_load(prog + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v != 0) break;
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > limit) { v = -1; break; }
-        __builtin_amdgcn_s_sleep(2);
-    }
-    *code = v;
-    __hip_atomic_store(prog + 4, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // After k_final (and the cross-rank sum): result[0..4] into host-mapped memory for the host's spin-wait, then
 // sequence word `seq` (system-scope release), so the host reads the trial's cost without a stream synchronization or a
 // copy launch.  With `cams_cur` set (insfm_ba_step: the caller's buffers hold the current parameters) the accepted
@@ -1664,10 +1329,9 @@ __global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__
                                                       int can_reject, const double* __restrict__ cams_new,
                                                       double* __restrict__ cams_cur, long long ncam,
                                                       const double* __restrict__ pts_new, double* __restrict__ pts_cur,
-                                                      long long npts, const int* __restrict__ gate) {
+                                                      long long npts) {
     const double loss = result[0];
-    // (gate: the CG status its gate saw -- anything but a converged CG is never accepted)
-    const bool acc = result[4] == 0.0 && !(last < loss && can_reject) && (gate == nullptr || *gate == 1);
+    const bool acc = result[4] == 0.0 && !(last < loss && can_reject);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int k = 0; k < 5; ++k) pub[k] = result[k];
         pub[5] = acc ? 1.0 : 0.0;
@@ -1716,7 +1380,6 @@ struct insfm_ba {
     int n_lin = 0;
     double* cm_uv = nullptr; // k_lin_cams: per camera-major observation, its uv
     double* Sn = nullptr;  // row-contiguous scaled neighbour blocks for the CG (both triangles, padded rows)
-    int probe = 0;         // INSFM_CG_PROBE: timing-only bisection of k_cg_iter phases (results are wrong when != 0)
     int64_t n_nbr = 0;
     int nbr_stride = 0;  // > 0: every CG row has exactly nbr_stride neighbour slots (padded), row r starts at r * stride
     bool flags_dirty = false;  // a solve's point preparation ran and no k_final has consumed (cleared) its flag yet
@@ -1724,25 +1387,6 @@ struct insfm_ba {
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
-    // re-deriving Schur (ba_schur_rc.h; BA, non-deterministic): its own row chunks, per-observation {sqrt(w), camera},
-    // per-point {V^-1, y, X}; W is then never formed
-    bool schur_rc = false;
-    int4* work_rc = nullptr;
-    int nwork_rc = 0;
-    size_t schur_rc_lds = 0;
-    double2* obrec = nullptr;
-    double* ptrec = nullptr;
-    const double* cams_lin = nullptr;  // camera rows of the last linearization (caller's or internal buffer)
-    const double* pts_lin = nullptr;   // its (local) points
-    bool w_compact = false;            // W holds the compact records {H, Wi} (wrec_len); INSFM_W_FULL=1: [3][D] records
-    // MFMA-accumulating variant (ba_schur_mf.h, D <= 8): work items, batch-ordered own descriptors, staging positions
-    bool schur_mf = false;
-    MfWork* mf_work = nullptr;
-    int n_mf_work = 0, mf_pcap = 0;
-    int4* mf_sd = nullptr;
-    unsigned short* mf_ppos = nullptr;
-    int* mf_boff = nullptr;
-    size_t schur_mf_lds = 0;
     // numeric (device)
     double *W = nullptr, *V = nullptr, *gp = nullptr, *Vinv = nullptr, *y = nullptr, *dp = nullptr;
     double *xbuf = nullptr;  // [S | b | U | gc | scal]
@@ -1762,19 +1406,9 @@ struct insfm_ba {
     int* flags = nullptr;
     double* host_res = nullptr;  // pinned 128 B: result[0..4] (doubles) | cg status (ints, from double slot 8)
     int* prog_host = nullptr;    // pinned, device-mapped: progress of the two-level CG (CgBufs::prog)
-    // CG on its own stream (single rank, two-level; opt-in, INSFM_CG_STREAM=1): the iterations go to `cgs` behind
-    // one event of the main stream, and the main stream continues at once with k_cg_gate (spins on the published
-    // status word) and the post-CG kernels, so they start as soon as the CG converges instead of after the host has
-    // seen the status and after the iterations queued past convergence.  ev_cgtail: the last iteration queued on cgs
-    // (the next solve's status reset waits for it); gate_dev: the status the gate saw (k_publish accepts only 1).
-    hipStream_t cgs = nullptr;
-    hipEvent_t ev_cg0 = nullptr, ev_cgtail = nullptr;
-    bool cgtail_pending = false, gate_used = false;
-    int gate_seq = 0;  // sequence of the last gate queued (acknowledged in prog_host[4])
     // the last linearization already prepared the points (Vinv, y, status) for damping factor prep_f (PointPrep)
     bool prep_valid = false;
     double prep_f = 0.0;
-    int* gate_dev = nullptr;
     double* pub_host = nullptr;  // pinned, device-mapped: k_publish's result[0..4], decision, sequence word (double 8)
     double* pub_dev = nullptr;
     unsigned pub_seq = 0;
@@ -1802,9 +1436,6 @@ struct insfm_ba {
     int* okbuf = nullptr;  // [2]
     hipStream_t side = nullptr;
     hipEvent_t ev_E = nullptr, ev_built = nullptr, ev_fact[2]{};
-    // the side-stream chain of a solve still to be issued (slot, next unit): issued a launch at a time from the CG's
-    // host poll loop, where the host otherwise only spins
-    int side_slot = -1, side_next = 0;
     // chunked [S | b] exchange (desc.allreduce_async): work-item / row boundaries of the chunks, the exchange stream
     std::vector<int> xw, xr, rptr_host;
     hipStream_t xstream = nullptr;
@@ -1818,7 +1449,6 @@ struct insfm_ba {
     bool built_pending = false;
     long long tl_solves = 0;
     bool tl_fresh = false;  // no solve since the last linearization (the lag rule applies to that solve only)
-    bool tl_sync = false;  // INSFM_TL_SYNC=1: factorize on the main stream (debug)
     int coarse_used = 0;
     // global positioning (kind 1, insfm_gp_*): per local observation ray / scale-free flag / source index, camera
     // factors, the linearization records and the scale-eliminated camera blocks of the current trial
@@ -1841,16 +1471,42 @@ namespace {
         }                                                                                         \
     } while (0)
 
+// INSFM_DIAG: comma-separated diagnostics, read once per process (none is on by default):
+//   poison        every buffer dalloc hands out is first filled with 0xff bytes (NaN doubles, -1 ints), so a read of
+//                 something never written shows up instead of a fresh allocation's zero pages
+//   pattern_host  create builds the block pattern by the host pass (the multi-rank path) on a single rank too
+//   trace         per solve, host microseconds spent enqueueing CG iterations (stderr)
+//   trace2        per LM step, host timestamps of the step's API calls (stderr)
+//   create        host milliseconds of create's phases (stderr)
+bool diag(const char* name) {
+    static const std::string v = [] { const char* e = std::getenv("INSFM_DIAG"); return std::string(e ? e : ""); }();
+    const size_t n = std::strlen(name);
+    for (size_t a = 0; a <= v.size();) {
+        size_t b = v.find(',', a);
+        if (b == std::string::npos) b = v.size();
+        if (b - a == n && v.compare(a, n, name) == 0) return true;
+        a = b + 1;
+    }
+    return false;
+}
+
 // Process-wide cache of the device buffers of destroyed handles.  TorchBA creates a handle per Solve (the mapper
 // solves 4-5 times per reconstruction), and freeing config 3's ~1 GB of buffers took ~7 ms per destroy (hipFree
 // synchronizes the device) plus the allocations of the next create.  insfm_ba_destroy waits for the handle's streams
-// and parks its buffers here; dalloc takes the smallest parked buffer of at least the requested size and at most
-// twice it.  Bounded by INSFM_DEVICE_CACHE_MB (default 16384; 0 disables it): beyond that, buffers are freed.
+// and parks its buffers here, keyed by their HIP device; dalloc takes the smallest parked buffer of the current device
+// of at least the requested size and at most twice it.  Bounded by INSFM_DEVICE_CACHE_MB (default 4096; 0 disables
+// it): beyond that, buffers are freed.  The parked memory is invisible to PyTorch's caching allocator, so
+// insfm_ba_release_cache() frees it all (TorchBA calls it when torch reports an out-of-memory error, the mapper at the
+// end of a reconstruction); a failing hipMalloc inside dalloc releases it too.
 struct DeviceCache {
+    struct Buf {
+        size_t bytes;
+        int dev;
+    };
     std::mutex m;
-    std::multimap<size_t, void*> free;  // size -> pointer
+    std::map<std::pair<int, size_t>, std::vector<void*>> free;  // (device, size) -> pointers
     size_t bytes = 0;
-    std::unordered_map<void*, size_t> size_of;  // every pointer dalloc handed out (cached or fresh)
+    std::unordered_map<void*, Buf> info;  // every pointer dalloc handed out (cached or fresh)
 };
 DeviceCache& device_cache() {
     static DeviceCache* c = new DeviceCache();  // (never destroyed: buffers may be parked until process exit)
@@ -1859,50 +1515,65 @@ DeviceCache& device_cache() {
 size_t device_cache_cap() {
     static const size_t v = [] {
         const char* e = std::getenv("INSFM_DEVICE_CACHE_MB");
-        return (size_t)(e ? std::max(0LL, std::atoll(e)) : 16384LL) << 20;
+        return (size_t)(e ? std::max(0LL, std::atoll(e)) : 4096LL) << 20;
     }();
     return v;
 }
 
-// INSFM_DEVICE_POISON=1 (diagnostic): every buffer dalloc hands out is first filled with 0xff bytes (NaN doubles,
-// -1 ints), so a read of something never written shows up instead of reading a fresh allocation's zero pages.
-bool device_poison() {
-    static const bool v = [] { const char* e = std::getenv("INSFM_DEVICE_POISON"); return e && *e == '1'; }();
-    return v;
+// frees every parked buffer (any device); returns the bytes released
+size_t release_cache() {
+    DeviceCache& c = device_cache();
+    std::vector<std::pair<void*, int>> drop;
+    size_t n = 0;
+    {
+        std::lock_guard<std::mutex> lk(c.m);
+        for (auto& kv : c.free)
+            for (void* q : kv.second) {
+                drop.emplace_back(q, kv.first.first);
+                c.info.erase(q);
+            }
+        c.free.clear();
+        n = c.bytes;
+        c.bytes = 0;
+    }
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto& d : drop) {
+        if (d.second != cur) (void)hipSetDevice(d.second);
+        (void)hipFree(d.first);
+        if (d.second != cur) (void)hipSetDevice(cur);
+    }
+    (void)hipGetLastError();
+    return n;
 }
 
 int dalloc(insfm_ba* h, void** p, size_t bytes) {
     if (bytes == 0) bytes = 16;
     bytes = (bytes + 255) & ~(size_t)255;
     DeviceCache& c = device_cache();
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     bool hit = false;
     {
         std::lock_guard<std::mutex> lk(c.m);
-        auto it = c.free.lower_bound(bytes);
-        if (it != c.free.end() && it->first <= 2 * bytes) {
-            *p = it->second;
-            c.bytes -= it->first;
-            c.free.erase(it);
+        auto it = c.free.lower_bound(std::make_pair(dev, bytes));
+        if (it != c.free.end() && it->first.first == dev && it->first.second <= 2 * bytes && !it->second.empty()) {
+            *p = it->second.back();
+            it->second.pop_back();
+            c.bytes -= it->first.second;
+            if (it->second.empty()) c.free.erase(it);
             hit = true;
         }
     }
     if (hit) {
         h->allocs.push_back(*p);
-        if (device_poison()) (void)hipMemset(*p, 0xff, bytes);
+        if (diag("poison")) (void)hipMemset(*p, 0xff, bytes);
         return 0;
     }
     hipError_t e = hipMalloc(p, bytes);
     if (e == hipErrorOutOfMemory) {  // give the parked buffers back and try once more
-        std::vector<void*> drop;
-        {
-            std::lock_guard<std::mutex> lk(c.m);
-            for (auto& kv : c.free) drop.push_back(kv.second);
-            for (void* q : drop) c.size_of.erase(q);
-            c.free.clear();
-            c.bytes = 0;
-        }
-        for (void* q : drop) (void)hipFree(q);
         (void)hipGetLastError();
+        release_cache();
         e = hipMalloc(p, bytes);
     }
     if (e != hipSuccess) {
@@ -1911,10 +1582,10 @@ int dalloc(insfm_ba* h, void** p, size_t bytes) {
     }
     {
         std::lock_guard<std::mutex> lk(c.m);
-        c.size_of[*p] = bytes;
+        c.info[*p] = DeviceCache::Buf{bytes, dev};
     }
     h->allocs.push_back(*p);
-    if (device_poison()) (void)hipMemset(*p, 0xff, bytes);
+    if (diag("poison")) (void)hipMemset(*p, 0xff, bytes);
     return 0;
 }
 
@@ -1926,18 +1597,19 @@ void dfree_all(insfm_ba* h) {
     {
         std::lock_guard<std::mutex> lk(c.m);
         for (void* q : h->allocs) {
-            auto it = c.size_of.find(q);
-            const size_t sz = it == c.size_of.end() ? 0 : it->second;
-            if (sz == 0 || c.bytes + sz > cap) {
-                if (it != c.size_of.end()) c.size_of.erase(it);
+            auto it = c.info.find(q);
+            if (it == c.info.end()) { drop.push_back(q); continue; }
+            const DeviceCache::Buf b = it->second;
+            if (c.bytes + b.bytes > cap) {
+                c.info.erase(it);
                 drop.push_back(q);
             } else {
-                c.free.emplace(sz, q);
-                c.bytes += sz;
+                c.free[std::make_pair(b.dev, b.bytes)].push_back(q);
+                c.bytes += b.bytes;
             }
         }
     }
-    for (void* q : drop) (void)hipFree(q);
+    for (void* q : drop) (void)hipFree(q);  // (hipFree takes a pointer of any device)
     h->allocs.clear();
 }
 
@@ -2014,14 +1686,14 @@ void rec(insfm_ba* h, int k) {
     if (h->timing) (void)hipEventRecord(h->ev[k], h->stream);
 }
 
-// INSFM_HOST_TRACE=2: host timestamps of one LM step's API calls (labels + microseconds since the step began),
+// INSFM_DIAG=trace2: host timestamps of one LM step's API calls (labels + microseconds since the step began),
 // printed to stderr when the step ends -- where the host, not the GPU, sets the pace
-int host_trace_level() {
-    static const int v = [] { const char* e = std::getenv("INSFM_HOST_TRACE"); return e ? std::atoi(e) : 0; }();
+bool host_trace2() {
+    static const bool v = diag("trace2");
     return v;
 }
 void hmark(insfm_ba* h, const char* what) {
-    if (host_trace_level() >= 2) h->hmarks.emplace_back(what, wall_seconds());
+    if (host_trace2()) h->hmarks.emplace_back(what, wall_seconds());
 }
 
 // after a stream sync: add the device time between events a and b to phase `slot`
@@ -2111,31 +1783,14 @@ int lin_join(insfm_ba* h) {
     return 0;
 }
 
-// k_lin_points writing W in the handle's record format (compact or [3][D]).
 template <int M>
 void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local, PointPrep pp1 = PointPrep{}) {
-    if (h->w_compact)
-        k_lin_points<M, true, true><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv,
-                                                                           h->pp, cams, pts_local, h->d.huber_delta, h->W,
-                                                                           h->V, h->gp, nullptr, pp1);
-    else
-        k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
-                                                             pts_local, h->d.huber_delta, h->W, h->V, h->gp, nullptr, pp1);
-}
-
-// The previous solve's CG iterations queued past convergence on the CG stream (INSFM_CG_STREAM=1) exit at the status
-// word the next solve resets: they must have run first (normally long done: then no wait marker is queued).
-int cgtail_join(insfm_ba* h) {
-    if (!h->cgtail_pending) return 0;
-    if (hipEventQuery(h->ev_cgtail) != hipSuccess) HIPCHK(hipStreamWaitEvent(h->stream, h->ev_cgtail, 0));
-    h->cgtail_pending = false;
-    return 0;
+    k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
+                                                         pts_local, h->d.huber_delta, h->W, h->V, h->gp, pp1);
 }
 
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
     h->tl_fresh = true;
-    h->cams_lin = cams;  // the re-deriving Schur evaluates the camera Jacobians at this linearization point
-    h->pts_lin = pts_local;  // (and the compact-record Schur rebuilds the camera factors of W from both)
     if (h->kind == 1) {
         if (h->Nl > 0)
             k_gp_lin<<<cdiv(h->Nl, kThreads), kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, h->sfree,
@@ -2146,15 +1801,12 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
     }
     if (int rc0 = lin_join(h)) return rc0;  // (the previous linearization's U / g_c writes come first)
-    if (int rc0 = cgtail_join(h)) return rc0;  // (the fused point preparation below clears the CG status words)
-    // The first trial's point preparation rides along with k_lin_points (W paths; the re-deriving Schur needs its
-    // per-point records from k_point_prep): lm_step's first trial runs at f = 1 + damping.
+    // The first trial's point preparation rides along with k_lin_points: lm_step's first trial runs at
+    // f = 1 + damping (config 3, same box, 3 runs each: 725 / 722 / 701 -> 733 / 725 / 734 LM it/s against a separate
+    // k_point_prep launch; profiles/r3_v13/prep_fuse_ab.log).
     PointPrep pp1;
     h->prep_valid = false;
-    // (config 3, same box, 3 runs each: 725 / 722 / 701 -> 733 / 725 / 734 LM it/s; profiles/r3_v13/prep_fuse_ab.log;
-    // INSFM_PREP_FUSE=0 keeps the separate k_point_prep launch)
-    static const bool fuse_prep = [] { const char* e = std::getenv("INSFM_PREP_FUSE"); return !(e && *e == '0'); }();
-    if (fuse_prep && h->kind == 0 && !h->schur_rc && h->Pl > 0) {
+    if (h->kind == 0 && h->Pl > 0) {
         if (h->flags_dirty) {  // a solve without a cost left the flags / status set: clear them first (k_zero_words)
             k_zero_words<<<1, 64, 0, h->stream>>>(h->flags, h->cg.status);
             if (int e = launch_err(h, "k_zero_words")) return e;
@@ -2193,21 +1845,11 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
             h->lin_pending = true;
             return launch_err(h, "k_lin_points");
         }
-        if (h->Pl > 0) {
-            if (h->schur_rc)
-                k_lin_points<M, false><<<h->n_lin, kLinThreads, 0, h->stream>>>(
-                    h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, pts_local, h->d.huber_delta, nullptr, h->V,
-                    h->gp, h->obrec);
-            else
-                launch_lin_points_w<M>(h, cams, pts_local, pp1);
-        }
-        static const bool batch_form = std::getenv("INSFM_LIN_CAMS_BATCH") != nullptr;  // experiments: old form
+        if (h->Pl > 0) launch_lin_points_w<M>(h, cams, pts_local, pp1);
         if constexpr (D <= 9) {
-            if (!batch_form) {
-                k_lin_cams_reg<M><<<h->C, LIN_CAMS_NT, 0, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams,
-                                                                    pts_local, h->d.huber_delta, h->U, h->gc);
-                return launch_err(h, "linearize");
-            }
+            k_lin_cams_reg<M><<<h->C, LIN_CAMS_NT, 0, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams,
+                                                                pts_local, h->d.huber_delta, h->U, h->gc);
+            return launch_err(h, "linearize");
         }
         const size_t lds = sizeof(double) * kThreads * (2 * D + 2);
         k_lin_cams<M><<<h->C, kThreads, lds, h->stream>>>(h->cam_ptr, h->cm_pt, h->cm_uv, h->pp, cams, pts_local,
@@ -2234,14 +1876,17 @@ int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
     });
 }
 
+// The side stream's E build runs with at most kErowGrid workgroups (rows strided over the grid): with one workgroup
+// per row it held CU / LDS slots the overlapping CG launches needed (config 3, round 1: grid 1000 / 512 / 384 / 256 /
+// 192 / 128 -> 593 / 616 / 612-615 / 603 / 594 LM it/s).
+constexpr int kErowGrid = 256;
 int run_tl_build(insfm_ba* h, int slot, hipStream_t stream) {
     const int C = h->C, m = h->tl.m;
     TlBufs tl = h->tl;
     tl.E = h->Ebuf[slot];
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
-        static const int grid_cap = [] { const char* e = std::getenv("INSFM_EROW_GRID"); return e ? std::atoi(e) : 256; }();
-        const int grid = (grid_cap > 0 && stream != h->stream) ? std::min(C, grid_cap) : C;
+        const int grid = stream != h->stream ? std::min(C, kErowGrid) : C;
         k_tl_erow<DV><<<grid, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
         k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, stream>>>(tl);
         return launch_err(h, "k_tl_erow/ereduce");
@@ -2270,96 +1915,43 @@ int run_tl_gj_unit(insfm_ba* h, int slot, int u, hipStream_t stream) {
 #define CG_INIT_BACK 2
 #endif
 constexpr int kCgAhead = CG_AHEAD;
-#ifndef SIDE_AHEAD
-#define SIDE_AHEAD 2
-#endif
-constexpr int kSideAhead = SIDE_AHEAD;  // extra CG iterations kept queued while side-chain units remain to be issued  // CG iterations the host keeps queued ahead of the device (pipelined two-level PCG)
 
-// The side-stream chain of a solve, in issue units: 0 = wait for the basis (ev_E), E build (k_tl_erow, k_tl_ereduce),
-// ev_built; 1 .. nB + 1 = the Gauss-Jordan launches, the last followed by ev_fact[slot].  Each unit is one or two
-// kernel launches (~5-10 us of host time each), so the chain can be issued piecemeal while the host waits on the CG.
-int side_units(const insfm_ba* h) { return 2 + gj_steps(h->tl.m); }
-
-// INSFM_EROW_MAIN=1: the E build runs on the main stream with its full grid right after the basis (experiment:
-// the capped side-stream build overlaps and slows several CG iterations).
-bool erow_on_main() {
-    static const bool v = [] { const char* e = std::getenv("INSFM_EROW_MAIN"); return e && std::atoi(e) != 0; }();
-    return v;
-}
-
-int side_issue(insfm_ba* h) {
-    if (h->side_slot < 0) return 0;
-    const int slot = h->side_slot, u = h->side_next;
-    hipStream_t fs = h->tl_sync ? h->stream : h->side;
-    int rc = 0;
-    if (u == 0) {
-        HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
-        if (!(erow_on_main() && !h->tl_sync) && (rc = run_tl_build(h, slot, fs))) return rc;
-        HIPCHK(hipEventRecord(h->ev_built, fs));
-        h->built_pending = true;
-    } else if ((rc = run_tl_gj_unit(h, slot, u - 1, fs))) {
-        return rc;
-    }
-    if (++h->side_next == side_units(h)) {
-        HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
-        h->side_slot = -1;
-    }
+// The side-stream chain of solve `slot`: wait for the basis (ev_E), the E build (k_tl_erow, k_tl_ereduce), ev_built,
+// then the Gauss-Jordan launches, the last followed by ev_fact[slot].  The whole chain (~20 launches) is issued at the
+// solve's setup, while the GPU is still in k_lin_points / k_schur: the host is then ~0.6 ms ahead of the GPU, the
+// launches cost the GPU nothing, and the chain overlaps the CG.  (Round 2 issued it piecemeal from the CG poll loop,
+// and a chain deferred past the CG was measured too: both slower)
+int issue_side_chain(insfm_ba* h, int slot) {
+    hipStream_t fs = h->side;
+    HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
+    if (int rc = run_tl_build(h, slot, fs)) return rc;
+    HIPCHK(hipEventRecord(h->ev_built, fs));
+    h->built_pending = true;
+    for (int u = 0; u <= gj_steps(h->tl.m); ++u)
+        if (int rc = run_tl_gj_unit(h, slot, u, fs)) return rc;
+    HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
     return 0;
 }
 
-int side_drain(insfm_ba* h) {
-    int rc = 0;
-    while (h->side_slot >= 0 && !(rc = side_issue(h))) {}
-    return rc;
-}
-
-// Side-chain schedule (INSFM_SIDE_SCHED).  0 (default, round 3): the whole chain of a lagged solve is issued at
-// its setup, right after the basis -- the host is then ~0.6 ms ahead of the GPU (k_schur has not even started), so
-// the ~20 launches cost the GPU nothing, the chain still starts when the basis is done and overlaps the CG, and the
-// CG poll loop has nothing but CG launches to issue (no extra iterations queued past convergence for it).
-// 2 (round 2's default): the chain is issued piecemeal from the CG poll loop while the host waits; what the CG leaves
-// unissued is issued while the host waits for the trial cost, the rest right after the next solve's k_schur.
-// 1: nothing is issued from the poll loop -- the whole chain overlaps back-substitution, the cost, the next
-// linearization and k_schur instead of the CG.  The lag rule is the same in all three (the next solve's
-// k_cg_scale / k_tl_basis wait for the E build; its CG waits for the factorization).
-int side_sched() {
-    static const int v = [] { const char* e = std::getenv("INSFM_SIDE_SCHED"); return e ? std::atoi(e) : 0; }();
-    return v;
-}
-
-// Issue side units while the main stream is still busy (the host would otherwise only wait).
-int side_issue_while_busy(insfm_ba* h) {
-    int rc = 0;
-    while (h->side_slot >= 0 && hipStreamQuery(h->stream) == hipErrorNotReady && !(rc = side_issue(h))) {}
-    return rc;
-}
-
-// Everything of the side chain issued and finished (debug getters, kernel timing, destroy).
+// Everything of the side chain finished (debug getters, kernel timing, destroy, reset).
 int side_flush(insfm_ba* h) {
-    int rc = side_drain(h);
     if (h->side) HIPCHK(hipStreamSynchronize(h->side));
-    return rc;
+    return 0;
 }
 
-// Per-solve setup on the main stream: the basis, then this solve's side chain is queued (side_slot).  Under the lag
-// rule the CG runs with the previous solve's E^-1 and the chain is issued piecemeal from the CG's poll loop (the
-// host time of issuing it does not hold back the CG); a solve that needs its own E^-1 issues it here and waits.
+// Per-solve setup on the main stream: the basis, then this solve's side chain; the CG uses the previous solve's
+// E^-1 under the lag rule, else its own (the main stream waits for the factorization).
 int run_tl_setup(insfm_ba* h, const double* cams) {
-    int rc = side_drain(h);  // (normally already issued after the previous k_schur; see run_solve)
-    if (rc) return rc;
     const int slot = (int)(h->tl_solves & 1);
-    if ((rc = run_tl_basis(h, cams, h->stream))) return rc;
-    if (erow_on_main() && !h->tl_sync && (rc = run_tl_build(h, slot, h->stream))) return rc;
+    int rc = run_tl_basis(h, cams, h->stream);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(h->ev_E, h->stream));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
-    h->side_slot = slot;
-    h->side_next = 0;
-    if ((use == slot || side_sched() == 0) && (rc = side_drain(h))) return rc;
+    if ((rc = issue_side_chain(h, slot))) return rc;
     // a lagged solve's coarse inverse normally finished long ago: a completed event needs no wait marker in the main
-    // queue (each one idles it a few us); INSFM_FACT_WAIT=1 always queues the wait
-    static const bool always_wait = [] { const char* e = std::getenv("INSFM_FACT_WAIT"); return e && std::atoi(e) != 0; }();
-    if (always_wait || use == slot || hipEventQuery(h->ev_fact[use]) != hipSuccess)
+    // queue (each one idles it a few us; always queueing it measured 659-665 vs 659-664 LM it/s, round 2)
+    if (use == slot || hipEventQuery(h->ev_fact[use]) != hipSuccess)
         HIPCHK(hipStreamWaitEvent(h->stream, h->ev_fact[use], 0));
     h->tl.Einv = h->Einvbuf[use];
     h->tl.ok = h->okbuf + use;
@@ -2378,8 +1970,7 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
                                                               h->cg, h->tl);
     }
-    static const bool pc_cl = [] { const char* e = std::getenv("INSFM_PC_CL"); return !e || std::atoi(e) != 0; }();
-    if (h->tl.Racc && pc_cl)
+    if (h->tl.Racc)  // per-cluster atomic sums of the row partials (single rank, non-deterministic)
         k_tl_pc_cl<D><<<h->tl.nc, kPcThreads, 0, h->stream>>>(it, h->C, maxit, tol2, h->cg, h->tl, h->tl.Einv);
     else
         k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
@@ -2401,31 +1992,8 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
                 h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
         else
             k_schur_gp<kSchurWaves, kGPSG><<<h->nwork, nt, h->schur_lds, h->stream>>>(
-                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->cam, h->W, h->VY, Uin, gcin, h->S, h->b,
-                h->probe);
+                h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->cam, h->W, h->VY, Uin, gcin, h->S, h->b);
         return launch_err(h, "k_schur");
-    }
-    if (h->schur_mf) {
-        return with_model(h->model, [&](auto mc) -> int {
-            constexpr int M = decltype(mc)::value;
-            if constexpr (kD<M> <= 8) {
-                k_schur_mf<M><<<h->n_mf_work, 256, h->schur_mf_lds, h->stream>>>(
-                    h->mf_work, h->row_ptr, h->col, h->C, h->mf_sd, h->mf_ppos, h->mf_boff, h->mf_pcap, h->obrec, h->ptrec,
-                    h->cams_lin, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
-                return launch_err(h, "k_schur_mf");
-            } else {
-                return INSFM_BA_EINVAL;
-            }
-        });
-    }
-    if (h->schur_rc) {
-        return with_model(h->model, [&](auto mc) -> int {
-            constexpr int M = decltype(mc)::value;
-            k_schur_rc<M, SCHUR_RC_WAVES><<<h->nwork_rc, SCHUR_RC_WAVES * 64, h->schur_rc_lds, h->stream>>>(
-                h->work_rc, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->obrec, h->ptrec, h->cams_lin, Uin, gcin, sf,
-                smin, smax, sdiag, h->S, h->b);
-            return launch_err(h, "k_schur_rc");
-        });
     }
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
@@ -2433,29 +2001,138 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(w1 - w0), dim3(nt), h->schur_lds, h->stream,
                 h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
-                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, h->cams_lin, h->pts_lin);
+                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
         };
-        if constexpr (DV >= 7) {
-            if (h->w_compact) {
-                if (det) go(k_schur<DV, 1, false, true>);
-                else go(k_schur<DV, kSchurWaves, false, true>);
-                return launch_err(h, "k_schur");
-            }
-        }
-        {
-            if (det) go(k_schur<DV, 1>);
-            else go(k_schur<DV, kSchurWaves>);
-        }
+        if (det) go(k_schur<DV, 1>);
+        else go(k_schur<DV, kSchurWaves>);
         return launch_err(h, "k_schur");
     });
+}
+
+// The two-level CG (precond 1): iterations enqueued from a host poll loop, no stream sync inside the CG.  k_tl_pc's
+// lead workgroup publishes its progress into host-mapped memory; more iterations are enqueued while the GPU has fewer
+// than kCgAhead pending, and the loop ends when the status word turns non-zero.  The few iterations enqueued past
+// convergence exit at the device status flag.  Returns 0 with st[0..2] = {status, iterations, coarse used}.
+int run_tl_cg(insfm_ba* h, int* st) {
+    const int D = h->D, maxit = h->d.pcg_max_iter;
+    const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
+    volatile int* pg = h->prog_host;
+    pg[0] = pg[1] = pg[2] = pg[3] = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    // INSFM_DIAG=trace: per solve, host microseconds spent enqueueing CG iterations and the longest single call
+    static const bool htrace = diag("trace");
+    double t_enq = 0.0, m_enq = 0.0, t_sol0 = htrace ? wall_seconds() : 0.0;
+    int n_enq = 0;
+    auto enqueue = [&](int from, int to) -> int {
+        const double t0 = htrace ? wall_seconds() : 0.0;
+        const int r = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
+            return launch_err(h, "k_tl_pc/k_tl_pspmv");
+        });
+        if (htrace) { const double dt = wall_seconds() - t0; t_enq += dt; m_enq = std::max(m_enq, dt / std::max(1, to - from)); n_enq += to - from; }
+        return r;
+    };
+    rec(h, 8);
+    // multi-rank: the CG's first launch waits for the exchange (the slowest peer); the stall deadline starts once
+    // everything queued in front of the CG has completed (ev_pre), and that gate has its own longer deadline
+    const bool gated = h->d.world_size > 1 || h->d.allreduce;
+    if (gated) HIPCHK(hipEventRecord(h->ev_pre, h->stream));
+    // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step); the loop
+    // below tops up one iteration at a time
+    int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
+    if (int rc = enqueue(0, enq)) return rc;
+    CgPoll poll;
+    poll.enq = enq;
+    static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
+    int erc = 0;
+    const int pr = cg_poll(
+        poll, maxit + 2, kCgAhead, stall_s, cg_gate_limit_s(stall_s), [&] { return (int)pg[1]; },
+        [&] { return (int)pg[0]; }, enqueue,
+        [&] {
+            const hipError_t q = hipStreamQuery(h->stream);
+            if (q == hipSuccess) { std::atomic_thread_fence(std::memory_order_seq_cst); return 0; }
+            return q == hipErrorNotReady ? 1 : -1;
+        },
+        wall_seconds,
+        [] {
+#if defined(__x86_64__)
+            __builtin_ia32_pause();
+#endif
+        },
+        [&] { return !gated || hipEventQuery(h->ev_pre) != hipErrorNotReady; }, &erc);
+    hmark(h, "cg converged");
+    if (htrace)
+        std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration)\n",
+                     1e6 * (wall_seconds() - t_sol0), n_enq, 1e6 * t_enq, 1e6 * m_enq);
+    enq = poll.enq;
+    if (pr == CgPoll::kEnqueueError) return erc;
+    if (pr == CgPoll::kStreamError) {
+        h->err = std::string("PCG: ") + hipGetErrorString(hipStreamQuery(h->stream));
+        return INSFM_BA_EHIP;
+    }
+    if (pr == CgPoll::kStalled || pr == CgPoll::kGateStalled) {
+        h->err = std::string(pr == CgPoll::kGateStalled ? "PCG: the cross-rank exchange in front of the CG did not "
+                                                          "complete within "
+                                                        : "PCG: no progress from the device for ") +
+                 std::to_string(poll.stalled_s) + " s (iterations started " + std::to_string(pg[0]) + ", status " +
+                 std::to_string(pg[1]) + ", enqueued " + std::to_string(enq) +
+                 "); set INSFM_CG_STALL_S to change the limit";
+        return INSFM_BA_EHIP;
+    }
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    rec(h, 9);
+    if (h->timing) {
+        HIPCHK(hipStreamSynchronize(h->stream));
+        acc_time(h, 8, 9, 5);
+    }
+    h->cg_launches += enq;
+    st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
+    return 0;
+}
+
+// The block-Jacobi CG (precond 0, or the two-level path without host-mapped memory): launches in chunks, a status
+// copy and a stream sync per chunk.
+int run_bj_cg(insfm_ba* h, int* st) {
+    const int D = h->D, maxit = h->d.pcg_max_iter;
+    const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
+    int it = 0;
+    for (;;) {
+        // the count grows by a few iterations per LM step as the damping drops: launch past the last count so most
+        // solves need one host poll (a converged iteration costs ~1 us per launch: its kernels exit at the flag)
+        const int chunk = (it == 0) ? std::max(8, h->last_cg_iters + 6) : 8;
+        const int stop = std::min(it + chunk, maxit + 2);
+        const int first = it;
+        rec(h, 8);
+        const int rc = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            for (int k = it; k < stop; ++k) {
+                if (h->tlon) {
+                    launch_tl_iter<DV>(h, k, maxit, tol2);
+                    continue;
+                }
+                if (k > 0) k_cg_dots<<<1, 64, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
+                k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(k, h->C, maxit, tol2, h->nbr_ptr, h->nbr_j, h->Sn,
+                                                                h->Lf, h->cg);
+            }
+            return launch_err(h, "k_cg_iter");
+        });
+        if (rc) return rc;
+        rec(h, 9);
+        it = stop;
+        HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        acc_time(h, 8, 9, 5);
+        h->cg_launches += stop - first;
+        if (st[0] != 0 || it >= maxit + 2) break;
+    }
+    return 0;
 }
 
 // Build S/b for factor f, solve, back-substitute and form the trial parameters.  Returns PCG iterations (>= 0),
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
-    if (int rc0 = cgtail_join(h)) return rc0;
-    h->gate_used = false;
     // the point preparation of the linearization covers this solve when it runs at the prepared damping factor
     const bool prepared = h->prep_valid && h->prep_f == f && h->kind == 0;
     h->prep_valid = false;
@@ -2484,14 +2161,13 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                                                                      h->gpc);
     } else if (h->Pl > 0 && !prepared && (hmark(h, "point_prep"), true))
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
-                                                                       h->Vinv, h->y, h->flags, h->cg.status, pts_local,
-                                                                       h->schur_rc ? h->ptrec : nullptr);
+                                                                       h->Vinv, h->y, h->flags, h->cg.status);
     int iters = 0;
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
         rec(h, 6);
         int rc = 0;
-        if (h->xstream && !h->schur_rc && !h->schur_mf) {
+        if (h->xstream) {
             // chunked exchange: each row chunk's blocks of S are summed across ranks on the exchange stream while the
             // next chunk's Schur rows are built; b (filled by every row) after the last chunk
             const int K = (int)h->xw.size() - 1;
@@ -2502,7 +2178,6 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
                 if (b1 > b0 && (rc = allreduce_async(h, h->S + b0 * D * D, (b1 - b0) * D * D))) return rc;
             }
-            if ((rc = side_drain(h))) return rc;  // what remains of the previous solve's side chain
             if ((rc = allreduce_async(h, h->b, (int64_t)h->C * D))) return rc;
             HIPCHK(hipEventRecord(h->ev_xdone, h->xstream));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
@@ -2511,8 +2186,6 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
             if (rc) return rc;
             hmark(h, "schur");
-            if ((rc = side_drain(h))) return rc;  // what remains of the previous solve's side chain
-            hmark(h, "side drained");
             rec(h, 7);
             rc = allreduce(h, h->S, (int64_t)h->nnzb * D * D + (int64_t)h->C * D);
             if (rc) return rc;
@@ -2536,199 +2209,25 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         hmark(h, "factor/scale");
         if (h->tlon && (rc = run_tl_setup(h, cams))) return rc;
         hmark(h, "tl setup");
-        const int maxit = h->d.pcg_max_iter;
-        const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
-        int it = 0;
         int* st = reinterpret_cast<int*>(h->host_res + 8);
-        if (h->tlon && h->prog_host) {
-            // Two-level path: no stream sync inside the CG.  k_tl_pc's lead workgroup publishes its progress into
-            // host-mapped memory; more iterations are enqueued while the GPU still has two or more pending, and the
-            // loop ends when the status word turns non-zero.  The few iterations enqueued past convergence exit at the
-            // device status flag.
-            volatile int* pg = h->prog_host;
-            if (h->gate_seq != 0 && pg[4] != h->gate_seq) {
-                // the last solve's gate has not acknowledged yet (it exits once it has seen that solve's status, which
-                // is non-zero by now): wait for it before the status word is reset under it
-                const double tg = wall_seconds();
-                static const double gate_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
-                while (pg[4] != h->gate_seq) {
-                    if (wall_seconds() - tg > gate_s) {
-                        h->err = "PCG: the previous solve's CG gate did not finish";
-                        return INSFM_BA_EHIP;
-                    }
-#if defined(__x86_64__)
-                    __builtin_ia32_pause();
-#endif
-                }
-            }
-            pg[0] = pg[1] = pg[2] = pg[3] = 0;
-            std::atomic_thread_fence(std::memory_order_seq_cst);
-            // INSFM_HOST_TRACE=1: per solve, host microseconds spent enqueueing CG iterations / issuing side units, and
-            // the longest single call of each (stderr; diagnostics of host-bound launch gaps)
-            static const bool htrace = [] { const char* e = std::getenv("INSFM_HOST_TRACE"); return e && *e == '1'; }();
-            double t_enq = 0.0, t_side = 0.0, m_enq = 0.0, m_side = 0.0, t_sol0 = htrace ? wall_seconds() : 0.0;
-            int n_enq = 0, n_side = 0;
-            // CG stream (see insfm_ba::cgs): not with the instrumented replay (its phase events are on the main stream)
-            // or multi-rank runs (their CG waits for the exchange; cgs is created single-rank only)
-            const bool on_cgs = h->cgs != nullptr && !h->timing;
-            hipStream_t cg_stream = on_cgs ? h->cgs : h->stream;
-            auto enqueue = [&](int from, int to) -> int {
-                const double t0 = htrace ? wall_seconds() : 0.0;
-                hipStream_t main_stream = h->stream;
-                h->stream = cg_stream;  // (launch_tl_iter launches on h->stream)
-                const int r = with_D(D, [&](auto dc_) -> int {
-                    constexpr int DV = decltype(dc_)::value;
-                    for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
-                    return launch_err(h, "k_tl_pc/k_tl_pspmv");
-                });
-                h->stream = main_stream;
-                if (htrace) { const double dt = wall_seconds() - t0; t_enq += dt; m_enq = std::max(m_enq, dt / std::max(1, to - from)); n_enq += to - from; }
-                return r;
-            };
-            rec(h, 8);
-            // multi-rank: the CG's first launch waits for the exchange (the slowest peer); the stall deadline starts
-            // once everything queued in front of the CG has completed (ev_pre)
-            const bool gated = h->d.world_size > 1 || h->d.allreduce;
-            if (gated) HIPCHK(hipEventRecord(h->ev_pre, h->stream));
-            // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step);
-            // the loop below tops up one iteration at a time
-            int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
-            if (on_cgs) {  // the CG stream starts behind everything queued so far on the main stream
-                HIPCHK(hipEventRecord(h->ev_cg0, h->stream));
-                HIPCHK(hipStreamWaitEvent(h->cgs, h->ev_cg0, 0));
-            }
-            if ((rc = enqueue(0, enq))) return rc;
-            if (on_cgs) {
-                // the main stream: the gate, then the post-CG kernels (k_cg_finish here, the back-substitution and the
-                // cost after the poll loop) -- they run as soon as the status word turns non-zero
-                if (++h->gate_seq == 0) h->gate_seq = 1;
-                k_cg_gate<<<1, 64, 0, h->stream>>>(h->cg.prog, h->gate_dev, 6000000000LL, h->gate_seq);
-                rc = with_D(D, [&](auto dc_) -> int {
-                    constexpr int DV = decltype(dc_)::value;
-                    k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
-                                                                                                  h->dc);
-                    return launch_err(h, "k_cg_gate/k_cg_finish");
-                });
-                if (rc) { pg[1] = 3; return rc; }
-                h->gate_used = true;
-            }
-            CgPoll poll;
-            poll.enq = enq;
-            poll.extra_ahead = (h->side_slot >= 0 && side_sched() == 2) ? kSideAhead : 0;
-            static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
-            int erc = 0;
-            const int pr = cg_poll(
-                poll, maxit + 2, kCgAhead, stall_s, [&] { return (int)pg[1]; }, [&] { return (int)pg[0]; }, enqueue,
-                [&] {
-                    const hipError_t q = hipStreamQuery(cg_stream);
-                    if (q == hipSuccess) { std::atomic_thread_fence(std::memory_order_seq_cst); return 0; }
-                    return q == hipErrorNotReady ? 1 : -1;
-                },
-                wall_seconds,
-                [&] {
-                    // the host has nothing to enqueue: issue one unit of this solve's side chain, else relax.  While
-                    // side units remain, two more CG iterations are kept queued: a side launch can hold the host
-                    // for longer than two iterations take on the GPU
-                    if (h->side_slot >= 0 && side_sched() == 2) {
-                        const double t0 = htrace ? wall_seconds() : 0.0;
-                        const int r = side_issue(h);
-                        if (htrace) { const double dt = wall_seconds() - t0; t_side += dt; m_side = std::max(m_side, dt); ++n_side; }
-                        if (r && !erc) erc = r;
-                        poll.extra_ahead = h->side_slot >= 0 ? kSideAhead : 0;
-                        return;
-                    }
-#if defined(__x86_64__)
-                    __builtin_ia32_pause();
-#endif
-                },
-                [&] { return !gated || hipEventQuery(h->ev_pre) != hipErrorNotReady; }, &erc);
-            // whatever the CG left unissued stays pending: it is issued while the GPU runs the back-substitution
-            // and cost (finish_cost), the rest after the next solve's k_schur is enqueued (run_solve) -- issuing it
-            // here would hold back k_cg_finish by the host time of every remaining launch
-            const int left = h->side_slot >= 0 ? side_units(h) - h->side_next : 0;
-            hmark(h, "cg converged");
-            if (on_cgs) {
-                HIPCHK(hipEventRecord(h->ev_cgtail, h->cgs));
-                h->cgtail_pending = true;
-                // on any error the gate is released here (status 3: never accepted by k_publish)
-                if (pr != CgPoll::kDone || erc) { std::atomic_thread_fence(std::memory_order_seq_cst); pg[1] = 3; }
-            }
-            if (erc) return erc;
-            if (htrace)
-                std::fprintf(stderr, "[insfm host] solve %.1f us: %d iterations enqueued in %.1f us (max %.1f per iteration), "
-                             "%d side units in the poll loop in %.1f us (max %.1f), %d left for after the CG\n",
-                             1e6 * (wall_seconds() - t_sol0), n_enq, 1e6 * t_enq, 1e6 * m_enq, n_side, 1e6 * t_side,
-                             1e6 * m_side, left);
-            enq = poll.enq;
-            if (pr == CgPoll::kEnqueueError) return erc;
-            if (pr == CgPoll::kStreamError) {
-                h->err = std::string("PCG: ") + hipGetErrorString(hipStreamQuery(cg_stream));
-                return INSFM_BA_EHIP;
-            }
-            if (pr == CgPoll::kStalled) {
-                h->err = "PCG: no progress from the device for " + std::to_string(poll.stalled_s) +
-                         " s (iterations started " + std::to_string(pg[0]) + ", status " + std::to_string(pg[1]) +
-                         ", enqueued " + std::to_string(enq) + "); set INSFM_CG_STALL_S to change the limit";
-                return INSFM_BA_EHIP;
-            }
-            std::atomic_thread_fence(std::memory_order_seq_cst);
-            rec(h, 9);
-            if (h->timing) {
-                HIPCHK(hipStreamSynchronize(h->stream));
-                acc_time(h, 8, 9, 5);
-            }
-            h->cg_launches += enq;
-            st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
-            it = enq;
-        } else
-        for (;;) {
-            // the count grows by a few iterations per LM step as the damping drops: launch past the last count so most
-            // solves need one host poll (a converged iteration costs ~1 us per launch: its kernels exit at the flag)
-            const int chunk = (it == 0) ? std::max(8, h->last_cg_iters + 6) : 8;
-            const int stop = std::min(it + chunk, maxit + 2);
-            const int first = it;
-            rec(h, 8);
-            rc = with_D(D, [&](auto dc_) -> int {
-                constexpr int DV = decltype(dc_)::value;
-                for (int k = it; k < stop; ++k) {
-                    if (h->tlon) {
-                        launch_tl_iter<DV>(h, k, maxit, tol2);
-                        continue;
-                    }
-                    if (k > 0) k_cg_dots<<<1, 64, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
-                    k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(k, h->C, maxit, tol2, h->nbr_ptr, h->nbr_j, h->Sn,
-                                                                    h->Lf, h->cg, h->probe);
-                }
-                return launch_err(h, "k_cg_iter");
-            });
-            if (rc) return rc;
-            if ((rc = side_drain(h))) return rc;
-            rec(h, 9);
-            it = stop;
-            HIPCHK(hipMemcpyAsync(st, h->cg.status, sizeof(int) * 3, hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            acc_time(h, 8, 9, 5);
-            h->cg_launches += stop - first;
-            if (st[0] != 0 || it >= maxit + 2) break;
-        }
+        rc = (h->tlon && h->prog_host) ? run_tl_cg(h, st) : run_bj_cg(h, st);
+        if (rc) return rc;
         if (st[0] != 1) {
             h->err = std::string("PCG ") + (st[0] == 2 ? "breakdown" : "did not finish") + " at iteration " +
                      std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
-                     (h->tlon ? std::to_string(st[2]) : std::string("off")) + ", launches " + std::to_string(it) + ")";
+                     (h->tlon ? std::to_string(st[2]) : std::string("off")) + ")";
             return INSFM_BA_ESOLVER;
         }
         iters = st[1];
         h->coarse_used = h->tlon ? st[2] : 0;
         h->last_cg_iters = iters;
-        if (!h->gate_used) {  // (on the CG-stream path k_cg_finish is already queued behind the gate)
-            rc = with_D(D, [&](auto dc_) -> int {
-                constexpr int DV = decltype(dc_)::value;
-                k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
-                                                                                                h->dc);
-                return launch_err(h, "k_cg_finish");
-            });
-            if (rc) return rc;
-        }
+        rc = with_D(D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
+                                                                                            h->dc);
+            return launch_err(h, "k_cg_finish");
+        });
+        if (rc) return rc;
         dcp = h->dc;
         hmark(h, "cg_finish");
     }
@@ -2744,15 +2243,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         return iters;
     }
     if (int rc0 = lin_join(h)) return rc0;  // the camera update reads U / g_c (points-only solves skip the factor)
-    static const bool backsub_w_env = std::getenv("INSFM_BACKSUB_W") != nullptr;  // experiments: read W instead
-    const bool backsub_w = backsub_w_env && h->W != nullptr && !h->w_compact;  // (reads [3][D] records)
-    int rc = backsub_w ? with_D(D, [&](auto dc_) -> int {
-        constexpr int DV = decltype(dc_)::value;
-        if (h->Pl > 0)
-            k_backsub<DV><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->W, dcp, h->V, h->Vinv,
-                                                                  h->gp, pts_local, h->dp, h->pts_new, h->part_gp);
-        return launch_err(h, "k_backsub");
-    }) : with_model(h->model, [&](auto mc) -> int {
+    const int rc = with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         const int nrun = h->Pl > 0 ? h->n_lin : 0;  // point runs, then the camera-update blocks
         k_backsub_rc<M><<<nrun + h->n_gc, kLinThreads, 0, h->stream>>>(
@@ -2762,15 +2253,6 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     });
     if (rc) return rc;
     hmark(h, "backsub");
-    if (backsub_w) {
-        rc = with_model(h->model, [&](auto mc) -> int {
-            constexpr int M = decltype(mc)::value;
-            k_update_cams<M><<<h->n_gc, kLinThreads, 0, h->stream>>>(h->C, cams, dcp, h->U, h->gc, h->d.rank == 0,
-                                                                     h->cams_new, h->part_gc);
-            return launch_err(h, "k_update_cams");
-        });
-        if (rc) return rc;
-    }
     return iters;
 }
 
@@ -2780,14 +2262,13 @@ struct TrialAccept {
     int can_reject;  // rejects < max_rejects
 };
 
-// The cost result to the host: k_publish into host-mapped memory and a spin on its sequence word (deferred side
-// units are issued while the GPU is still busy); without the mapped block, a copy and a stream synchronization.
+// The cost result to the host: k_publish into host-mapped memory and a spin on its sequence word; without the mapped
+// block, a copy and a stream synchronization.
 // Sets h->trial_copied when k_publish also copied an accepted trial (h->pub_host[5] holds its decision).
 int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     h->trial_copied = false;
     if (!h->pub_host) {
         HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
-        if (int rc = side_issue_while_busy(h)) return rc;
         HIPCHK(hipStreamSynchronize(h->stream));
         return 0;
     }
@@ -2797,12 +2278,9 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     const long long ncam = copy ? (long long)h->C * h->stride : 0, npts = copy ? (long long)h->Pl * 3 : 0;
     const int grid = copy ? std::max(1, std::min(1024, cdiv(std::max(ncam, npts / 2 + 1), kThreads))) : 1;
     k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->pub_dev, seq, ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
-                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts,
-                                               (ta && h->gate_used) ? h->gate_dev : nullptr);
+                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
     if (int rc = launch_err(h, "k_publish")) return rc;
     hmark(h, "publish");
-    if (int rc = side_issue_while_busy(h)) return rc;
-    hmark(h, "side while busy");
     const unsigned* w = reinterpret_cast<const unsigned*>(h->pub_host + 8);
     // bounded like the CG poll: a device that neither publishes nor reports an error ends the step with EHIP
     static const double stall_s = 6.0 * cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
@@ -2966,7 +2444,7 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         st->coarse_used = h->coarse_used;
     }
     h->timing = false;
-    if (host_trace_level() >= 2 && !h->hmarks.empty()) {
+    if (host_trace2() && !h->hmarks.empty()) {
         hmark(h, "step end");
         std::string line = "[insfm host2]";
         for (auto& m : h->hmarks) line += " " + std::string(m.first) + "=" + std::to_string((int)(1e6 * (m.second - h->hmarks[0].second)));
@@ -3007,7 +2485,7 @@ void insfm_ba_destroy(insfm_ba* h) {
     if (!h) return;
     if (h->side) (void)side_flush(h);
     // every stream that may still use the buffers, before they are parked for the next handle
-    for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux, h->cgs})
+    for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux})
         if (st) (void)hipStreamSynchronize(st);
     if (!h->stream) (void)hipDeviceSynchronize();
     dfree_all(h);
@@ -3028,12 +2506,6 @@ void insfm_ba_destroy(insfm_ba* h) {
         (void)hipStreamSynchronize(h->aux);
         (void)hipStreamDestroy(h->aux);
     }
-    if (h->cgs) {
-        (void)hipStreamSynchronize(h->cgs);
-        (void)hipStreamDestroy(h->cgs);
-    }
-    if (h->ev_cg0) (void)hipEventDestroy(h->ev_cg0);
-    if (h->ev_cgtail) (void)hipEventDestroy(h->ev_cgtail);
     if (h->ev_lin0) (void)hipEventDestroy(h->ev_lin0);
     if (h->ev_lc) (void)hipEventDestroy(h->ev_lc);
     if (h->ev_x) (void)hipEventDestroy(h->ev_x);
@@ -3047,6 +2519,8 @@ void insfm_ba_destroy(insfm_ba* h) {
 }
 
 int64_t insfm_ba_nnzb(const insfm_ba* h) { return h ? h->nnzb : -1; }
+
+int64_t insfm_ba_release_cache(void) { return (int64_t)release_cache(); }
 
 }  // extern "C"
 
@@ -3086,6 +2560,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (desc->world_size < 1 || desc->rank < 0 || desc->rank >= desc->world_size) return fail(INSFM_BA_EINVAL, "bad rank");
     if (desc->world_size > 1 && !desc->allreduce) return fail(INSFM_BA_EINVAL, "world_size > 1 needs allreduce");
     if (h->C > 30000) return fail(INSFM_BA_EINVAL, "n_cams > 30000 not supported (LDS slot table)");
+    // desc.schur_variant: only 0 (the W-reading k_schur) remains.  Variants 1 / 2 (camera-point blocks re-derived per
+    // pair, LDS-atomic rows / MFMA register accumulation) and 3 (compact W records) were built, parity-tested and
+    // measured slower or even in rounds 2-3; they live in the git history.
+    if (desc->schur_variant != 0) return fail(INSFM_BA_EINVAL, "schur_variant must be 0");
     const int C = h->C, P = h->P, N = h->N, D = h->D;
     // every pass over the observations below runs on this pool (create_host.h); joined when create returns
     HostPool pool(host_pool_size());
@@ -3109,8 +2587,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->p1 = desc->shard_point_end < 0 ? P : std::min(P, desc->shard_point_end);
     if (h->p1 < h->p0) return fail(INSFM_BA_EINVAL, "bad shard range");
     h->Pl = h->p1 - h->p0;
-    // INSFM_CREATE_TRACE=1: host milliseconds of create's phases (stderr)
-    static const bool ctrace = [] { const char* e = std::getenv("INSFM_CREATE_TRACE"); return e && *e == '1'; }();
+    // INSFM_DIAG=create: host milliseconds of create's phases (stderr)
+    static const bool ctrace = diag("create");
     const double ct0 = wall_seconds();
     auto tick = [&](const char* what) {
         if (ctrace) std::fprintf(stderr, "[insfm create] %-28s %8.1f ms\n", what, 1e3 * (wall_seconds() - ct0));
@@ -3154,51 +2632,31 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     });
     const int kmax = *std::max_element(kmax_t.begin(), kmax_t.end());
     tick("local track order");
-    // camera-major lists.  Default (INSFM_SCHUR_ORDER=1): within a camera the observations in point order, cut into
-    // chunks of four k_schur rounds (4 x 64 own observations for D = 8; INSFM_SCHUR_CHUNK rounds), each chunk sorted
-    // by descending upper-partner count (stable; balances the Schur groups of a wave: 2.8 % more wave partner slots
-    // than the global count sort, 10.8 % with one-round chunks).  Every k_schur row then walks the points in the same
-    // global order at about the same pace, so rows running together read a shared track's partner W records close
-    // together in time.  Config 3, k_schur: 491 us (count sort) -> 467 us (chunks of 4 rounds; 1 / 2 / 8 / 16 rounds:
-    // 541 / 499 / 471 / 483 us -- the wave partner slots cost more than the locality buys below 4).
-    // INSFM_SCHUR_ORDER=0: descending partner count over the whole camera (stable counting sorts: count, camera).
+    // camera-major lists: within a camera the observations in point order, cut into chunks of kSchurChunk k_schur
+    // rounds (4 x 64 own observations for D = 8), each chunk sorted by descending upper-partner count (stable;
+    // balances the Schur groups of a wave: 2.8 % more wave partner slots than a global count sort, 10.8 % with
+    // one-round chunks).  Every k_schur row then walks the points in the same global order at about the same pace, so
+    // rows running together read a shared track's partner W records close together in time.  Config 3, k_schur:
+    // 491 us (count sort over the whole camera) -> 467 us (chunks of 4 rounds; 1 / 2 / 8 / 16 rounds: 541 / 499 / 471 /
+    // 483 us -- the wave partner slots cost more than the locality buys below 4).  Measured and dropped in round 3
+    // (DESIGN.md section 8): the chunk's slices dealt to the waves in snake order (480-484 vs 473-475 us) and runs of
+    // consecutive rows per XCD (L2 hit 4 -> 54 %, yet 469-515 us).
     std::vector<int> cptr;
     nivec<int> cobs;
-    static const int schur_order = [] { const char* e = std::getenv("INSFM_SCHUR_ORDER"); return e ? std::atoi(e) : 1; }();
-    if (schur_order == 1) {
+    {
         // observations are track-major (point order), so a stable counting sort by camera leaves each list in point
         // order; then a stable sort of each chunk by descending partner count
         pcount_sort(pool, Nl, C, nullptr, [&](int o) { return lcam[o]; }, cobs, cptr);
-        static const int rounds = [] { const char* e = std::getenv("INSFM_SCHUR_CHUNK"); const int v = e ? std::atoi(e) : 4; return v > 0 ? v : 4; }();
-        // INSFM_SCHUR_SNAKE=1: after the sort of a chunk the slices of round r go to the waves in snake order (r even:
-        // wave w <- sorted slice r W + w; r odd: r W + W - 1 - w), so no wave always gets the heaviest slice of every
-        // round (k_schur's waves run their slices w * NG + r * R independently; the row ends with its slowest wave).
-        // A model of config 3 gives critical wave / ideal work 1.26 -> 1.06, but k_schur measured 473-475 us without
-        // it and 480-484 with it (profiles/r3_v10/snake_probe.log), so it is off by default.
-        static const bool snake = [] { const char* e = std::getenv("INSFM_SCHUR_SNAKE"); return e && *e == '1'; }();
-        const int NG = 64 / D, R = kSchurWaves * NG, K = rounds * R;
+        const int NG = 64 / D, K = kSchurChunk * kSchurWaves * NG;
         pool.ranges(C, [&](int, long long i0, long long i1) {
-            std::vector<int> tmp(K);
             for (long long i = i0; i < i1; ++i)
                 for (int a = cptr[i]; a < cptr[i + 1]; a += K) {
-                    const int e = std::min(a + K, cptr[i + 1]), m = e - a;
-                    int* c = cobs.data() + a;
-                    std::stable_sort(c, c + m, [&](int x, int y) { return key[x] > key[y]; });
-                    if (m < K || !snake) continue;  // (a row's short last chunk stays in sorted order)
-                    std::copy(c, c + m, tmp.begin());
-                    for (int r = 0; r < rounds; ++r)
-                        for (int w = 0; w < kSchurWaves; ++w) {
-                            const int src = r * kSchurWaves + ((r & 1) ? kSchurWaves - 1 - w : w);
-                            std::copy(tmp.begin() + src * NG, tmp.begin() + src * NG + NG, c + (r * kSchurWaves + w) * NG);
-                        }
+                    const int e = std::min(a + K, cptr[i + 1]);
+                    std::stable_sort(cobs.data() + a, cobs.data() + e, [&](int x, int y) { return key[x] > key[y]; });
                 }
         });
-    } else {
-        nivec<int> byk;
-        std::vector<int> kptr;
-        pcount_sort(pool, Nl, kmax + 1, nullptr, [&](int o) { return kmax - key[o]; }, byk, kptr);
-        pcount_sort(pool, Nl, C, byk.data(), [&](int o) { return lcam[o]; }, cobs, cptr);
     }
+    (void)kmax;
     tick("camera-major lists");
     // the per-observation arrays go to the device now: the block pattern below is derived there (single rank)
     int rc;
@@ -3260,11 +2718,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     // camera every other camera sharing a track, weighted by the number of (obs of i, obs of j) pairs sharing one:
     // the two-level clustering's weights).  Single rank: on the device (k_pattern, two passes), the lower half of the
     // graph transposed from the upper on the host.  Multi-rank (every rank needs the global pattern, and holds only its
-    // shard's observations on the device) or INSFM_PATTERN_HOST=1: one host pass over the global camera-major list.
+    // shard's observations on the device) or INSFM_DIAG=pattern_host: one host pass over the global camera-major list.
     std::vector<int> gcptr;
     CovisGraph g;
     std::vector<int> rptr(C + 1, 0), cols;
-    static const bool pattern_host = [] { const char* e = std::getenv("INSFM_PATTERN_HOST"); return e && *e == '1'; }();
+    static const bool pattern_host = diag("pattern_host");
     const bool gpu_pattern = !pattern_host && Pl == P && o0 == 0 && Nl == N && C <= kPatternMaxC && Nl > 0;
     std::vector<int> upw;  // (device pattern) the pair count of every upper block, indexed like cols
     if (gpu_pattern) {
@@ -3456,25 +2914,15 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     h->max_chunk = maxc;
     if (kind == 0 && desc->allreduce_async && (desc->world_size > 1 || desc->allreduce) && desc->exchange_chunks > 1 &&
         desc->optimize_poses) {
-        // chunk boundaries at rows where the block counts follow a geometric series (chunk c ~ ratio^c of the
-        // blocks, INSFM_XCHUNK_RATIO in (0, 4], default 1 = equal chunks; DESIGN.md section 5 for why decreasing
-        // chunks do not pay: the all-reduces run back to back on one stream), and the first work item of each
-        // boundary row
+        // chunk boundaries at rows splitting the blocks into about equal counts (geometric series of chunk sizes
+        // were measured in round 3 and do not pay: the all-reduces run back to back on one stream; DESIGN.md section
+        // 5), and the first work item of each boundary row
         const int K = std::min(desc->exchange_chunks, C);
-        static const double ratio = [] {
-            const char* e = std::getenv("INSFM_XCHUNK_RATIO");
-            const double v = e ? std::atof(e) : 1.0;
-            return (v > 0.0 && v <= 4.0) ? v : 1.0;
-        }();
-        double tot = 0.0;
-        for (int c = 0; c < K; ++c) tot += std::pow(ratio, c);
-        double cum = 0.0;
         h->rptr_host = rptr;
         h->xr.assign(1, 0);
         h->xw.assign(1, 0);
         for (int c = 1; c < K; ++c) {
-            cum += std::pow(ratio, c - 1);
-            const int64_t target = (int64_t)((double)rptr[C] * cum / tot);
+            const int64_t target = (int64_t)rptr[C] * c / K;
             const int r = (int)(std::upper_bound(rptr.begin(), rptr.end(), (int)target) - rptr.begin()) - 1;
             if (r <= h->xr.back() || r >= C) continue;
             int w = h->xw.back();
@@ -3490,144 +2938,13 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("exchange stream: ") + hipGetErrorString(e));
     }
     // Work order: natural (row order), so the 256 rows running at once are 256 consecutive cameras that share tracks
-    // in the Infinity Cache.  INSFM_SCHUR_XCD=B (with the point-order chunks) deals runs of B consecutive items to one
-    // XCD instead (workgroups go round-robin over the 8 XCDs): measured on config 3 (tools/order_probe.sh,
-    // profiles/r3_v10/): B = 1 / 2 / 4 / 16 / 125 -> k_schur 467 / 469 / 471 / 491 / 515 us -- the whole-XCD runs lift the
-    // L2 hit rate from 4 to 54 % and cut the average L1->L2 read latency 562 -> 402 cycles, yet the kernel is slower:
-    // it is not bound by that latency.
-    {
-        static const int xcd = [] { const char* e = std::getenv("INSFM_SCHUR_XCD"); return e ? std::atoi(e) : 0; }();
-        const int nw = (int)work.size();
-        if (xcd >= 1 && schur_order == 1 && nw >= 16 && h->xw.empty()) {  // (the chunked exchange needs row order)
-            // natural item k goes to XCD (k / xcd) % 8: runs of `xcd` consecutive items per XCD; position 8 j + x
-            // takes the j-th item of XCD x (leftovers of unequal lists at the end)
-            std::vector<std::vector<int>> lx(8);
-            for (int k = 0; k < nw; ++k) lx[(k / xcd) % 8].push_back(k);
-            std::vector<int4> w2;
-            w2.reserve(nw);
-            size_t mn = lx[0].size();
-            for (int x = 1; x < 8; ++x) mn = std::min(mn, lx[x].size());
-            for (size_t j = 0; j < mn; ++j)
-                for (int x = 0; x < 8; ++x) w2.push_back(work[lx[x][j]]);
-            for (int x = 0; x < 8; ++x)
-                for (size_t j = mn; j < lx[x].size(); ++j) w2.push_back(work[lx[x][j]]);
-            work.swap(w2);
-        }
-    }
+    // in the Infinity Cache.
     h->schur_lds = sizeof(double) * ((size_t)maxc * schur_bs(D) + D + 12) + wsh_lds + sizeof(int) * (size_t)C;
     h->schur_lds = (h->schur_lds + 15) & ~(size_t)15;
-    // Schur variant (INSFM_SCHUR): "w" (default) reads the stored W records (k_schur); "rc" re-derives the camera-point
-    // blocks per pair and adds them with LDS atomics (ba_schur_rc.h); "mf" re-derives them and accumulates in MFMA
-    // registers (ba_schur_mf.h, D <= 8).  Measured on config 3: w 0.51 ms, rc 0.68-0.70 ms
-    // (LDS-atomic bound), mf 1.2-1.6 ms (latency / barrier bound); rc / mf save the 384-MB W write of k_lin_points.
-    static const char* schur_env = std::getenv("INSFM_SCHUR");
-    const std::string schur_kind = schur_env ? std::string(schur_env)
-                                             : (desc->schur_variant == 1 ? "rc"
-                                                : (desc->schur_variant == 2 ? "mf" : (desc->schur_variant == 3 ? "cw" : "w")));
-    h->schur_rc = kind == 0 && !desc->deterministic && desc->optimize_poses && (schur_kind == "rc" || schur_kind == "mf");
-    std::vector<int4> work_rc;
-    if (h->schur_rc) {
-        // chunks sized for its LDS layout (block + camera-table entry per slot)
-        int rc_cap = 0;
-        with_model(h->model, [&](auto mc) -> int {
-            constexpr int M = decltype(mc)::value;
-            const size_t fixed = schur_rc_lds_bytes<M>(0, C);
-            const size_t per = sizeof(double) * (schur_rc_bs(D) + kCamTab<M>);
-            rc_cap = fixed + per > (size_t)kLdsBudget ? 0 : (int)((kLdsBudget - fixed) / per);
-            return 0;
-        });
-        if (rc_cap < 1) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
-        int maxrc = 1;
-        for (int i = 0; i < C; ++i) {
-            for (int kb = rptr[i]; kb < rptr[i + 1]; kb += rc_cap) {
-                const int ke = std::min(kb + rc_cap, rptr[i + 1]);
-                work_rc.push_back(make_int4(i, kb, ke, 0));
-                maxrc = std::max(maxrc, ke - kb);
-            }
-        }
-        h->nwork_rc = (int)work_rc.size();
-        with_model(h->model, [&](auto mc) -> int {
-            h->schur_rc_lds = schur_rc_lds_bytes<decltype(mc)::value>(maxrc, C);
-            return 0;
-        });
-    }
-    // MFMA-accumulating variant for D <= 8 (ba_schur_mf.h): rows in chunks of <= 64 blocks; each chunk's own
-    // observations in batches of 64 taken round-robin from the camera's list (partner-count-sorted chunks), so every batch
-    // carries about the average number of pairs; every pair's staging position groups the batch's pairs by
-    // destination block (own order, then partner order, inside a block).
-    const bool no_mf = schur_kind != "mf";
-    std::vector<MfWork> mfw;
-    std::vector<int4> mfsd;
-    std::vector<unsigned short> mfpp;
-    std::vector<int> mfbo;
-    if (h->schur_rc && D <= 8 && !no_mf) {
-        std::vector<int4> sdesc(std::max(Nl, 1));  // (the device copy is derived by k_derive_cm)
-        for (int e = 0; e < Nl; ++e) {
-            const int o = cobs[e], p = lptl[o];
-            sdesc[e] = make_int4(o, p, lust[o], lptr[p + 1]);
-        }
-        std::vector<int> slotmap(C, -1), cnt(kMfSlots + 1), run(kMfSlots + 1);
-        int pcap = 0;
-        bool ok = true;
-        for (int i = 0; i < C && ok; ++i) {
-            const int n_own = cptr[i + 1] - cptr[i];
-            for (int kb = rptr[i]; kb < rptr[i + 1]; kb += kMfSlots) {
-                const int ke = std::min(kb + kMfSlots, rptr[i + 1]);
-                for (int e = kb; e < ke; ++e) slotmap[cols[e]] = e - kb;
-                const int nbat = (n_own + kMfOwn - 1) / kMfOwn;
-                MfWork w{i, kb, ke, nbat, (int)(mfbo.size() / kMfBR), 0, 0, 0};
-                for (int bt = 0; bt < nbat; ++bt) {
-                    std::fill(cnt.begin(), cnt.end(), 0);
-                    std::vector<int> members;
-                    for (int k = bt; k < n_own; k += nbat) members.push_back(cptr[i] + k);
-                    if ((int)members.size() > kMfOwn) { ok = false; break; }
-                    for (int e : members) {
-                        const int4 d = sdesc[e];
-                        for (int q = d.z; q < d.w; ++q) {
-                            const int sl = slotmap[lcam[q]];
-                            if (sl >= 0) cnt[sl]++;
-                        }
-                    }
-                    std::vector<int> bo(kMfSlots + 1, 0);
-                    for (int sl = 0; sl < kMfSlots; ++sl) bo[sl + 1] = bo[sl] + cnt[sl];
-                    pcap = std::max(pcap, bo[kMfSlots]);
-                    for (int sl = 0; sl <= kMfSlots; ++sl) mfbo.push_back(bo[sl]);
-                    mfbo.push_back((int)mfsd.size());
-                    mfbo.push_back((int)members.size());
-                    std::copy(bo.begin(), bo.end(), run.begin());
-                    for (int e : members) {
-                        const int4 d = sdesc[e];
-                        const int n = d.w - d.z, ofs = d.x - d.z;
-                        if (n >= 0x10000 || ofs >= 0x10000) { ok = false; break; }
-                        mfsd.push_back(make_int4(d.y, d.z, n | (ofs << 16), (int)mfpp.size()));
-                        for (int q = d.z; q < d.w; ++q) {
-                            const int sl = slotmap[lcam[q]];
-                            mfpp.push_back(sl >= 0 ? (unsigned short)run[sl]++ : (unsigned short)0xffff);
-                        }
-                    }
-                    if (bo[kMfSlots] >= 0xffff) ok = false;
-                }
-                for (int e = kb; e < ke; ++e) slotmap[cols[e]] = -1;
-                mfw.push_back(w);
-            }
-        }
-        size_t lds = 0;
-        with_model(h->model, [&](auto mc) -> int {
-            lds = schur_mf_lds_bytes<decltype(mc)::value>(std::max(pcap, 16), C);
-            return 0;
-        });
-        if (ok && lds <= (size_t)kLdsBudget) {
-            h->schur_mf = true;
-            h->mf_pcap = std::max(pcap, 16);  // >= 16: the slot-0 quarters are summed in the staging area
-            h->schur_mf_lds = lds;
-            h->n_mf_work = (int)mfw.size();
-        }
-    }
-    // Camera linearization beside k_lin_points / k_schur (u_late), single rank on the W-reading Schur build.
-    // INSFM_U_LATE=0 keeps it on the main stream (U added inside k_schur).
+    // Camera linearization beside k_lin_points / k_schur (u_late), single rank (multi-rank, U / g_c are all-reduced
+    // before the Schur build adds them).
     {
-        static const bool env_on = [] { const char* e = std::getenv("INSFM_U_LATE"); return !e || std::atoi(e) != 0; }();
-        if (env_on && kind == 0 && desc->world_size <= 1 && !desc->allreduce && !h->schur_rc && !h->schur_mf) {
+        if (kind == 0 && desc->world_size <= 1 && !desc->allreduce) {
             hipError_t e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lin0, hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lc, hipEventDisableTiming);
@@ -3660,25 +2977,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     }
     if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
     auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
-    if (h->schur_mf) {
-        if (mfsd.empty()) mfsd.push_back(make_int4(0, 0, 0, 0));
-        if (mfbo.empty()) mfbo.assign(kMfBR, 0);
-        if ((rc = upload(h, &h->mf_work, mfw.data(), mfw.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->mf_sd, mfsd.data(), mfsd.size()))) return fail(rc, "");
-        if (mfpp.empty()) mfpp.push_back(0xffff);
-        if ((rc = upload(h, &h->mf_ppos, mfpp.data(), mfpp.size()))) return fail(rc, "");
-        if ((rc = upload(h, &h->mf_boff, mfbo.data(), mfbo.size()))) return fail(rc, "");
-    }
-    if (h->schur_rc) {  // W is never formed
-        if ((rc = upload(h, &h->work_rc, work_rc.data(), work_rc.size()))) return fail(rc, "");
-        if ((rc = dalloc(h, (void**)&h->obrec, sizeof(double2) * (size_t)std::max(Nl, 1)))) return fail(rc, "");
-        if ((rc = dd(&h->ptrec, (size_t)std::max(Pl, 1) * 12))) return fail(rc, "");
-    } else {
-        // BA: [3][D] records, or the compact ones for schur_variant 3 ("cw")
-        h->w_compact = kind == 0 && D >= 7 && schur_kind == "cw";
-        // (+2: load_crec's 16-B pieces of the last record may reach one value past it)
-        if ((rc = dd(&h->W, (size_t)Nl * (h->w_compact ? wrec_len(D) : D * 3) + 2))) return fail(rc, "");
-    }
+    // W: [3][D] records per observation (global positioning: its 32-B {u, beta^2} records fit in the same buffer)
+    if ((rc = dd(&h->W, (size_t)Nl * D * 3 + 2))) return fail(rc, "");
     if ((rc = dd(&h->V, (size_t)Pl * 6))) return fail(rc, "");
     if ((rc = dd(&h->gp, (size_t)Pl * 3))) return fail(rc, "");
     if ((rc = dd(&h->Vinv, (size_t)Pl * 6))) return fail(rc, "");
@@ -3757,28 +3057,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("init: ") + hipGetErrorString(e));
     }
     // the Schur kernels may need more than the default dynamic-LDS limit
-    if (h->schur_rc)
-        with_model(h->model, [&](auto mc) -> int {
-            constexpr int M = decltype(mc)::value;
-            (void)hipFuncSetAttribute((const void*)k_schur_rc<M, SCHUR_RC_WAVES>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h->schur_rc_lds);
-            if constexpr (kD<M> <= 8)
-                if (h->schur_mf)
-                    (void)hipFuncSetAttribute((const void*)k_schur_mf<M>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)h->schur_mf_lds);
-            return 0;
-        });
     with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)h->schur_lds);
-        if constexpr (DV >= 7) {
-            (void)hipFuncSetAttribute((const void*)k_schur<DV, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h->schur_lds);
-            (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves, false, true>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
-        }
         if constexpr (DV == 3) {
             (void)hipFuncSetAttribute((const void*)k_schur<3, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->schur_lds);
@@ -3791,22 +3074,31 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     });
     tick("uploads + allocations");
     if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
+    // ---- two-level preconditioner: clusters ----
+    // Target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
+    // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
+    // While the coarse dimension exceeds kCoarseMax the target grows in proportion to the excess (at least by one),
+    // rounded up to even (aggregates below K / 2 are dissolved: an odd K would keep singletons):
+    // K' = max(K + 1, ceil(K nc MC / kCoarseMax)) rounded up to even, at most C -- the oracle's ora_cluster_cameras.
+    // With K = C the clusters are the co-visibility components: if even those do not fit (more components than
+    // kCoarseMax / MC), the solver runs the block-Jacobi PCG (precond 0) instead.
+    const int MC = D + 1;
+    int nc = 0;
+    bool coarse_ok = false;
+    std::vector<int>& lab = h->clab_host;
     if (desc->precond == 1 && h->d.optimize_poses) {
-        // ---- two-level preconditioner: clusters, source lists of E, buffers ----
-        const int MC = D + 1;
-        // target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
-        // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
-        // While the coarse dimension exceeds kCoarseMax the target grows in proportion to the excess (at least by
-        // one), rounded up to even (aggregates below K / 2 are dissolved: an odd K would keep singletons):
-        // K' = max(K + 1, ceil(K nc MC / kCoarseMax)) rounded up to even -- the oracle's ora_cluster_cameras
-        int K = desc->cluster_size > 0 ? desc->cluster_size : 14;
-        std::vector<int>& lab = h->clab_host;
-        int nc = aggregate(g, C, K, lab);
-        while (nc * MC > kCoarseMax) {
-            K = std::max(K + 1, (int)(((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));
+        int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 14, C);
+        nc = aggregate(g, C, K, lab);
+        while (nc * MC > kCoarseMax && K < C) {
+            K = (int)std::min<long long>(C, std::max<long long>(K + 1, ((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));
             K += K & 1;
+            K = std::min(K, C);
             nc = aggregate(g, C, K, lab);
         }
+        coarse_ok = nc * MC <= kCoarseMax;
+    }
+    if (coarse_ok) {
+        // ---- two-level preconditioner: source lists of E, buffers ----
         const int m = nc * MC;
         tick("covisibility + clusters");
         std::vector<int> clp(nc + 1, 0), clc(C), alone(C);
@@ -3918,27 +3210,13 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         if ((rc = dd(&tl.Rc, (size_t)m))) return fail(rc, "");
         if ((rc = dd(&tl.gd, 3 * (size_t)C))) return fail(rc, "");
         {
-            // cluster reduction of the CG's row partials by the last-arriving row of each cluster in k_tl_pspmv
-            // (INSFM_PC_CLUSTER=1; off by default): measured on config 3, k_tl_pc 9.7 -> 7.0 us but k_tl_pspmv
-            // 13.5 -> 18.7 us -- every workgroup waits for its write-through stores and for its counter add to
-            // return, and all 1000 rows run in one round, so the launch grows by that round trip
-            static const bool pc_cluster = [] { const char* e = std::getenv("INSFM_PC_CLUSTER"); return e && std::atoi(e) != 0; }();
             if ((rc = upload(h, &ip, lab.data(), lab.size()))) return fail(rc, "");
             tl.clab = ip;
-            tl.ccnt = nullptr;
-            if (pc_cluster) {
-                if ((rc = dalloc(h, (void**)&tl.ccnt, sizeof(int) * (size_t)nc))) return fail(rc, "");
-                if (hipMemsetAsync(tl.ccnt, 0, sizeof(int) * (size_t)nc, h->stream) != hipSuccess)
-                    return fail(INSFM_BA_EHIP, "ccnt clear");
-            }
-            if ((rc = dd(&tl.Rcl, (size_t)m))) return fail(rc, "");
-            if ((rc = dd(&tl.gcl, 3 * (size_t)nc))) return fail(rc, "");
-            // atomic cluster sums of the CG partials (INSFM_PC_ATOMIC=0 disables): single GPU, non-deterministic mode
-            // only -- the replicated multi-rank CG needs bitwise-equal inputs on every rank
-            static const bool pc_atomic = [] { const char* e = std::getenv("INSFM_PC_ATOMIC"); return !e || std::atoi(e) != 0; }();
+            // atomic cluster sums of the CG partials: single GPU, non-deterministic mode only -- the replicated
+            // multi-rank CG needs bitwise-equal inputs on every rank (config 3: CG iteration 23.9 -> 22.3 us, round 3)
             tl.Racc = nullptr;
             tl.Gacc = nullptr;
-            if (pc_atomic && !pc_cluster && !desc->deterministic && desc->world_size <= 1 && !desc->allreduce) {
+            if (!desc->deterministic && desc->world_size <= 1 && !desc->allreduce) {
                 if ((rc = dd(&tl.Racc, 2 * (size_t)m))) return fail(rc, "");
                 if ((rc = dd(&tl.Gacc, 2 * 3 * (size_t)nc))) return fail(rc, "");
                 if (hipMemsetAsync(tl.Racc, 0, sizeof(double) * 2 * (size_t)m, h->stream) != hipSuccess ||
@@ -3969,13 +3247,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         tl.Einv = h->Einvbuf[0];
         tl.ok = h->okbuf;
         hipError_t e = hipMemsetAsync(h->okbuf, 0, sizeof(int) * 2, h->stream);
-        // The side stream (E build + factorization, off the critical path) runs at the lowest priority, so its
-        // workgroups do not take CUs from the CG iterations that overlap it.  INSFM_SIDE_PRIO overrides (experiments).
+        // The side stream (E build + factorization, off the critical path) at the lowest priority (ROCm exposes only
+        // normal and high: no measured effect either way, round 1)
         int prio_lo = 0, prio_hi = 0;
         if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-        const char* sp = std::getenv("INSFM_SIDE_PRIO");
-        const int side_prio = sp ? std::atoi(sp) : prio_lo;
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, side_prio);
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_built, hipEventDisableTiming);
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);
@@ -4004,21 +3280,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             if (hipHostGetDevicePointer(&dp, pm, 0) == hipSuccess) h->cg.prog = static_cast<int*>(dp);
             else { (void)hipHostFree(pm); h->prog_host = nullptr; }
         }
-        // opt-in (INSFM_CG_STREAM=1): measured slower on config 3 -- 659-672 vs 709-726 LM it/s on one box
-        // (profiles/r3_v11/cg_stream_ab.log); the iterations behind a cross-queue event and the gated tail cost more
-        // than the host round trip and the launches past convergence they remove
-        static const bool cg_stream = [] { const char* e = std::getenv("INSFM_CG_STREAM"); return e && *e == '1'; }();
-        if (cg_stream && h->prog_host && kind == 0 && desc->world_size <= 1 && !desc->allreduce) {
-            hipError_t e2 = hipStreamCreateWithFlags(&h->cgs, hipStreamNonBlocking);
-            if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&h->ev_cg0, hipEventDisableTiming);
-            if (e2 == hipSuccess) e2 = hipEventCreateWithFlags(&h->ev_cgtail, hipEventDisableTiming);
-            if (e2 != hipSuccess) return fail(INSFM_BA_EHIP, std::string("CG stream: ") + hipGetErrorString(e2));
-            if ((rc = dalloc(h, (void**)&h->gate_dev, sizeof(int)))) return fail(rc, "");
-        }
     }
     tick("two-level setup (end)");
-    if (const char* pe = std::getenv("INSFM_CG_PROBE")) h->probe = std::atoi(pe);
-    if (const char* ts = std::getenv("INSFM_TL_SYNC")) h->tl_sync = std::atoi(ts) != 0;
     h->damping = 1.0 / desc->tr_radius;
     h->down = desc->tr_down;
     *out = h;
@@ -4060,6 +3323,12 @@ int insfm_ba_reset(insfm_ba* h) {
     h->damping = 1.0 / h->d.tr_radius;
     h->down = h->d.tr_down;
     h->have_loss = false;
+    // a fresh LM: the first solve after the reset factorizes its own coarse matrix (no lagged E^-1 of an earlier solve
+    // survives) and the CG's first batch is sized as for a new handle
+    if (int rc = side_flush(h)) return rc;
+    h->tl_solves = 0;
+    h->tl_fresh = false;
+    h->last_cg_iters = 16;
     return INSFM_BA_OK;
 }
 
@@ -4100,7 +3369,7 @@ int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts)
     int rc = run_linearize(h, h->cams_cur, h->pts_cur);
     if (!rc) rc = lin_join(h);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
+    HIPCHK(hipStreamSynchronize(h->stream));
     return 0;
 }
 
@@ -4109,7 +3378,7 @@ int insfm_ba_debug_solve(insfm_ba* h, double f) {
     h->keep_S = 1;
     // solves around the parameters last passed to insfm_ba_debug_linearize
     int it = run_solve(h, f, h->cams_cur, h->pts_cur);
-    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
+    HIPCHK(hipStreamSynchronize(h->stream));
     return it;
 }
 
@@ -4166,7 +3435,6 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     // re-run one kernel `reps` times back to back on the data of the last solve; the CG state it overwrites is
     // scratch once the solve has finished (dc already extracted).  0: k_cg_iter  1: k_schur (damping factor 1)
     // 2: one two-level CG iteration  3: k_tl_pspmv  4: the two-level setup  5: k_lin_points (overwrites W / V / g_p)
-    if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));  // (iterations queued past convergence read the status word)
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
     HIPCHK(hipMemsetAsync(h->cg.scal, 0, sizeof(double) * 4, h->stream));
     if (((which >= 2 && which <= 4) || which == 6 || which == 7) && !h->tlon) return INSFM_BA_EINVAL;
@@ -4213,7 +3481,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 });
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
-                                                                h->Lf, h->cg, 0);
+                                                                h->Lf, h->cg);
             else {
                 const int det = h->d.deterministic;
                 h->d.deterministic = 0;
@@ -4248,28 +3516,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     const double* src = nullptr;
     size_t n = 0;
     switch (which) {
-        case 0:
-            if (!h->W) { h->err = "W is not formed by the re-deriving Schur (use deterministic = 1 or INSFM_SCHUR_W=1)"; return INSFM_BA_EINVAL; }
-            if (h->w_compact) {  // rebuilt as [3][D] records from the compact ones at the linearization point
-                n = Nl * D * 3;
-                if (n == 0) return 0;
-                double* tmp = nullptr;
-                HIPCHK(hipMalloc(&tmp, sizeof(double) * n));
-                int rc = with_D(h->D, [&](auto dc_) -> int {
-                    constexpr int DV = decltype(dc_)::value;
-                    if constexpr (DV >= 7)
-                        k_w_expand<DV><<<cdiv(Nl, kThreads), kThreads, 0, h->stream>>>(
-                            (int)Nl, h->cam, h->ptl, h->cams_lin, h->pts_lin, h->W, tmp);
-                    return launch_err(h, "k_w_expand");
-                });
-                hipError_t e = hipStreamSynchronize(h->stream);
-                if (!rc && e == hipSuccess) e = hipMemcpy(host, tmp, sizeof(double) * n, hipMemcpyDeviceToHost);
-                (void)hipFree(tmp);
-                if (rc) return rc;
-                if (e != hipSuccess) { h->err = hipGetErrorString(e); return INSFM_BA_EHIP; }
-                return (int64_t)n;
-            }
-            src = h->W; n = Nl * D * 3; break;
+        case 0: src = h->W; n = Nl * D * 3; break;
         case 1: src = h->V; n = Pl * 6; break;
         case 2: src = h->gp; n = Pl * 3; break;
         case 3: src = h->U; n = C * D * D; break;
@@ -4282,7 +3529,6 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 9: src = h->tl.u; n = h->tlon ? C * D : 0; break;
         case 10: src = h->cg.w[0]; n = C * D; break;
         case 11: src = h->tl.rowR; n = h->tlon ? C * (D + 1) : 0; break;  // restriction row partials
-        case 22: src = h->tl.Rc; n = h->tlon ? (size_t)h->tl.m : 0; break;  // k_tl_pc phase timestamps (PC_TRACE)
         case 12: src = h->Einvbuf[0]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 13: src = h->Einvbuf[1]; n = h->tlon ? (size_t)h->tl.m * h->tl.m : 0; break;
         case 14: src = h->tl.gd; n = h->tlon ? 2 * C : 0; break;
@@ -4294,7 +3540,7 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
     if (int rc0 = side_flush(h)) return rc0;
     if (int rc0 = lin_join(h)) return rc0;
     if (n) HIPCHK(hipMemcpyAsync(host, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream)); if (h->cgs) HIPCHK(hipStreamSynchronize(h->cgs));
+    HIPCHK(hipStreamSynchronize(h->stream));
     return (int64_t)n;
 }
 

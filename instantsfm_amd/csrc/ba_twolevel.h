@@ -38,11 +38,6 @@ struct TlBufs {
     double* Rc;          // [m]   (debug) restriction
     double* gd;          // [3][C] row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2 (k_tl_pspmv), rows in cluster-member order
     double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
-    // cluster reduction in k_tl_pspmv (nullptr: k_tl_pc reduces the row partials itself): the last-arriving row of a
-    // cluster sums its members' partials (members in camera order) into
-    int* ccnt;           // [nc] arrival counters (reset to 0 by the last arriver)
-    double* Rcl;         // [nc][MC] restriction Z~^T w per cluster
-    double* gcl;         // [3][nc] the scalar partials per cluster
     // atomic cluster sums (single GPU, non-deterministic mode; nullptr otherwise): k_tl_pspmv adds each row's
     // restriction and scalar partials into its cluster's entries with no-return f64 atomics, double-buffered by
     // iteration parity (k_tl_pc of iteration i reads buffer i & 1 and clears buffer (i + 1) & 1 for k_tl_pspmv)
@@ -666,12 +661,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     __shared__ double y[MC];
     __shared__ double red[3][kPcWaves];
     __shared__ double sc[3];
-#ifdef PC_TRACE
-#define PCT(k) if (blockIdx.x == 0 && threadIdx.x == 0 && it == 3) tl.Rc[k] = (double)wall_clock64();
-#else
-#define PCT(k)
-#endif
-    PCT(0)
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int c = blockIdx.x, m = tl.m;
     const bool setup = it < 0;
@@ -690,13 +679,12 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     // issue order), so that reduction overlaps the E^-1 / restriction batch still in flight
     // the first GK partials per thread are held in registers and summed at the scalar phase (a summing loop here
     // would wait for them before the batch below is issued); rows past GK * kPcThreads are summed there too
-    // with the cluster reduction (tl.ccnt) k_tl_pspmv's last arrivers left one record per cluster: nc scalar partials
-    // and the full restriction (m values) instead of C and C * MC row partials
-    const bool usea = tl.Racc != nullptr && !setup;
-    const bool usecl = (tl.ccnt != nullptr || usea) && !setup;
-    const double* gsrc = usea ? tl.Gacc + (size_t)(it & 1) * 3 * tl.nc : (usecl ? tl.gcl : tl.gd);
+    // with the atomic cluster sums (tl.Racc) k_tl_pspmv left one record per cluster: nc scalar partials and the full
+    // restriction (m values) instead of C and C * MC row partials
+    const bool usecl = tl.Racc != nullptr && !setup;
+    const double* gsrc = usecl ? tl.Gacc + (size_t)(it & 1) * 3 * tl.nc : tl.gd;
     const int gn = usecl ? tl.nc : C;
-    const double* rsrc = usea ? tl.Racc + (size_t)(it & 1) * tl.m : tl.Rcl;
+    const double* rsrc = usecl ? tl.Racc + (size_t)(it & 1) * tl.m : nullptr;
     constexpr int GK = 2;
     double ga0[GK], ga1[GK], ga2[GK];
 #pragma unroll
@@ -745,7 +733,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
 #pragma unroll
     for (int k = 0; k < MC; ++k) Zq[k] = tl.Ztc[ci * MC + k];
     const size_t pidx = (size_t)tl.cl_cams[e0 + tp / D] * D + tp % D;  // only the output store waits for it
-    PCT(1)
     if (!setup) {
         const int i = it;
         double g0 = 0.0, g1 = 0.0, g2 = 0.0;
@@ -818,7 +805,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
                                                                     nlr0 - UR * kPcThreads);
         }
     }
-    PCT(2)
     if (use && !usecl) {
         // full restriction: entry (c', k) sums the row partials of cluster c' in ascending camera order (from LDS)
         for (int pass = 0; pass < np; ++pass) {
@@ -840,7 +826,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     }
     if (use) {
         __syncthreads();
-        PCT(3)
         constexpr int KPW = (MC + kPcWaves - 1) / kPcWaves, LPL = (kCoarseMax + 63) / 64;
         double sy[KPW];
 #pragma unroll
@@ -865,7 +850,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         __syncthreads();
     }
-    PCT(4)
     double* dst = setup ? tl.u : cg.s[1];
     for (int e = t; e < ne * D; e += kPcThreads) {
         const bool first = e == t;
@@ -880,8 +864,6 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
         }
         dst[idx] = v;
     }
-    PCT(5)
-#undef PCT
 }
 
 // k_tl_pc for iterations it >= 0 when the row partials arrive as per-cluster sums (tl.Racc: atomic cluster sums):
@@ -1161,29 +1143,6 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
         return;
     }
     if (lane == 0) { st_sc1(tl.gd + cp, g0); st_sc1(tl.gd + C + cp, g1); st_sc1(tl.gd + 2 * C + cp, g2); }
-    if (tl.ccnt == nullptr) return;
-    // the cluster's last-arriving row reduces its members' partials (fixed order: members ascending)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int c = tl.clab[row], e0 = tl.cl_ptr[c], e1 = tl.cl_ptr[c + 1];
-    int last = 0;
-    if (lane == 0)
-        last = __hip_atomic_fetch_add(tl.ccnt + c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == e1 - e0 - 1;
-    if (__builtin_amdgcn_readfirstlane(last) == 0) return;
-    if (lane < MC + 3) {
-        const double* src = lane < MC ? tl.rowR + lane : tl.gd + (size_t)(lane - MC) * C;
-        const int step = lane < MC ? MC : 1;
-        double v = 0.0;
-        int e = e0;
-        for (; e + 4 <= e1; e += 4) {  // loads four at a time, adds in member order
-            const double v0 = ld_sc1(src + (size_t)e * step), v1 = ld_sc1(src + (size_t)(e + 1) * step);
-            const double v2 = ld_sc1(src + (size_t)(e + 2) * step), v3 = ld_sc1(src + (size_t)(e + 3) * step);
-            v += v0; v += v1; v += v2; v += v3;
-        }
-        for (; e < e1; ++e) v += ld_sc1(src + (size_t)e * step);
-        if (lane < MC) tl.Rcl[(size_t)c * MC + lane] = v;
-        else tl.gcl[(size_t)(lane - MC) * tl.nc + c] = v;
-    }
-    if (lane == 0) __hip_atomic_store(tl.ccnt + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 }  // namespace insfm

@@ -6,6 +6,9 @@
 // Deadline: if neither the progress word nor the status changes for `stall_s` seconds of wall clock, the poll gives up
 // (CgPoll::kStalled) instead of spinning forever on a CG launch that never publishes (a hung kernel, or a fault that
 // does not surface as a stream error).  A live CG iteration takes ~10-20 us, so any stall of seconds is a failure.
+// Multi-rank, the stall clock only starts once the work queued in front of the CG (the cross-rank exchange) has
+// completed; that gate has its own, longer deadline `gate_s` (a peer that died or never sends its exchange would
+// otherwise keep the gate shut forever): past it the poll returns CgPoll::kGateStalled.
 #pragma once
 #include <chrono>
 #include <cstdlib>
@@ -14,7 +17,7 @@
 namespace insfm {
 
 struct CgPoll {
-    enum Result { kDone = 0, kDrained = 1, kEnqueueError = -1, kStreamError = -2, kStalled = -3 };
+    enum Result { kDone = 0, kDrained = 1, kEnqueueError = -1, kStreamError = -2, kStalled = -3, kGateStalled = -4 };
     int enq = 0;            // iterations enqueued so far
     int last_reached = 0;   // last progress word seen
     long spins = 0;
@@ -32,6 +35,9 @@ inline double cg_stall_limit_s(const char* env_value) {
     return 10.0;
 }
 
+// Deadline of the multi-rank gate (the exchange in front of the CG): six stall limits.
+inline double cg_gate_limit_s(double stall_s) { return 6.0 * stall_s; }
+
 // status():  the published status word (0 running, non-zero finished)
 // reached(): the published count of iterations started
 // enqueue(from, to) -> int: launch iterations [from, to); non-zero = error (returned as kEnqueueError, code in *rc)
@@ -40,11 +46,12 @@ inline double cg_stall_limit_s(const char* env_value) {
 // pause(): a CPU relax hint
 // started(): whether the work queued in front of the CG has completed; until it has, the deadline clock does not run
 //   (multi-rank: the first CG launch waits for the cross-rank exchange, i.e. for the slowest peer, which is not a
-//   stall of this device)
+//   stall of this device); it must open within gate_s seconds of the poll's start
 template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause, class Started>
-int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reached reached, Enqueue enqueue,
-            Query query, Now now, Pause pause, Started started, int* rc) {
-    double t_progress = now();
+int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, double gate_s, Status status, Reached reached,
+            Enqueue enqueue, Query query, Now now, Pause pause, Started started, int* rc) {
+    const double t_start = now();
+    double t_progress = t_start;
     bool live = false;
     for (;;) {
         if (status() != 0) return CgPoll::kDone;
@@ -73,7 +80,13 @@ int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reac
             if (q < 0) return CgPoll::kStreamError;
             if (!live) {
                 live = started();
-                if (!live) t_progress = now();
+                if (!live) {
+                    t_progress = now();
+                    if (t_progress - t_start > gate_s) {
+                        s.stalled_s = t_progress - t_start;
+                        return CgPoll::kGateStalled;
+                    }
+                }
             }
             const double dt = now() - t_progress;
             if (dt > stall_s) {
@@ -88,7 +101,8 @@ int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reac
 template <class Status, class Reached, class Enqueue, class Query, class Now, class Pause>
 int cg_poll(CgPoll& s, int limit, int ahead, double stall_s, Status status, Reached reached, Enqueue enqueue,
             Query query, Now now, Pause pause, int* rc) {
-    return cg_poll(s, limit, ahead, stall_s, status, reached, enqueue, query, now, pause, [] { return true; }, rc);
+    return cg_poll(s, limit, ahead, stall_s, stall_s, status, reached, enqueue, query, now, pause, [] { return true; },
+                   rc);
 }
 
 inline double wall_seconds() {

@@ -113,11 +113,21 @@ done:
     return res;
 }
 
-static int get_buf(PyObject* o, Py_buffer* b, Py_ssize_t itemsize, const char* what) {
-    if (PyObject_GetBuffer(o, b, PyBUF_C_CONTIGUOUS) < 0) return -1;
-    if (b->itemsize != itemsize && b->len % itemsize != 0) {
+/* A C-contiguous buffer of exactly the expected element type: kind 'i' = 8-byte signed integer, 'f' = 8-byte float,
+ * 'b' = one byte (uint8 / int8 / bool).  A buffer of another dtype is refused even when its byte length happens to
+ * divide (an int32 obs array or float32 features would otherwise be reinterpreted). */
+static int get_buf(PyObject* o, Py_buffer* b, char kind, const char* what) {
+    if (PyObject_GetBuffer(o, b, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) < 0) return -1;
+    const char* f = b->format ? b->format : "B";
+    while (*f == '@' || *f == '=' || *f == '<') ++f;  /* native / little-endian byte order only */
+    int ok = 0;
+    if (kind == 'i') ok = b->itemsize == 8 && (f[0] == 'l' || f[0] == 'q') && f[1] == 0;
+    else if (kind == 'f') ok = b->itemsize == 8 && f[0] == 'd' && f[1] == 0;
+    else ok = b->itemsize == 1 && (f[0] == 'B' || f[0] == 'b' || f[0] == '?') && f[1] == 0;
+    if (!ok) {
+        PyErr_Format(PyExc_TypeError, "finish: %s has the wrong dtype (buffer format '%s', itemsize %zd)", what,
+                     b->format ? b->format : "B", b->itemsize);
         PyBuffer_Release(b);
-        PyErr_Format(PyExc_TypeError, "finish: %s has the wrong element size", what);
         return -1;
     }
     return 0;
@@ -140,9 +150,9 @@ static PyObject* finish(PyObject* self, PyObject* args) {
     PyObject* res = NULL;
     char *pc = NULL, *pp = NULL;
     int64_t *tid = NULL, *cnt = NULL;
-    if (get_buf(o_obs, &bo, 8, "obs") || get_buf(o_len, &bl, 8, "lengths") || get_buf(o_reg, &br, 1, "registered") ||
-        get_buf(o_feat, &bf, 8, "features") || get_buf(o_foff, &bff, 8, "foff") || get_buf(o_pts, &bp, 8, "points") ||
-        get_buf(o_pose, &bq, 8, "poses"))
+    if (get_buf(o_obs, &bo, 'i', "obs") || get_buf(o_len, &bl, 'i', "lengths") || get_buf(o_reg, &br, 'b', "registered") ||
+        get_buf(o_feat, &bf, 'f', "features") || get_buf(o_foff, &bff, 'i', "foff") || get_buf(o_pts, &bp, 'f', "points") ||
+        get_buf(o_pose, &bq, 'f', "poses"))
         goto done;
     {
         const int64_t* obs = (const int64_t*)bo.buf;
@@ -157,6 +167,16 @@ static PyObject* finish(PyObject* self, PyObject* args) {
             PyErr_SetString(PyExc_ValueError, "finish: inconsistent array sizes");
             goto done;
         }
+        /* the valid tracks' lengths must sum to the observation count exactly (checked before any write) */
+        {
+            int64_t tot = 0;
+            for (int64_t t = 0; t < nT; ++t)
+                if (len[t] >= min_len) {
+                    if (len[t] < 0) { tot = -1; break; }
+                    tot += len[t];
+                }
+            if (tot != n) { PyErr_SetString(PyExc_ValueError, "finish: lengths do not match obs"); goto done; }
+        }
         /* track id of every observation (valid tracks only, in order) */
         tid = (int64_t*)PyMem_Malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
         if (!tid) { PyErr_NoMemory(); goto done; }
@@ -164,9 +184,8 @@ static PyObject* finish(PyObject* self, PyObject* args) {
             int64_t k = 0;
             for (int64_t t = 0; t < nT; ++t) {
                 if (len[t] < min_len) continue;
-                for (int64_t q = 0; q < len[t] && k < n; ++q) tid[k++] = t;
+                for (int64_t q = 0; q < len[t]; ++q) tid[k++] = t;
             }
-            if (k != n) { PyErr_SetString(PyExc_ValueError, "finish: lengths do not match obs"); goto done; }
         }
         int bad = 0;
         #pragma omp parallel for schedule(static) reduction(|:bad)
@@ -322,10 +341,20 @@ static PyMethodDef methods[] = {
 
 static struct PyModuleDef mod = {PyModuleDef_HEAD_INIT, "_packx", NULL, -1, methods, NULL, NULL, NULL, NULL};
 
+/* SRC_HASH: instantsfm_amd/build.py passes the hash of this file (packx_hash()); the loader compares it with the tree */
+#ifndef PACKX_SRC_HASH
+#define PACKX_SRC_HASH "unknown"
+#endif
+
 PyMODINIT_FUNC PyInit__packx(void) {
     import_array();
     s_obs = PyUnicode_InternFromString("observations");
     s_xyz = PyUnicode_InternFromString("xyz");
     if (!s_obs || !s_xyz) return NULL;
-    return PyModule_Create(&mod);
+    PyObject* m = PyModule_Create(&mod);
+    if (m && PyModule_AddStringConstant(m, "SRC_HASH", PACKX_SRC_HASH) < 0) {
+        Py_DECREF(m);
+        return NULL;
+    }
+    return m;
 }

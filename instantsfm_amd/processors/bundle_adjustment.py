@@ -14,21 +14,38 @@ from ..scene.defs import CameraModelId, IMPLEMENTED_MODELS, get_camera_model_inf
 
 
 def _load_packx():
-    """The native packing extension (csrc/packx.c, built by instantsfm_amd.build next to libinsfm_ba.so)."""
+    """The native packing extension (csrc/packx.c, built by instantsfm_amd.build next to libinsfm_ba.so).  Missing: a
+    warning, and the bit-identical numpy path packs instead.  Built from other sources than this tree's packx.c: an
+    error, as for the main library (_capi._check_provenance)."""
     import importlib.util
     import os
     import sysconfig
+    import warnings
     path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_lib",
                         "_packx" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
     if not os.path.exists(path):
+        warnings.warn(f"{path} not built: TorchBA packs with the (slower, bit-identical) numpy path", RuntimeWarning)
         return None
     spec = importlib.util.spec_from_file_location("_packx", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    from .. import build as _b
+    if os.path.exists(_b.PACKX_SRC) and getattr(mod, "SRC_HASH", None) != _b.packx_hash():
+        raise RuntimeError(f"{path} was built from other sources (SRC_HASH {getattr(mod, 'SRC_HASH', None)}, this tree's "
+                           f"packx.c hashes to {_b.packx_hash()}): rebuild it (python -c 'import __graft_entry__ as g; "
+                           "g.build()')")
     return mod
 
 
-_packx = _load_packx()
+_PACKX = []
+
+
+def packx():
+    """The native packing extension, loaded (and its provenance checked) on first use: the package must stay
+    importable while build() rebuilds a stale extension."""
+    if not _PACKX:
+        _PACKX.append(_load_packx())
+    return _PACKX[0]
 
 
 def _quat_xyzw_from_matrix(R):
@@ -131,7 +148,7 @@ def pack(cameras, images, tracks, options, native=True):
     min_len = options['min_num_view_per_track']
     track_keys = list(tracks.keys())
     track_vals = list(tracks.values())
-    got = _packx.collect(track_vals, int(min_len)) if (native and _packx is not None) else None
+    got = packx().collect(track_vals, int(min_len)) if (native and packx() is not None) else None
     if got is not None:
         lengths = np.frombuffer(got[0], np.int64)
         obs_valid = np.frombuffer(got[1], np.int64).reshape(-1, 2)
@@ -165,7 +182,7 @@ def pack(cameras, images, tracks, options, native=True):
     if got is not None:
         # :85-113 in C: registered filter, feature gather, cheirality z > 0.1, torch.unique compaction
         cp = np.ascontiguousarray(camera_params)
-        r = _packx.finish(obs_valid, lengths, int(min_len), registered.astype(np.uint8), feat_all, foff,
+        r = packx().finish(obs_valid, lengths, int(min_len), registered.astype(np.uint8), feat_all, foff,
                           np.ascontiguousarray(points_3d), cp, cp.shape[1])
         points_2d = np.frombuffer(r[0], np.float64).reshape(-1, 2)
         cam_inv, pt_inv = np.frombuffer(r[1], np.int64), np.frombuffer(r[2], np.int64)
@@ -225,8 +242,8 @@ def update(cameras, images, tracks, packed, camera_params, points_3d):
     full[:, packed.pp_indices] = packed.camera_pps
     mats = _pose_matrices(full[:, :7])
     keys = packed.track_keys
-    if _packx is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2:
-        _packx.assign_xyz(list(tracks.values()) if packed.track_vals is None else packed.track_vals,
+    if packx() is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2:
+        packx().assign_xyz(list(tracks.values()) if packed.track_vals is None else packed.track_vals,
                           np.ascontiguousarray(packed.unique_points, np.int64), pts)
     else:
         for orig, xyz in zip(packed.unique_points.tolist(), pts):

@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from ..engine import GlobalPositioner
-from .bundle_adjustment import _packx
+from .bundle_adjustment import packx
 
 
 class PackedGP:
@@ -29,7 +29,7 @@ def pack_gp(cameras, images, tracks, depths, options, depth_only=False, native=T
     attributes that are not plain ndarrays (or ``native=False``) take the numpy path, which gives the same arrays."""
     min_len = options['min_num_view_per_track']
     keys, vals = list(tracks.keys()), list(tracks.values())
-    got = _packx.collect(vals, 0) if (native and _packx is not None) else None
+    got = packx().collect(vals, 0) if (native and packx() is not None) else None
     if got is not None:
         lengths = np.frombuffer(got[0], np.int64)
         short = lengths < min_len
@@ -138,8 +138,8 @@ class TorchGP:
         # uniform(-1, 1, 3) per track (tests/test_gp_packing.py), and each track gets its own row
         vals = list(tracks.values())
         xyz = scene_scale * np.random.uniform(-1, 1, 3 * len(vals)).reshape(-1, 3)
-        if _packx is not None and xyz.dtype == np.float64 and vals:
-            _packx.assign_xyz(vals, np.arange(len(vals), dtype=np.int64), np.ascontiguousarray(xyz))
+        if packx() is not None and xyz.dtype == np.float64 and vals:
+            packx().assign_xyz(vals, np.arange(len(vals), dtype=np.int64), np.ascontiguousarray(xyz))
         else:
             for track, row in zip(vals, xyz):
                 track.xyz = row
@@ -215,8 +215,8 @@ class TorchGP:
     def _write_back(images, pk, pos_t, pts_t):
         pts = pts_t.detach().cpu().numpy()
         pos = pos_t.detach().cpu().numpy()
-        if _packx is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2 and len(pts):
-            _packx.assign_xyz(pk.track_list, np.arange(len(pk.track_list), dtype=np.int64), pts)
+        if packx() is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2 and len(pts):
+            packx().assign_xyz(pk.track_list, np.arange(len(pk.track_list), dtype=np.int64), pts)
         else:
             for track, xyz in zip(pk.track_list, pts):
                 track.xyz = xyz

@@ -9,7 +9,7 @@ FilterTracksByReprojectionNormalized's counter, which the reference computes on 
 import numpy as np
 
 from .. import passes
-from .bundle_adjustment import _packx
+from .bundle_adjustment import packx
 
 EPSILON = 1e-10
 
@@ -18,9 +18,9 @@ def collect_tracks(tracks, with_obs=True):
     """(per-track counts int64, observations [X,2] int64 in dict order, xyz [T,3] float64) read in one C loop by the
     native pack extension (csrc/packx.c ``collect``), or None when it is missing or a Track's attributes are not the
     plain (n, 2) integer / (3,) float arrays it takes.  ``with_obs=False`` skips copying the observations."""
-    if _packx is None or not tracks:
+    if packx() is None or not tracks:
         return None
-    got = _packx.collect(list(tracks.values()), 0 if with_obs else (1 << 62))
+    got = packx().collect(list(tracks.values()), 0 if with_obs else (1 << 62))
     if got is None:
         return None
     return (np.frombuffer(got[0], np.int64), np.frombuffer(got[1], np.int64).reshape(-1, 2),

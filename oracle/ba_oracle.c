@@ -347,15 +347,21 @@ static int ora_aggregate(ora_t* h, int K);
 /* The coarse dimension nclust * (D + 1) is capped at COARSE_MAX (the GPU's k_tl_pc keeps a cluster's rows of E^-1
  * in registers; csrc/ba_twolevel.h COARSE_MAX_DIM): while the aggregation yields more clusters, it is redone with the
  * target size grown in proportion to the excess, K' = max(K + 1, ceil(K nclust (D + 1) / COARSE_MAX)) rounded up to
- * even (aggregates below K / 2 are dissolved, so an odd K would keep singletons). */
+ * even (aggregates below K / 2 are dissolved, so an odd K would keep singletons), at most C.  With K = C the clusters
+ * are the co-visibility components; if even those exceed the cap, the solver falls back to block-Jacobi (precond 0):
+ * returns 0 then, 1 when the clusters fit. */
 #define COARSE_MAX 768
-static void ora_cluster_cameras(ora_t* h) {
-    int K = h->cluster_size, nc;
-    while ((nc = ora_aggregate(h, K)) * (h->D + 1) > COARSE_MAX) {
-        const long g = ((long)K * nc * (h->D + 1) + COARSE_MAX - 1) / COARSE_MAX;
-        K = g > K + 1 ? (int)g : K + 1;
+static int ora_cluster_cameras(ora_t* h) {
+    int K = h->cluster_size < h->C ? h->cluster_size : h->C, nc;
+    while ((nc = ora_aggregate(h, K)) * (h->D + 1) > COARSE_MAX && K < h->C) {
+        long g = ((long)K * nc * (h->D + 1) + COARSE_MAX - 1) / COARSE_MAX;
+        if (g < K + 1) g = K + 1;
+        if (g > h->C) g = h->C;
+        K = (int)g;
         K += K & 1;
+        if (K > h->C) K = h->C;
     }
+    return nc * (h->D + 1) <= COARSE_MAX;
 }
 
 static int ora_aggregate(ora_t* h, int K) {
@@ -573,7 +579,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     free(cols); free(cnt);
     h->clab = (int*)malloc(sizeof(int) * C);
     h->csize = (int*)calloc(C, sizeof(int));
-    ora_cluster_cameras(h);
+    if (!ora_cluster_cameras(h) && h->precond == 1) h->precond = 0;
     /* lower references: row j lists (i < j, blk of (i,j)) in increasing i */
     h->lo_ptr = (int*)calloc(C + 1, sizeof(int));
     for (int i = 0; i < C; ++i)

@@ -68,11 +68,21 @@ int main() {
         int rc = 0;
         double fake_t = 0.0, opened = -1.0;
         const int r = cg_poll(
-            s, 502, 2, 0.5, [&] { d.tick(); return d.status; }, [&] { return d.reached; },
+            s, 502, 2, 0.5, 3.0, [&] { d.tick(); return d.status; }, [&] { return d.reached; },
             [&](int, int to) { d.enqueued = to; return 0; }, [&] { return 1; },
             [&] { fake_t += 1e-4; return fake_t; }, [] {},
             [&] { const bool o = fake_t >= 2.0; if (o && opened < 0) opened = fake_t; return o; }, &rc);
         std::printf("gated result=%d stalled_s=%.3f end=%.3f opened=%.3f\n", r, s.stalled_s, fake_t, opened);
+    }
+    {   // gate never opens (a peer died before its exchange): the gate deadline (3 s) ends the poll with kGateStalled
+        FakeDevice d; d.hung = true; CgPoll s; s.enq = 4; d.enqueued = 4;
+        int rc = 0;
+        double fake_t = 0.0;
+        const int r = cg_poll(
+            s, 502, 2, 0.5, 3.0, [&] { d.tick(); return d.status; }, [&] { return d.reached; },
+            [&](int, int to) { d.enqueued = to; return 0; }, [&] { return 1; },
+            [&] { fake_t += 1e-4; return fake_t; }, [] {}, [] { return false; }, &rc);
+        std::printf("gate_never result=%d stalled_s=%.3f end=%.3f\n", r, s.stalled_s, fake_t);
     }
     {   // status never set, device drains everything: stops at the launch limit
         FakeDevice d; CgPoll s;
@@ -100,7 +110,7 @@ int main() {
         const int code = run(d, 502, 2, 10.0, s);
         std::printf("enqueue_error code=%d\n", code);
     }
-    std::printf("limit default=%.1f env=%.2f bad=%.1f\n", cg_stall_limit_s(nullptr), cg_stall_limit_s("0.25"),
-                cg_stall_limit_s("x"));
+    std::printf("limit default=%.1f env=%.2f bad=%.1f gate=%.1f\n", cg_stall_limit_s(nullptr), cg_stall_limit_s("0.25"),
+                cg_stall_limit_s("x"), cg_gate_limit_s(10.0));
     return 0;
 }

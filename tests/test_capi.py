@@ -55,7 +55,8 @@ def _create(desc, uv, cam, pt, pp):
     return rc, msg
 
 
-@pytest.mark.parametrize("case", ["model7", "model10", "not_track_major", "cam_oob", "pt_oob", "bad_rank"])
+@pytest.mark.parametrize("case", ["model7", "model10", "not_track_major", "cam_oob", "pt_oob", "bad_rank",
+                                  "schur_variant"])
 def test_create_rejects_bad_inputs_without_gpu(case):
     d = _capi.default_desc()
     uv = np.zeros((4, 2))
@@ -75,6 +76,8 @@ def test_create_rejects_bad_inputs_without_gpu(case):
         pt = np.array([0, 0, 1, 5], np.int32)
     elif case == "bad_rank":
         d.world_size, d.rank = 2, 3
+    elif case == "schur_variant":  # the round-2/3 Schur variants 1-3 were removed
+        d.schur_variant = 3
     rc, msg = _create(d, uv, cam, pt, pp)
     assert rc == _capi.INSFM_BA_EINVAL, (rc, msg)
     assert msg

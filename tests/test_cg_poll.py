@@ -48,6 +48,7 @@ def test_stream_error_and_enqueue_error(poll_out):
 def test_stall_limit_env(poll_out):
     lim = poll_out["limit"]
     assert float(lim["default"]) == 10.0 and float(lim["env"]) == 0.25 and float(lim["bad"]) == 10.0
+    assert float(lim["gate"]) == 60.0
 
 
 def test_deadline_starts_after_the_gate(poll_out):
@@ -58,3 +59,12 @@ def test_deadline_starts_after_the_gate(poll_out):
     assert float(g["opened"]) >= 2.0
     assert 0.5 <= float(g["stalled_s"]) < 0.6
     assert float(g["end"]) >= 2.5
+
+
+def test_gate_that_never_opens_ends_the_poll(poll_out):
+    """A peer that dies before its exchange keeps the multi-rank gate shut: the poll must still end (kGateStalled,
+    -4) once the gate deadline passes, not spin forever with the stall clock held at zero."""
+    g = poll_out["gate_never"]
+    assert int(g["result"]) == -4
+    assert 3.0 <= float(g["stalled_s"]) < 3.1
+    assert 3.0 <= float(g["end"]) < 3.2

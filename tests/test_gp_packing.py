@@ -106,8 +106,8 @@ def test_gp_pack_native_matches_numpy_path(golden_dir, name):
     """The C collect path of pack_gp (observations and xyz read in one loop) gives the numpy path's arrays and the
     same scene mutations, also when one Track's observations are an array layout collect does not take (int16,
     Fortran order: the numpy path for the whole call)."""
-    from instantsfm_amd.processors.bundle_adjustment import _packx
-    assert _packx is not None
+    from instantsfm_amd.processors.bundle_adjustment import packx
+    assert packx() is not None
     g = np.load(os.path.join(golden_dir, name + ".npz"))
     outs = []
     for native in (True, False):

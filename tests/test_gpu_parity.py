@@ -445,48 +445,6 @@ def test_solver_failure_leaves_caller_buffers_unchanged():
     assert np.array_equal(co, prob.cams_init) and np.array_equal(po, prob.points_init)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
-@pytest.mark.parametrize("model", (0, 2, 4, 9))
-def test_schur_variant_solve_parity(model, variant):
-    """The other Schur builds (desc.schur_variant 1: re-derived blocks, LDS-atomic rows, 2: re-derived, MFMA register
-    accumulation for D <= 8, D > 8 falls back to 1; 3: compact W records with the camera factors applied per block)
-    against the oracle: b, S~, dc, dp at equal PCG iterations, same tolerances as test_solve_parity.  1 and 2 never
-    form W, so the camera-point blocks are checked through S~; 3's records are rebuilt into W_o and checked too."""
-    prob = make_problem(30, 800, seed=5, model=model)
-    eng, ora = engines(prob, schur_variant=variant)
-    eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
-    ora.linearize(prob.cams_init, prob.points_init)
-    if variant == 3:
-        N, D = prob.n_obs, eng.D
-        assert rel(eng.debug_get(0, (N, 3, D)).transpose(0, 2, 1), ora.get(O.W)) < 1e-12
-    f = 1.0 + 1e-4
-    assert eng.debug_solve(f) == ora.solve(f)
-    C, P, D = prob.n_cams, prob.n_points, eng.D
-    nb = eng.nnzb()
-    assert rel(eng.debug_get(6, (C, D)), ora.get(O.B)) < 1e-10
-    assert rel(eng.debug_get(5, (nb, D, D)), ora.get(O.S)) < 1e-9
-    assert rel(eng.debug_get(7, (C, D)), ora.get(O.DC)) < 1e-8
-    assert rel(eng.debug_get(8, (P, 3)), ora.get(O.DP)) < 1e-8
-
-
-@pytest.mark.parametrize("variant", [1, 2, 3])
-def test_schur_variant_step_parity(variant):
-    """Config 2 LM steps with the re-deriving Schur builds: same trials / PCG iterations as the oracle, parameters
-    1e-9 (long rows: more than 64 upper blocks split into several work items)."""
-    prob = make_config(2)
-    eng, ora = engines(prob, schur_variant=variant)
-    cg, pg = dev(prob.cams_init), dev(prob.points_init)
-    co, po = prob.cams_init.copy(), prob.points_init.copy()
-    for s in range(2):
-        lg, st = eng.step(cg, pg)
-        lo = ora.step(co, po)
-        so = ora.stats()
-        assert st["pcg_iters"] == so["pcg_iters"] and st["trials"] == so["trials"], (s, st, so)
-        assert abs(lg - lo) / lo < 1e-10, (s, lg, lo)
-        assert rel(cg.cpu().numpy(), co) < 1e-9
-        assert rel(pg.cpu().numpy(), po) < 1e-9
-
-
 def _spd(m, seed, cond_exp=4.0):
     """B B^T + 1e-3 m I with rows / columns scaled over cond_exp decades (the coarse matrix's wide diagonal)."""
     rng = np.random.default_rng(seed)
@@ -529,10 +487,9 @@ def test_coarse_inverse_matches_numpy(m):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.timeout(300)
 def test_device_block_pattern_matches_host_pass():
     """insfm_ba_create derives the Schur block pattern and the co-visibility graph on the device (k_pattern) on a
-    single rank; the host pass (multi-rank, INSFM_PATTERN_HOST=1) must give the same result: the same block count,
+    single rank; the host pass (multi-rank, INSFM_DIAG=pattern_host) must give the same result: the same block count,
     the same two-level clusters (which read the graph's weights) and bitwise the same deterministic LM steps, on
     config 2, a scene with duplicated observations and one with a camera that sees nothing."""
     import json
@@ -541,53 +498,14 @@ def test_device_block_pattern_matches_host_pass():
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = []
-    for host in ("0", "1"):
+    for diag in ("", "pattern_host"):
         p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pattern_check.py")], capture_output=True,
-                           text=True, timeout=140, env=dict(os.environ, INSFM_PATTERN_HOST=host), cwd=repo)
+                           text=True, timeout=140, env=dict(os.environ, INSFM_DIAG=diag), cwd=repo)
         assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
         outs.append(json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]))
-    assert outs[0]["env"] == "0" and outs[1]["env"] == "1"
+    assert outs[0]["env"] == "" and outs[1]["env"] == "pattern_host"
     assert outs[0]["scenes"] == outs[1]["scenes"]
     assert set(outs[0]["scenes"]) == {"config2", "duplicates", "empty_camera"}
-
-
-def test_pc_cluster_reduction_parity():
-    """The opt-in cluster reduction of the CG's row partials (INSFM_PC_CLUSTER=1: the last-arriving row of each cluster
-    in k_tl_pspmv sums its members' partials through write-through stores and one agent-scope counter; k_tl_pc then
-    reads one record per cluster) against the oracle on config-2 LM steps: same PCG iterations and trials, loss
-    1e-10, parameters 1e-9.  The variable is read once per process, hence the subprocess."""
-    import json
-    import os
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pc_cluster_check.py")], capture_output=True,
-                       text=True, timeout=280, env=dict(os.environ, INSFM_PC_CLUSTER="1"), cwd=repo)
-    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
-    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert out["env"] == "1"
-    for s in out["steps"]:
-        assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
-        assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s
-
-
-def test_cg_stream_parity():
-    """The opt-in CG stream (INSFM_CG_STREAM=1: iterations on their own stream behind one event, the main stream gated
-    by k_cg_gate on the published status word, k_publish accepting only a converged CG) against the oracle on config-2
-    LM steps: same PCG iterations and trials, loss 1e-10, parameters 1e-9.  Read once per process: a subprocess."""
-    import json
-    import os
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    p = subprocess.run([sys.executable, os.path.join(repo, "tools", "pc_cluster_check.py"), "INSFM_CG_STREAM"],
-                       capture_output=True, text=True, timeout=280, env=dict(os.environ, INSFM_CG_STREAM="1"), cwd=repo)
-    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
-    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
-    assert out["env"] == "1"
-    for s in out["steps"]:
-        assert s["pcg"][0] == s["pcg"][1] and s["trials"][0] == s["trials"][1], s
-        assert s["loss_rel"] < 1e-10 and s["cams_rel"] < 1e-9 and s["points_rel"] < 1e-9, s
 
 
 @pytest.mark.parametrize("K", (2, 3))

@@ -109,7 +109,7 @@ def test_native_pack_is_built_and_matches_numpy_path():
     (a Python list) fall back to the numpy path."""
     from instantsfm_amd.processors import bundle_adjustment as BA
     from instantsfm_amd.synth import make_problem, to_scene
-    assert BA._packx is not None, "instantsfm_amd/_lib/_packx*.so not built (instantsfm_amd.build.build_packx)"
+    assert BA.packx() is not None, "instantsfm_amd/_lib/_packx*.so not built (instantsfm_amd.build.build_packx)"
     prob = make_problem(30, 1500, seed=3)
     cams, imgs, tracks = to_scene(prob)
     rng = np.random.default_rng(0)
@@ -135,9 +135,9 @@ def test_native_pack_is_built_and_matches_numpy_path():
         np.testing.assert_array_equal(x, y)
     np.testing.assert_array_equal(a.indices32()[0], a.camera_indices)
     np.testing.assert_array_equal(a.indices32()[1], a.point_indices)
-    assert BA._packx.collect(list(tracks.values()), 2) is not None
+    assert BA.packx().collect(list(tracks.values()), 2) is not None
     tracks[keys[0]].observations = tracks[keys[0]].observations.tolist()
-    assert BA._packx.collect(list(tracks.values()), 2) is None
+    assert BA.packx().collect(list(tracks.values()), 2) is None
     c = pack(cams, imgs, tracks, OPTS)
     for x, y in zip(_fields(c), _fields(b)):
         np.testing.assert_array_equal(x, y)

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Host-side cost of one TorchBA.Solve on the config-3 scene, phase by phase: pack(), engine creation
-(insfm_ba_create's host phases via INSFM_CREATE_TRACE=1, printed to stderr), the LM steps and the write-back.
+(insfm_ba_create's host phases via INSFM_DIAG=create, printed to stderr), the LM steps and the write-back.
 
-    INSFM_CREATE_TRACE=1 python tools/create_probe.py [--config 3] [--reps 3]
+    INSFM_DIAG=create python tools/create_probe.py [--config 3] [--reps 3]
 """
 import argparse
 import os

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Config-3 LM steps with INSFM_HOST_TRACE=2 (set it in the environment): the library prints, per step, the host
-timestamps (us since the step began) of its API calls to stderr.  usage: INSFM_HOST_TRACE=2 python tools/host_trace.py"""
+"""Config-3 LM steps with INSFM_DIAG=trace2 (set it in the environment): the library prints, per step, the host
+timestamps (us since the step began) of its API calls to stderr.  usage: INSFM_DIAG=trace2 python tools/host_trace.py"""
 import os
 import sys
 import time

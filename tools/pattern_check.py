@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Device vs host derivation of the Schur block pattern and the co-visibility graph in insfm_ba_create
-(INSFM_PATTERN_HOST=1 selects the host pass; read once per process).  For a few scenes -- config 2, a scene with
+(INSFM_DIAG=pattern_host selects the host pass; read once per process).  For a few scenes -- config 2, a scene with
 duplicated observations (two observations of one track on one camera) and one with a camera that sees nothing --
 prints one JSON line with the block count, the two-level cluster labels and the bits of three deterministic LM steps.
 Run twice by tests/test_gpu_parity.py::test_device_block_pattern_matches_host_pass and compared."""
@@ -36,7 +36,7 @@ def scenes():
 
 def main():
     dev = torch.device("cuda:0")
-    out = dict(env=os.environ.get("INSFM_PATTERN_HOST"), scenes={})
+    out = dict(env=os.environ.get("INSFM_DIAG", ""), scenes={})
     for name, prob in scenes():
         eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                              device=dev, deterministic=True)
