@@ -477,6 +477,8 @@ def solve_end_to_end(prob, dev):
     return {"solve_total_s": round(t["total_s"], 4), "pack_s": round(t["pack_s"], 4),
             "create_s": round(t["create_s"], 4), "steps_s": round(t["steps_s"], 4),
             "update_s": round(t["update_s"], 4), "steps": t["steps"], "host_frac": round(host / t["total_s"], 4),
+            "pack_phases_ms": {k: round(1e3 * v, 2) for k, v in t.get("pack_phases", {}).items()},
+            "update_phases_ms": {k: round(1e3 * v, 2) for k, v in t.get("update_phases", {}).items()},
             "final_rmse_px": t.get("final_rmse")}
 
 

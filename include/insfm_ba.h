@@ -87,7 +87,8 @@ typedef struct {
     int32_t pcg_iters_last; /* PCG iterations of the final trial */
     int32_t pcg_iters_total;
     int32_t solver_failed;
-    int32_t cg_launches;    /* k_cg_iter launches this step (incl. the cheap early-exit ones after convergence) */
+    int32_t cg_launches;    /* CG iteration launches this step (incl. the cheap early-exit ones after convergence;
+                               the persistent two-level CG k_tl_cgp counts one per solve) */
     double time_ms[8];      /* device time per phase (hipEvent on the library stream), filled when stats != NULL:
                                [0] linearize  [1] k_schur  [2] whole linear solve (point prep .. CG finish, incl. the
                                host polls of the CG status)  [3] back-substitution + update  [4] trial cost
@@ -149,7 +150,8 @@ const char* insfm_ba_last_error(const insfm_ba* h);
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cam_params, const double* points);
 /* Build and solve the damped system for cumulative damping factor f; returns PCG iterations or a negative code. */
 int insfm_ba_debug_solve(insfm_ba* h, double f);
-/* Copy an internal buffer to HOST memory: 0 W[N,3,D] (column-major blocks) 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
+/* Copy an internal buffer to HOST memory: 0 the camera-point records Y[N,3,D] (Y_o = W_o R_p^-T, R_p the Cholesky
+ * factor of point p's block damped for the first trial: S = U - sum Y Y^T; column-major blocks) 1 V[P,6] 2 g_p[P,3] 3 U[C,D,D] 4 g_c[C,D] 5 S(scaled after a
  * solve)[nnzb,D,D] 6 b[C,D] 7 dc[C,D] 8 dp[P,3].  Returns the number of doubles copied or a negative code. */
 int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
 /* Device time per launch (us, hipEvents on the library stream) of `reps` back-to-back launches of one kernel on the

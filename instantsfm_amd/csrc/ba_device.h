@@ -223,6 +223,36 @@ __device__ __forceinline__ double clampd(double x, double lo, double hi) { retur
 
 // Inverse of an SPD 3x3 given as [xx, xy, xz, yy, yz, zz] via Cholesky (same operation order as the oracle).
 // Returns false if not positive definite.  Output in the same packed layout.
+// The same Cholesky steps as spd3_inverse (bitwise the same inverse o), also returning the factor R (s = R R^T, lower)
+// and R^-1, packed (00, 10, 20, 11, 21, 22).  On failure nothing is written.
+__device__ __forceinline__ bool spd3_factor(const double s[6], double o[6], double R[6], double Ri[6]) {
+    const double a00 = s[0], a10 = s[1], a20 = s[2], a11 = s[3], a21 = s[4], a22 = s[5];
+    if (!(a00 > 0.0)) return false;
+    const double l00 = sqrt(a00);
+    const double l10 = a10 / l00;
+    const double l20 = a20 / l00;
+    const double d11 = a11 - l10 * l10;
+    if (!(d11 > 0.0)) return false;
+    const double l11 = sqrt(d11);
+    const double l21 = (a21 - l20 * l10) / l11;
+    const double d22 = a22 - l20 * l20 - l21 * l21;
+    if (!(d22 > 0.0)) return false;
+    const double l22 = sqrt(d22);
+    const double i00 = 1.0 / l00, i11 = 1.0 / l11, i22 = 1.0 / l22;
+    const double i10 = (-l10 * i00) / l11;
+    const double i20 = (-(l20 * i00) - l21 * i10) / l22;
+    const double i21 = (-l21 * i11) / l22;
+    o[0] = i00 * i00 + i10 * i10 + i20 * i20;
+    o[1] = i10 * i11 + i20 * i21;
+    o[2] = i20 * i22;
+    o[3] = i11 * i11 + i21 * i21;
+    o[4] = i21 * i22;
+    o[5] = i22 * i22;
+    R[0] = l00; R[1] = l10; R[2] = l20; R[3] = l11; R[4] = l21; R[5] = l22;
+    Ri[0] = i00; Ri[1] = i10; Ri[2] = i20; Ri[3] = i11; Ri[4] = i21; Ri[5] = i22;
+    return true;
+}
+
 __device__ __forceinline__ bool spd3_inverse(const double s[6], double o[6]) {
     const double a00 = s[0], a10 = s[1], a20 = s[2], a11 = s[3], a21 = s[4], a22 = s[5];
     if (!(a00 > 0.0)) return false;

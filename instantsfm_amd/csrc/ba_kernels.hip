@@ -36,6 +36,7 @@
 #include "ba_device.h"
 #include "ba_common.h"
 #include "ba_twolevel.h"
+#include "ba_cgp.h"
 #include "ba_gp.h"
 #include "cg_poll.h"
 #include "create_host.h"
@@ -121,35 +122,118 @@ __device__ __forceinline__ double huber_weight_sqrt(double s, double delta) {
 // as one contiguous segment in k_schur); each track reduces V_p = sum J~p^T J~p (packed sym) and g_p = -sum J~p^T r~.
 constexpr int kLinThreads = 128;  // k_lin_points workgroup (LDS: W staging + V/g terms of its observations)
 
-// The first trial's point preparation fused into k_lin_points (the damping factor of a step's first trial is known
-// when the linearization is enqueued: f = 1 + damping): per track the damped V_p (diagonal clamped, times f), its
-// 3x3 inverse and y = V_p^-1 g_p from the same doubles k_point_prep would read back -- bitwise its result -- and the
-// CG status words cleared.  Vinv null: no fusion (retrials, the re-deriving Schur, global positioning).
+// Symmetric camera-point records (round 4).  With R_p the Cholesky factor of point p's damped block at the first
+// trial's damping (V_p,d = R_p R_p^T; f = 1 + damping is known when the linearization is enqueued) and L_p = R_p^-T,
+// L_p L_p^T = V_p,d^-1, so every observation's record is stored as Y_o = W_o L_p (D x 3, [o][3][D] like W) and
+//   S_ij -= sum_p Y_ip Y_jp^T,   b_i -= sum Y_o z_p,  z_p = L_p^T g_p = R_p^-1 g_p:
+// k_schur's first trial needs no per-observation V^-1 loads or W V^-1 products.  A retried trial at another damping
+// factor f' uses M_p = L_p^-1 V'_p^-1 L_p^-T = R_p^T V'_p^-1 R_p (symmetric) between the records and z'_p = R_p^T y'_p
+// (y'_p = V'_p^-1 g_p), formed per point by k_point_prep: the same k_schur with M_p where the GP build has V^-1.
+// The first trial's point preparation itself is fused into k_lin_points: per track the damped V_p (diagonal clamped,
+// times f), its 3x3 inverse (bitwise k_point_prep's: the same Cholesky steps), R_p and z_p, and the CG status words
+// cleared.
 struct PointPrep {
     double f = 1.0, cmin = 0.0, cmax = 0.0;
     double* Vinv = nullptr;
-    double* y = nullptr;
+    double* y = nullptr;   // z_p = R_p^-1 g_p (with R), else y_p = V_p^-1 g_p
+    double* R = nullptr;   // R_p packed (00, 10, 20, 11, 21, 22); null: no records (points-only solves)
     int* flags = nullptr;
     int* status = nullptr;
 };
-__device__ __forceinline__ void point_prep_one(int p, const double V[6], const double g[3], const PointPrep& a) {
+// Returns R_p^-1 (packed) in Ri; all zero when the damped block is not positive definite (flag raised).
+__device__ __forceinline__ void point_prep_first(int p, const double V[6], const double g[3], const PointPrep& a,
+                                                 double Ri[6]) {
     double s[6];
 #pragma unroll
     for (int k = 0; k < 6; ++k) s[k] = V[k];
     s[0] = clampd(s[0], a.cmin, a.cmax) * a.f;
     s[3] = clampd(s[3], a.cmin, a.cmax) * a.f;
     s[5] = clampd(s[5], a.cmin, a.cmax) * a.f;
-    double o[6];
-    if (!spd3_inverse(s, o)) {
+    double o[6], R[6];
+    if (!spd3_factor(s, o, R, Ri)) {
         atomicOr(a.flags, 1);
 #pragma unroll
-        for (int k = 0; k < 6; ++k) o[k] = 0.0;
+        for (int k = 0; k < 6; ++k) o[k] = R[k] = Ri[k] = 0.0;
     }
 #pragma unroll
     for (int k = 0; k < 6; ++k) a.Vinv[6 * (size_t)p + k] = o[k];
-    a.y[3 * (size_t)p + 0] = o[0] * g[0] + o[1] * g[1] + o[2] * g[2];
-    a.y[3 * (size_t)p + 1] = o[1] * g[0] + o[3] * g[1] + o[4] * g[2];
-    a.y[3 * (size_t)p + 2] = o[2] * g[0] + o[4] * g[1] + o[5] * g[2];
+    if (a.R) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) a.R[6 * (size_t)p + k] = R[k];
+        a.y[3 * (size_t)p + 0] = Ri[0] * g[0];
+        a.y[3 * (size_t)p + 1] = Ri[1] * g[0] + Ri[3] * g[1];
+        a.y[3 * (size_t)p + 2] = Ri[2] * g[0] + Ri[4] * g[1] + Ri[5] * g[2];
+    } else {
+        a.y[3 * (size_t)p + 0] = o[0] * g[0] + o[1] * g[1] + o[2] * g[2];
+        a.y[3 * (size_t)p + 1] = o[1] * g[0] + o[3] * g[1] + o[4] * g[2];
+        a.y[3 * (size_t)p + 2] = o[2] * g[0] + o[4] * g[1] + o[5] * g[2];
+    }
+}
+
+// One observation's weighted linearization: the V / g_p terms (cv: V packed sym 6, J~p^T r~ 3) and W_o (w[k * D + a] =
+// (J~c^T J~p)[a][k]).
+template <int M>
+__device__ __forceinline__ void lin_obs(int o, const int* __restrict__ cam, const int* __restrict__ ptl,
+                                        const double* __restrict__ uv, const double* __restrict__ pp,
+                                        const double* __restrict__ cams, const double* __restrict__ pts, double delta,
+                                        double cv[9], double w[3 * kD<M>]) {
+    constexpr int D = kD<M>, ST = kStride<M>;
+    const int c = cam[o], p = ptl[o];
+    const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
+    const double2 z = reinterpret_cast<const double2*>(uv)[o];
+    const double uvo[2] = {z.x, z.y};
+    const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
+    double r[2], Jc[2][D], Jp[2][3];
+    eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
+    const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
+    r[0] *= sw; r[1] *= sw;
+#pragma unroll
+    for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
+    cv[0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
+    cv[1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
+    cv[2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
+    cv[3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
+    cv[4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
+    cv[5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
+#pragma unroll
+    for (int a = 0; a < D; ++a)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
+}
+
+// Y_o = W_o L_p in place (w[k * D + a] as lin_obs), L_p = R_p^-T: Y[a][j] = sum_{k <= j} W[a][k] (R_p^-1)[j][k].
+template <int D>
+__device__ __forceinline__ void y_from_w(double w[3 * D], const double Ri[6]) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) {
+        const double w0 = w[a], w1 = w[D + a], w2 = w[2 * D + a];
+        w[a] = w0 * Ri[0];
+        w[D + a] = w0 * Ri[1] + w1 * Ri[3];
+        w[2 * D + a] = w0 * Ri[2] + w1 * Ri[4] + w2 * Ri[5];
+    }
+}
+
+// Records of observations [base, base + n) from the LDS staging rows (odd stride WRP) to HBM, consecutive lanes storing
+// consecutive 16-B pairs when the record length is even (a pair never crosses a record; every record starts 16-B
+// aligned).
+template <int WR, int WRP>
+__device__ __forceinline__ void store_records(const double* wst, double* __restrict__ Y, int base, int n) {
+    const int t = threadIdx.x;
+    if constexpr ((WR & 1) == 0) {
+        double2* dst = reinterpret_cast<double2*>(Y + (size_t)base * WR);
+        for (int k2 = t; k2 < n * (WR / 2); k2 += kLinThreads) {
+            const int k = 2 * k2, rec = k / WR, e = k - rec * WR;
+            const double* src = wst + rec * WRP + e;
+            dst[k2] = make_double2(src[0], src[1]);
+        }
+    } else {
+        double* dst = Y + (size_t)base * WR;
+        for (int k = t; k < n * WR; k += kLinThreads) dst[k] = wst[(k / WR) * WRP + k % WR];
+    }
 }
 
 template <int M>
@@ -157,73 +241,32 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
                                                          const int* __restrict__ cam, const int* __restrict__ ptl,
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
-                                                         double delta, double* __restrict__ W, double* __restrict__ V,
-                                                         double* __restrict__ gp, PointPrep pp1 = PointPrep{}) {
+                                                         double delta, double* __restrict__ Y, double* __restrict__ V,
+                                                         double* __restrict__ gp, PointPrep pp1) {
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
-    // is longer), one thread per observation: coalesced uv / cam / point loads and 192-B W records written by
-    // consecutive lanes (16 B per lane).  Each observation's V / g_p terms go to LDS and one thread per track adds them
-    // in observation order -- the same sequence of additions as a thread walking its track.  The terms reuse the W
-    // staging area once the records are stored (one 25.6-KB LDS buffer: 6 workgroups per CU instead of 4).
-    constexpr int D = kD<M>, ST = kStride<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride
-    static_assert(WRP >= 9, "the V / g terms reuse a W staging row");
-    __shared__ double wst[kLinThreads * WRP];  // the run's W records, stored coalesced from here; then the V / g terms
+    // is longer), one thread per observation: coalesced uv / cam / point loads.  Each observation's V / g terms go to
+    // LDS and one thread per track adds them in observation order -- the same sequence of additions as a thread walking
+    // its track; that thread then prepares the point (damped V^-1, R_p, z_p) and puts R_p^-1 in LDS, and every
+    // observation turns its W_o (kept in registers) into Y_o, staged in LDS (odd row stride) and stored coalesced in
+    // 16-B pairs (192-B records for D = 8).  A run that is one track longer than the workgroup evaluates its
+    // observations twice (once for the sums, once for the records).  One 25.6-KB LDS buffer serves the terms, the
+    // R_p^-1 table and the record staging (6 workgroups per CU).  Y null (points-only solves): no records.
+    constexpr int D = kD<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride
+    static_assert(WRP >= 9, "the V / g terms reuse a record staging row");
+    __shared__ double wst[kLinThreads * WRP];
     const int t = threadIdx.x;
     const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
     const int ob = pt_ptr[tb], oe = pt_ptr[te];
+    const bool one = oe - ob <= kLinThreads;  // (uniform) the run's observations fit one pass
     double Vs[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
     const int tr = tb + t;  // the track this thread sums (tracks of the run)
     const int tlo = tr < te ? pt_ptr[tr] : 0, thi = tr < te ? pt_ptr[tr + 1] : 0;
+    double w[WR];
     for (int base = ob; base < oe; base += kLinThreads) {
         const int o = base + t;
         double cv[9];
         if (o < oe) {
-            const int c = cam[o], p = ptl[o];
-            const double X[3] = {pts[3 * (size_t)p], pts[3 * (size_t)p + 1], pts[3 * (size_t)p + 2]};
-            const double2 z = reinterpret_cast<const double2*>(uv)[o];
-            const double uvo[2] = {z.x, z.y};
-            const double ppc[2] = {pp[2 * c], pp[2 * c + 1]};
-            double r[2], Jc[2][D], Jp[2][3];
-            eval_obs<M, true>(cams + (size_t)c * ST, X, ppc, uvo, r, Jc, Jp);
-            const double sw = huber_weight_sqrt(r[0] * r[0] + r[1] * r[1], delta);
-            r[0] *= sw; r[1] *= sw;
-#pragma unroll
-            for (int a = 0; a < D; ++a) { Jc[0][a] *= sw; Jc[1][a] *= sw; }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) { Jp[0][k] *= sw; Jp[1][k] *= sw; }
-            cv[0] = Jp[0][0] * Jp[0][0] + Jp[1][0] * Jp[1][0];
-            cv[1] = Jp[0][0] * Jp[0][1] + Jp[1][0] * Jp[1][1];
-            cv[2] = Jp[0][0] * Jp[0][2] + Jp[1][0] * Jp[1][2];
-            cv[3] = Jp[0][1] * Jp[0][1] + Jp[1][1] * Jp[1][1];
-            cv[4] = Jp[0][1] * Jp[0][2] + Jp[1][1] * Jp[1][2];
-            cv[5] = Jp[0][2] * Jp[0][2] + Jp[1][2] * Jp[1][2];
-            {
-                double* Wo = wst + (size_t)t * WRP;
-#pragma unroll
-                for (int a = 0; a < D; ++a)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) Wo[k * D + a] = Jc[0][a] * Jp[0][k] + Jc[1][a] * Jp[1][k];
-            }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) cv[6 + k] = Jp[0][k] * r[0] + Jp[1][k] * r[1];
-        }
-        const int n = min(kLinThreads, oe - base);
-        if constexpr ((WR & 1) == 0) {
-            __syncthreads();
-            // W records of observations [base, base + n) are contiguous in HBM: consecutive lanes store consecutive
-            // 16-B pairs (WR even: a pair never crosses a record, and every record starts 16-B aligned)
-            double2* dst = reinterpret_cast<double2*>(W + (size_t)base * WR);
-            for (int k2 = t; k2 < n * (WR / 2); k2 += kLinThreads) {
-                const int k = 2 * k2, rec = k / WR, e = k - rec * WR;
-                const double* src = wst + rec * WRP + e;
-                dst[k2] = make_double2(src[0], src[1]);
-            }
-        } else {
-            __syncthreads();
-            double* dst = W + (size_t)base * WR;
-            for (int k = t; k < n * WR; k += kLinThreads) dst[k] = wst[(k / WR) * WRP + k % WR];
-        }
-        __syncthreads();
-        if (o < oe) {
+            lin_obs<M>(o, cam, ptl, uv, pp, cams, pts, delta, cv, w);
 #pragma unroll
             for (int k = 0; k < 9; ++k) wst[(size_t)t * 9 + k] = cv[k];
         }
@@ -240,14 +283,61 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
         }
         __syncthreads();
     }
+    double Ri[6];
     if (tr < te) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) V[6 * (size_t)tr + k] = Vs[k];
 #pragma unroll
         for (int k = 0; k < 3; ++k) gp[3 * (size_t)tr + k] = g[k];
-        if (pp1.Vinv) point_prep_one(tr, Vs, g, pp1);  // the first trial's k_point_prep, on the same doubles
+        point_prep_first(tr, Vs, g, pp1, Ri);
+        if (Y) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) wst[(size_t)t * 6 + k] = Ri[k];
+        }
     }
-    if (pp1.Vinv && blockIdx.x == 0 && threadIdx.x < 4) pp1.status[threadIdx.x] = 0;  // (k_point_prep's status clear)
+    if (blockIdx.x == 0 && threadIdx.x < 4) pp1.status[threadIdx.x] = 0;  // (k_point_prep's status clear)
+    if (!Y) return;
+    __syncthreads();
+    if (one) {
+        const int o = ob + t;
+        if (o < oe) {
+            const double* rq = wst + (size_t)(ptl[o] - tb) * 6;
+            double r6[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) r6[k] = rq[k];
+            y_from_w<D>(w, r6);
+        }
+        __syncthreads();  // (every R^-1 read before the staging overwrites the table)
+        if (o < oe) {
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) wst[(size_t)t * WRP + k * D + a] = w[k * D + a];
+        }
+        __syncthreads();
+        store_records<WR, WRP>(wst, Y, ob, oe - ob);
+        return;
+    }
+    // one track longer than the workgroup: its R^-1 from the table, then the records chunk by chunk
+    double r6[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r6[k] = wst[k];
+    __syncthreads();
+    for (int base = ob; base < oe; base += kLinThreads) {
+        const int o = base + t;
+        if (o < oe) {
+            double cv[9];
+            lin_obs<M>(o, cam, ptl, uv, pp, cams, pts, delta, cv, w);
+            y_from_w<D>(w, r6);
+#pragma unroll
+            for (int a = 0; a < D; ++a)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) wst[(size_t)t * WRP + k * D + a] = w[k * D + a];
+        }
+        __syncthreads();
+        store_records<WR, WRP>(wst, Y, base, min(kLinThreads, oe - base));
+        __syncthreads();
+    }
 }
 
 // One workgroup per camera: 256 observations at a time are evaluated (one per thread) into an LDS batch
@@ -426,7 +516,10 @@ __global__ __launch_bounds__(NT) void k_lin_cams_reg(const int* __restrict__ cam
 __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* __restrict__ V, const double* __restrict__ gp,
                                                          double f, double cmin, double cmax, double* __restrict__ Vinv,
                                                          double* __restrict__ y, int* __restrict__ flags,
-                                                         int* __restrict__ status) {
+                                                         int* __restrict__ status, const double* __restrict__ R,
+                                                         double* __restrict__ Mp) {
+    // R non-null (a retried trial on the symmetric records, see PointPrep): M_p = R^T V'^-1 R (packed sym) and
+    // z'_p = R^T y'_p into y; else y'_p = V'^-1 g_p (global positioning's re-prep, points-only solves)
     const int p = blockIdx.x * kThreads + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0;  // the CG status word of this solve
     if (p >= Pl) return;
@@ -448,17 +541,42 @@ __global__ __launch_bounds__(kThreads) void k_point_prep(int Pl, const double* _
     const double y0 = o[0] * g0 + o[1] * g1 + o[2] * g2;
     const double y1 = o[1] * g0 + o[3] * g1 + o[4] * g2;
     const double y2 = o[2] * g0 + o[4] * g1 + o[5] * g2;
-    y[3 * (size_t)p + 0] = y0;
-    y[3 * (size_t)p + 1] = y1;
-    y[3 * (size_t)p + 2] = y2;
+    if (!R) {
+        y[3 * (size_t)p + 0] = y0;
+        y[3 * (size_t)p + 1] = y1;
+        y[3 * (size_t)p + 2] = y2;
+        return;
+    }
+    const double* r = R + 6 * (size_t)p;
+    const double r00 = r[0], r10 = r[1], r20 = r[2], r11 = r[3], r21 = r[4], r22 = r[5];
+    // T = V'^-1 R (columns of R: (r00, r10, r20), (0, r11, r21), (0, 0, r22))
+    const double Rm[3][3] = {{r00, 0.0, 0.0}, {r10, r11, 0.0}, {r20, r21, r22}};
+    const double O[3][3] = {{o[0], o[1], o[2]}, {o[1], o[3], o[4]}, {o[2], o[4], o[5]}};
+    double T[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) T[a][c] = O[a][0] * Rm[0][c] + O[a][1] * Rm[1][c] + O[a][2] * Rm[2][c];
+    double Mq[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) Mq[a][c] = Rm[0][a] * T[0][c] + Rm[1][a] * T[1][c] + Rm[2][a] * T[2][c];
+    double* mo = Mp + 6 * (size_t)p;
+    mo[0] = Mq[0][0]; mo[1] = Mq[0][1]; mo[2] = Mq[0][2]; mo[3] = Mq[1][1]; mo[4] = Mq[1][2]; mo[5] = Mq[2][2];
+    y[3 * (size_t)p + 0] = r00 * y0 + r10 * y1 + r20 * y2;
+    y[3 * (size_t)p + 1] = r11 * y1 + r21 * y2;
+    y[3 * (size_t)p + 2] = r22 * y2;
 }
 
 // ------------------------------------------------------------------------------------------------------------
 // Schur complement: one workgroup per (camera row i, chunk of its upper blocks); the chunk of S's row lives in LDS.
 // A group of D lanes owns one of camera i's observations o (64/D observations in flight per wave); lane b of the
-// group owns column b.  The group forms W^_o = W_o V_p^-1 (row b per lane, shared through LDS), then walks the
-// upper partners q of track p -- tracks are sorted by camera at create, so they are exactly [ustart[o], end) --
-// and adds column b of -W^_o W_q^T into slot(cam[q]) with LDS f64 atomics (ds_add_f64).  Each camera's
+// group owns column b.  The group stages the rows of its own record (row b per lane, shared through LDS) -- the BA's
+// symmetric record Y_o as it is on the first trial, Y_o M_p on a retried one (PointPrep), global positioning's
+// W^_o = W_o V_p^-1 -- then walks the upper partners q of track p -- tracks are sorted by camera at create, so they
+// are exactly [ustart[o], end) -- and adds column b of -Y^_o Y_q^T into slot(cam[q]) with LDS f64 atomics
+// (ds_add_f64).  b_i -= Y_o z_p (z_p, z'_p: PointPrep) alongside.  Each camera's
 // observation list is in point order cut into chunks sorted by partner count (create: the groups of a wave stay
 // balanced, and the rows walk the tracks in step).  The kernel is bound by the
 // chain of dependent loads per round, not by bytes (cache-resident partner data: no faster): every own-observation
@@ -488,7 +606,7 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
     }
 }
 
-template <int D, int WAVES, bool GPW = false>
+template <int D, int WAVES, bool GPW = false, bool RETRY = false>
 __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
@@ -546,8 +664,10 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         // so the W^ staging waits only for the own record while the partner loads stay in flight
         double w0 = 0.0, w1 = 0.0, w2 = 0.0, v00 = 0.0, v01 = 0.0, v02 = 0.0, v11 = 0.0, v12 = 0.0, v22 = 0.0;
         if (has) {
-            const double* vi = Vinv + 6 * (size_t)dcur.y;
-            v00 = vi[0]; v01 = vi[1]; v02 = vi[2]; v11 = vi[3]; v12 = vi[4]; v22 = vi[5];
+            if constexpr (GPW || RETRY) {  // V^-1 (global positioning) or M_p (a retried trial on the Y records)
+                const double* vi = Vinv + 6 * (size_t)dcur.y;
+                v00 = vi[0]; v01 = vi[1]; v02 = vi[2]; v11 = vi[3]; v12 = vi[4]; v22 = vi[5];
+            }
             load_wcol<D, GPW>(W, dcur.x, cb, w0, w1, w2);
         }
         double x[UP][3];
@@ -561,9 +681,15 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             }
         }
         if (has) {
-            my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
-            my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
-            my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
+            if constexpr (GPW || RETRY) {
+                my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
+                my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
+                my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
+            } else {  // the first trial on the Y records: S_ij -= Y_o Y_q^T directly
+                my_wh[cb * 4 + 0] = w0;
+                my_wh[cb * 4 + 1] = w1;
+                my_wh[cb * 4 + 2] = w2;
+            }
             if (diag_chunk) {
                 const double* yp = y + 3 * (size_t)dcur.y;
                 breg -= w0 * yp[0] + w1 * yp[1] + w2 * yp[2];
@@ -1388,7 +1514,10 @@ struct insfm_ba {
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
     // numeric (device)
+    // W: the BA's symmetric records Y_o = W_o L_p (PointPrep; global positioning: its {u, beta^2} records); y: z_p
+    // (BA) / y_p (GP); Rf: R_p of the first trial's damped point blocks; Mp: M_p of a retried trial
     double *W = nullptr, *V = nullptr, *gp = nullptr, *Vinv = nullptr, *y = nullptr, *dp = nullptr;
+    double *Rf = nullptr, *Mp = nullptr;
     double *xbuf = nullptr;  // [S | b | U | gc | scal]
     double *S = nullptr, *b = nullptr, *U = nullptr, *gc = nullptr, *scal = nullptr;
     int64_t xcount = 0;
@@ -1429,6 +1558,14 @@ struct insfm_ba {
     std::vector<int> clab_host;
     size_t erow_lds = 0, pc_lds = 0;
     int pc_rows = 0;  // k_tl_pc rows per restriction pass
+    // the register-resident persistent CG (ba_cgp.h k_tl_cgp): blocks per row (0: not eligible), grid, the w exchange
+    // [C][8], the coarse vector [kCoarseMax], the grid-barrier words; cgp_defer: the side chain of slot cgp_slot is
+    // issued behind the CG (k_tl_cgp holds every SIMD of its CUs, so a chain beside it would crawl on the rest)
+    int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
+    bool cgp_defer = false;
+    double* cgp_trace = nullptr;  // INSFM_DIAG=cgp_trace: [64][4] of the last solve, printed to stderr
+    double *cgp_wx = nullptr, *cgp_yx = nullptr;
+    unsigned* cgp_sync = nullptr;
     // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
     double *Ebuf[2]{}, *Einvbuf[2]{};
     double* gjW = nullptr;  // Gauss-Jordan ping-pong buffer [ldE][ldE]
@@ -1478,6 +1615,10 @@ namespace {
 //   trace         per solve, host microseconds spent enqueueing CG iterations (stderr)
 //   trace2        per LM step, host timestamps of the step's API calls (stderr)
 //   create        host milliseconds of create's phases (stderr)
+//   no_cgp        the two-level CG runs as two launches per iteration (k_tl_pc_cl + k_tl_pspmv) even where the
+//                 persistent register-resident k_tl_cgp is eligible (A/B and parity of the two paths)
+//   cgp_trace     k_tl_cgp records gamma, delta, rho and its stop flag per iteration; printed after each solve
+//   cgp128        k_tl_cgp with 128 register blocks per row even for shorter rows (tests the wide variant)
 bool diag(const char* name) {
     static const std::string v = [] { const char* e = std::getenv("INSFM_DIAG"); return std::string(e ? e : ""); }();
     const size_t n = std::strlen(name);
@@ -1783,10 +1924,26 @@ int lin_join(insfm_ba* h) {
     return 0;
 }
 
+// The first trial's point preparation of a BA linearization (PointPrep): damping factor f = 1 + damping, records Y
+// (and R_p) only when the poses are optimized (points-only solves have no Schur complement).
+PointPrep first_trial_prep(insfm_ba* h) {
+    PointPrep pp1;
+    pp1.f = 1.0 + h->damping;
+    pp1.cmin = h->d.clamp_min;
+    pp1.cmax = h->d.clamp_max;
+    pp1.Vinv = h->Vinv;
+    pp1.y = h->y;
+    pp1.R = h->d.optimize_poses ? h->Rf : nullptr;
+    pp1.flags = h->flags;
+    pp1.status = h->cg.status;
+    return pp1;
+}
+
 template <int M>
-void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local, PointPrep pp1 = PointPrep{}) {
+void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local, const PointPrep& pp1) {
     k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
-                                                         pts_local, h->d.huber_delta, h->W, h->V, h->gp, pp1);
+                                                         pts_local, h->d.huber_delta, pp1.R ? h->W : nullptr, h->V, h->gp,
+                                                         pp1);
 }
 
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
@@ -1801,10 +1958,10 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
         return allreduce(h, h->U, (int64_t)h->C * h->D * h->D + (int64_t)h->C * h->D);
     }
     if (int rc0 = lin_join(h)) return rc0;  // (the previous linearization's U / g_c writes come first)
-    // The first trial's point preparation rides along with k_lin_points: lm_step's first trial runs at
+    // The first trial's point preparation rides along with k_lin_points (PointPrep): lm_step's first trial runs at
     // f = 1 + damping (config 3, same box, 3 runs each: 725 / 722 / 701 -> 733 / 725 / 734 LM it/s against a separate
-    // k_point_prep launch; profiles/r3_v13/prep_fuse_ab.log).
-    PointPrep pp1;
+    // k_point_prep launch; profiles/r3_v13/prep_fuse_ab.log).  The records Y_o depend on it (R_p).
+    const PointPrep pp1 = first_trial_prep(h);
     h->prep_valid = false;
     if (h->kind == 0 && h->Pl > 0) {
         if (h->flags_dirty) {  // a solve without a cost left the flags / status set: clear them first (k_zero_words)
@@ -1812,13 +1969,6 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
             if (int e = launch_err(h, "k_zero_words")) return e;
             h->flags_dirty = false;
         }
-        pp1.f = 1.0 + h->damping;
-        pp1.cmin = h->d.clamp_min;
-        pp1.cmax = h->d.clamp_max;
-        pp1.Vinv = h->Vinv;
-        pp1.y = h->y;
-        pp1.flags = h->flags;
-        pp1.status = h->cg.status;
         h->prep_valid = true;
         h->prep_f = pp1.f;
     }
@@ -1948,7 +2098,10 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
     HIPCHK(hipEventRecord(h->ev_E, h->stream));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
-    if ((rc = issue_side_chain(h, slot))) return rc;
+    // k_tl_cgp under the lag rule: this solve's chain runs after the CG (run_tl_cg); else it runs now and the CG waits
+    h->cgp_defer = h->cgp_nb && use != slot;
+    h->cgp_slot = slot;
+    if (!h->cgp_defer && (rc = issue_side_chain(h, slot))) return rc;
     // a lagged solve's coarse inverse normally finished long ago: a completed event needs no wait marker in the main
     // queue (each one idles it a few us; always queueing it measured 659-665 vs 659-664 LM it/s, round 2)
     if (use == slot || hipEventQuery(h->ev_fact[use]) != hipSuccess)
@@ -1979,9 +2132,27 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
                                                           h->cg, h->tl);
 }
 
+// The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): the setup launches of
+// launch_tl_iter(0), the barrier words cleared, one launch for every iteration.
+int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
+    constexpr int D = 8;
+    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
+                                                               h->tl.Einv);
+    k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
+                                                          h->cg, h->tl);
+    HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->Sn,
+                           h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yx, h->cgp_sync, h->cgp_trace);
+    };
+    if (h->cgp_nb == 64) go(k_tl_cgp<64>);
+    else go(k_tl_cgp<128>);
+    return launch_err(h, "k_tl_cgp");
+}
+
 // k_schur for the handle's kind (BA: template on D; global positioning: D = 3 with the compact W record).
 int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, double smin, double smax, int sdiag,
-                 int w0 = 0, int w1 = -1) {
+                 bool retry, int w0 = 0, int w1 = -1) {
     const bool det = h->d.deterministic != 0;
     if (w1 < 0) w1 = h->nwork;
     const int nt = det ? 64 : kSchurWaves * 64;
@@ -2001,10 +2172,10 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(w1 - w0), dim3(nt), h->schur_lds, h->stream,
                 h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
-                h->W, h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+                h->W, h->Mp, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
         };
-        if (det) go(k_schur<DV, 1>);
-        else go(k_schur<DV, kSchurWaves>);
+        if (det) retry ? go(k_schur<DV, 1, false, true>) : go(k_schur<DV, 1>);
+        else retry ? go(k_schur<DV, kSchurWaves, false, true>) : go(k_schur<DV, kSchurWaves>);
         return launch_err(h, "k_schur");
     });
 }
@@ -2025,6 +2196,7 @@ int run_tl_cg(insfm_ba* h, int* st) {
     int n_enq = 0;
     auto enqueue = [&](int from, int to) -> int {
         const double t0 = htrace ? wall_seconds() : 0.0;
+        if (h->cgp_nb) return from == 0 ? launch_tl_cgp(h, maxit, tol2) : 0;
         const int r = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
@@ -2041,7 +2213,13 @@ int run_tl_cg(insfm_ba* h, int* st) {
     // first batch: a little less than the last solve's count (counts drift by a few iterations per LM step); the loop
     // below tops up one iteration at a time
     int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
+    if (h->cgp_nb) enq = maxit + 2;  // k_tl_cgp: one launch runs every iteration
     if (int rc = enqueue(0, enq)) return rc;
+    if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup)
+        HIPCHK(hipEventRecord(h->ev_E, h->stream));
+        if (int rc = issue_side_chain(h, h->cgp_slot)) return rc;
+        h->cgp_defer = false;
+    }
     CgPoll poll;
     poll.enq = enq;
     static const double stall_s = cg_stall_limit_s(std::getenv("INSFM_CG_STALL_S"));
@@ -2086,8 +2264,16 @@ int run_tl_cg(insfm_ba* h, int* st) {
         HIPCHK(hipStreamSynchronize(h->stream));
         acc_time(h, 8, 9, 5);
     }
-    h->cg_launches += enq;
+    h->cg_launches += h->cgp_nb ? 1 : enq;
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
+    if (h->cgp_nb && h->cgp_trace) {
+        double tr[256];
+        HIPCHK(hipMemcpy(tr, h->cgp_trace, sizeof(tr), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d\n", st[0], st[1], st[2]);
+        for (int k = 0; k <= std::min(st[1], 63); ++k)
+            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g\n", k, tr[4 * k],
+                         tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3]);
+    }
     return 0;
 }
 
@@ -2161,7 +2347,8 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                                                                      h->gpc);
     } else if (h->Pl > 0 && !prepared && (hmark(h, "point_prep"), true))
         k_point_prep<<<cdiv(h->Pl, kThreads), kThreads, 0, h->stream>>>(h->Pl, h->V, h->gp, f, h->d.clamp_min, h->d.clamp_max,
-                                                                       h->Vinv, h->y, h->flags, h->cg.status);
+                                                                       h->Vinv, h->y, h->flags, h->cg.status,
+                                                                       h->d.optimize_poses ? h->Rf : nullptr, h->Mp);
     int iters = 0;
     const double* dcp = nullptr;
     if (h->d.optimize_poses) {
@@ -2172,7 +2359,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             // next chunk's Schur rows are built; b (filled by every row) after the last chunk
             const int K = (int)h->xw.size() - 1;
             for (int c = 0; c < K; ++c) {
-                if ((rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag, h->xw[c], h->xw[c + 1]))) return rc;
+                if ((rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag, !prepared, h->xw[c], h->xw[c + 1]))) return rc;
                 const int64_t b0 = h->rptr_host[h->xr[c]], b1 = h->rptr_host[h->xr[c + 1]];
                 HIPCHK(hipEventRecord(h->ev_x, h->stream));
                 HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
@@ -2183,7 +2370,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
             rec(h, 7);
         } else {
-            rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag);
+            rc = launch_schur(h, Uin, gcin, sf, smin, smax, sdiag, !prepared);
             if (rc) return rc;
             hmark(h, "schur");
             rec(h, 7);
@@ -2213,7 +2400,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         rc = (h->tlon && h->prog_host) ? run_tl_cg(h, st) : run_bj_cg(h, st);
         if (rc) return rc;
         if (st[0] != 1) {
-            h->err = std::string("PCG ") + (st[0] == 2 ? "breakdown" : "did not finish") + " at iteration " +
+            h->err = std::string("PCG ") +
+                     (st[0] == 2 ? "breakdown" : st[0] == 4 ? "grid barrier timed out (k_tl_cgp)" : "did not finish") +
+                     " at iteration " +
                      std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
                      (h->tlon ? std::to_string(st[2]) : std::string("off")) + ")";
             return INSFM_BA_ESOLVER;
@@ -2848,14 +3037,54 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
     }
     tick("block pattern + covisibility");
-    // flattened CG neighbour list per row: upper blocks then lower (transposed) ones; pos_up/pos_lo give each upper
+    if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
+    // ---- two-level preconditioner: clusters ----
+    // Target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
+    // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
+    // While the coarse dimension exceeds kCoarseMax the target grows in proportion to the excess (at least by one),
+    // rounded up to even (aggregates below K / 2 are dissolved: an odd K would keep singletons):
+    // K' = max(K + 1, ceil(K nc MC / kCoarseMax)) rounded up to even, at most C -- the oracle's ora_cluster_cameras.
+    // With K = C the clusters are the co-visibility components: if even those do not fit (more components than
+    // kCoarseMax / MC), the solver runs the block-Jacobi PCG (precond 0) instead.
+    const int MC = D + 1;
+    int nc = 0;
+    bool coarse_ok = false;
+    std::vector<int>& lab = h->clab_host;
+    if (desc->precond == 1 && h->d.optimize_poses) {
+        int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 14, C);
+        nc = aggregate(g, C, K, lab);
+        while (nc * MC > kCoarseMax && K < C) {
+            K = (int)std::min<long long>(C, std::max<long long>(K + 1, ((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));
+            K += K & 1;
+            K = std::min(K, C);
+            nc = aggregate(g, C, K, lab);
+        }
+        coarse_ok = nc * MC <= kCoarseMax;
+    }
+    tick("clusters");
+    // flattened CG neighbour list per row: upper blocks then lower (transposed) ones -- with the two-level
+    // preconditioner each row's list is sorted by (cluster of the neighbour, neighbour), so that a row's
+    // neighbour-cluster segments are contiguous runs of its blocks (the register-resident CG kernel k_tl_cgp walks
+    // them in block order); pos_up/pos_lo give each upper
     // block's two slots in the row-contiguous copy Sn
     std::vector<int> nptr(C + 1, 0), nj, pup(std::max(1, h->nnzb), -1), plo(std::max(1, h->nnzb), -1);
     nj.reserve(2 * (size_t)h->nnzb);
-    for (int i = 0; i < C; ++i) {
-        for (int e = rptr[i] + 1; e < rptr[i + 1]; ++e) { pup[e] = (int)nj.size(); nj.push_back(cols[e]); }
-        for (int k = lop[i]; k < lop[i + 1]; ++k) { plo[loblk[k]] = (int)nj.size(); nj.push_back(locol[k]); }
-        nptr[i + 1] = (int)nj.size();
+    {
+        // per row entries (neighbour j, block e, 0 = upper slot / 1 = lower slot), in cluster order when the coarse
+        // space exists (stable: within a cluster the upper-then-lower order)
+        std::vector<int4> ent;
+        for (int i = 0; i < C; ++i) {
+            ent.clear();
+            for (int e = rptr[i] + 1; e < rptr[i + 1]; ++e) ent.push_back(make_int4(cols[e], e, 0, 0));
+            for (int k = lop[i]; k < lop[i + 1]; ++k) ent.push_back(make_int4(locol[k], loblk[k], 1, 0));
+            if (coarse_ok)
+                std::stable_sort(ent.begin(), ent.end(), [&](const int4& x, const int4& y) { return lab[x.x] < lab[y.x]; });
+            for (const int4& q : ent) {
+                (q.z ? plo : pup)[q.y] = (int)nj.size();
+                nj.push_back(q.x);
+            }
+            nptr[i + 1] = (int)nj.size();
+        }
     }
     // Equal-length rows (every row padded to the longest with zero blocks of neighbour = the row itself) when that
     // costs at most 10 % more slots: the CG's product kernel then derives a row's range from its index instead of
@@ -2866,19 +3095,33 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         for (int i = 0; i < C; ++i) stride = std::max(stride, nptr[i + 1] - nptr[i]);
         const int64_t nn = (int64_t)nj.size();
         if (stride > 0 && nn > 0 && (int64_t)C * stride * 10 <= nn * 11) {
-            std::vector<int> nj2((size_t)C * stride), nptr2(C + 1);
+            // the pad slots of a row (neighbour = the row itself) go behind the row's own-cluster entries when the
+            // list is in cluster order, so that it stays in cluster order; else at the end
+            std::vector<int> nj2((size_t)C * stride), nptr2(C + 1), ins(C);
             for (int i = 0; i < C; ++i) {
+                const int n = nptr[i + 1] - nptr[i], pad = stride - n;
+                int at = n;
+                if (coarse_ok) {
+                    at = 0;
+                    while (at < n && lab[nj[nptr[i] + at]] <= lab[i]) ++at;
+                }
+                ins[i] = at;
                 nptr2[i] = i * stride;
-                for (int q = nptr[i]; q < nptr[i + 1]; ++q) nj2[(size_t)i * stride + (q - nptr[i])] = nj[q];
-                for (int q = nptr[i + 1] - nptr[i]; q < stride; ++q) nj2[(size_t)i * stride + q] = i;
+                int* dst = nj2.data() + (size_t)i * stride;
+                for (int q = 0; q < n; ++q) dst[q < at ? q : q + pad] = nj[nptr[i] + q];
+                for (int q = 0; q < pad; ++q) dst[at + q] = i;
             }
             nptr2[C] = C * stride;
             // remap the Sn slots of every upper block (row i = brow[e] for pos_up, row cols[e] for pos_lo)
+            auto slot = [&](int r, int p) {
+                const int q = p - nptr[r];
+                return r * stride + (q < ins[r] ? q : q + stride - (nptr[r + 1] - nptr[r]));
+            };
             for (int e = 0; e < h->nnzb; ++e) {
                 if (e == rptr[brow[e]]) continue;  // diagonal block: no slot
                 const int i = brow[e], j = cols[e];
-                pup[e] = i * stride + (pup[e] - nptr[i]);
-                plo[e] = j * stride + (plo[e] - nptr[j]);
+                pup[e] = slot(i, pup[e]);
+                plo[e] = slot(j, plo[e]);
             }
             nj.swap(nj2);
             nptr.swap(nptr2);
@@ -2983,6 +3226,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = dd(&h->gp, (size_t)Pl * 3))) return fail(rc, "");
     if ((rc = dd(&h->Vinv, (size_t)Pl * 6))) return fail(rc, "");
     if ((rc = dd(&h->y, (size_t)Pl * 3))) return fail(rc, "");
+    if (kind == 0) {
+        if ((rc = dd(&h->Rf, (size_t)Pl * 6))) return fail(rc, "");
+        if ((rc = dd(&h->Mp, (size_t)Pl * 6))) return fail(rc, "");
+    }
     if ((rc = dd(&h->dp, (size_t)Pl * 3))) return fail(rc, "");
     h->xcount = (int64_t)h->nnzb * D * D + (int64_t)C * D + (int64_t)C * D * D + (int64_t)C * D + 8;
     if ((rc = dd(&h->xbuf, (size_t)h->xcount))) return fail(rc, "");
@@ -3062,6 +3309,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         if constexpr (DV == 3) {
             (void)hipFuncSetAttribute((const void*)k_schur<3, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->schur_lds);
@@ -3073,30 +3324,6 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         return 0;
     });
     tick("uploads + allocations");
-    if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
-    // ---- two-level preconditioner: clusters ----
-    // Target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
-    // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
-    // While the coarse dimension exceeds kCoarseMax the target grows in proportion to the excess (at least by one),
-    // rounded up to even (aggregates below K / 2 are dissolved: an odd K would keep singletons):
-    // K' = max(K + 1, ceil(K nc MC / kCoarseMax)) rounded up to even, at most C -- the oracle's ora_cluster_cameras.
-    // With K = C the clusters are the co-visibility components: if even those do not fit (more components than
-    // kCoarseMax / MC), the solver runs the block-Jacobi PCG (precond 0) instead.
-    const int MC = D + 1;
-    int nc = 0;
-    bool coarse_ok = false;
-    std::vector<int>& lab = h->clab_host;
-    if (desc->precond == 1 && h->d.optimize_poses) {
-        int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 14, C);
-        nc = aggregate(g, C, K, lab);
-        while (nc * MC > kCoarseMax && K < C) {
-            K = (int)std::min<long long>(C, std::max<long long>(K + 1, ((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));
-            K += K & 1;
-            K = std::min(K, C);
-            nc = aggregate(g, C, K, lab);
-        }
-        coarse_ok = nc * MC <= kCoarseMax;
-    }
     if (coarse_ok) {
         // ---- two-level preconditioner: source lists of E, buffers ----
         const int m = nc * MC;
@@ -3279,6 +3506,38 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             void* dp = nullptr;
             if (hipHostGetDevicePointer(&dp, pm, 0) == hipSuccess) h->cg.prog = static_cast<int*>(dp);
             else { (void)hipHostFree(pm); h->prog_host = nullptr; }
+        }
+        // the persistent register-resident CG (ba_cgp.h): D = 8, atomic cluster sums, host-mapped progress, rows of
+        // at most NB = 128 blocks in cluster order, at most kCgpSegMax neighbour clusters per row, and the whole grid
+        // resident at once
+        int maxlen = 0;
+        for (int i = 0; i < C; ++i) maxlen = std::max(maxlen, nptr[i + 1] - nptr[i]);
+        bool in_order = true;
+        for (int64_t q = 0; q < h->n_nbr && in_order; ++q) in_order = sperm[q] == q;
+        const int nb = (maxlen <= 64 && !diag("cgp128")) ? 64 : maxlen <= 128 ? 128 : 0;
+        const int grid = (C + kCgpRows - 1) / kCgpRows;
+        if (diag("create"))
+            std::fprintf(stderr, "[insfm create] k_tl_cgp eligibility: D %d, atomic sums %d, progress %d, max row %d, "
+                         "cluster order %d, max segments %d\n", D, tl.Racc != nullptr, h->prog_host != nullptr, maxlen,
+                         (int)in_order, maxseg);
+        if (D == 8 && tl.Racc && h->prog_host && nb && in_order && maxseg <= kCgpSegMax && !diag("no_cgp")) {
+            int dev = 0, ncu = 0, per_cu = 0;
+            hipError_t ce = hipGetDevice(&dev);
+            if (ce == hipSuccess) ce = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+            if (ce == hipSuccess)
+                ce = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &per_cu, nb == 64 ? (const void*)k_tl_cgp<64> : (const void*)k_tl_cgp<128>, kCgpThreads, 0);
+            if (ce == hipSuccess && per_cu >= 1 && grid <= ncu) {
+                if ((rc = dd(&h->cgp_wx, cd))) return fail(rc, "");
+                if ((rc = dd(&h->cgp_yx, (size_t)kCoarseMax))) return fail(rc, "");
+                if ((rc = dalloc(h, (void**)&h->cgp_sync, sizeof(unsigned) * kCgpSyncWords))) return fail(rc, "");
+                if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, 256))) return fail(rc, "");
+                h->cgp_nb = nb;
+                h->cgp_grid = grid;
+                if (diag("create"))
+                    std::fprintf(stderr, "[insfm create] k_tl_cgp<%d>: %d workgroups, %d CUs, %d per CU\n", nb, grid, ncu,
+                                 per_cu);
+            }
         }
     }
     tick("two-level setup (end)");
@@ -3476,7 +3735,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 5 && h->kind == 0 && h->W) {  // k_lin_points at the last trial's parameters
                 with_model(h->model, [&](auto mc) -> int {
                     constexpr int M = decltype(mc)::value;
-                    if (h->Pl > 0) launch_lin_points_w<M>(h, h->cams_new, h->pts_new);
+                    if (h->Pl > 0) launch_lin_points_w<M>(h, h->cams_new, h->pts_new, first_trial_prep(h));
                     return 0;
                 });
             } else if (which == 0)
@@ -3487,7 +3746,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 h->d.deterministic = 0;
                 const int rc2 = launch_schur(h, h->kind ? h->Up : h->U, h->kind ? h->gpc : h->gc, 1.0,
                                              h->kind ? -1e308 : h->d.clamp_min, h->kind ? 1e308 : h->d.clamp_max,
-                                             h->kind ? 1 : h->d.rank == 0);
+                                             h->kind ? 1 : h->d.rank == 0, false);
                 h->d.deterministic = det;
                 if (rc2) return rc2;
             }

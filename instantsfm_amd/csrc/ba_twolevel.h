@@ -427,6 +427,44 @@ __device__ bool gj_invert_block(double (*M)[kGS]) {
     }
     __syncthreads();
     return bad;
+#elif GJ_PINV == 5
+    // one wave, the layout of variant 4 (lane l: row l & 31, columns 16 (l >> 5) .. +15), the pivot row and column
+    // exchanged by lane permutes (ds_bpermute) instead of LDS stores, a fence and loads: per pivot p every lane reads
+    // the pivot row's entries of its column half from lane p + 32 h and its row's pivot-column entry from lane
+    // r + 32 (p >> 4); the same arithmetic in the same order as variants 3 and 4.
+    static_assert(kGB == 32, "64 lanes = 32 rows x 2 column halves");
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, r = l & 31, h = l >> 5, cb = 16 * h;
+        double a[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = M[r][cb + j];
+#pragma unroll
+        for (int p = 0; p < kGB; ++p) {
+            const int hp = p >> 4, jp = p & 15;
+            double pr[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) pr[j] = __shfl(a[j], p + 32 * h, 64);
+            const double aip = __shfl(a[jp], r + 32 * hp, 64);
+            double piv = readlane_d(a[jp], p + 32 * hp);
+            if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+            const double inv = 1.0 / piv;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (cb + j == p) {
+                    a[j] = (r == p) ? inv : -aip * inv;
+                } else {
+                    const double rpc = pr[j] * inv;
+                    a[j] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) M[r][cb + j] = a[j];
+    }
+    __syncthreads();
+    return bad;
 #elif GJ_PINV == 1
     __shared__ __attribute__((aligned(16))) double prow[kGB];
     __syncthreads();

@@ -228,7 +228,13 @@ static PyObject* finish(PyObject* self, PyObject* args) {
                     keep = z > 0.1;
                 }
                 ok[k] = keep;
-                if (keep) { pc[im] = 1; pp[tid[k]] = 1; ++c; }
+                /* the flags are written only when not yet set: every thread marks the same ~1000 image bytes, and
+                 * unconditional stores would ping-pong their cache lines between cores */
+                if (keep) {
+                    if (!pc[im]) pc[im] = 1;
+                    if (!pp[tid[k]]) pp[tid[k]] = 1;
+                    ++c;
+                }
             }
             cnt[t + 1] = c;
         }

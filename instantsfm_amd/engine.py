@@ -189,6 +189,10 @@ class BundleAdjuster:
         except Exception:
             pass
 
+    def last_error(self):
+        """The handle's last error message (e.g. why a step reported ``failed``)."""
+        return _capi.load().insfm_ba_last_error(self._h).decode() if getattr(self, "_h", None) is not None else ""
+
     def _ptr(self, t, shape):
         if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()):
             raise ValueError("parameters must be contiguous float64 tensors on the GPU")

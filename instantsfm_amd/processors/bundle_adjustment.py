@@ -137,10 +137,18 @@ class PackedProblem:
         return self.indices_i32
 
 
-def pack(cameras, images, tracks, options, native=True):
+def pack(cameras, images, tracks, options, native=True, phases=None):
     """Vectorized restatement of bundle_adjustment.py:66-113.  With the native extension (csrc/packx.c) the per-Track
     reads and the per-observation filtering run in C on all host cores; ``native=False`` (or Track attributes that are
-    not plain ndarrays) takes the numpy path, which gives the same arrays (tests/test_packing.py checks both)."""
+    not plain ndarrays) takes the numpy path, which gives the same arrays (tests/test_packing.py checks both).
+    ``phases``: a dict that receives the wall seconds of the native path's parts (keys, collect, images, features,
+    finish, outputs)."""
+    tp = [time.perf_counter()]
+
+    def mark(name):
+        if phases is not None:
+            tp.append(time.perf_counter())
+            phases[name] = tp[-1] - tp[-2]
     model = cameras[0].model_id  # :45 "assume all cameras are under the same model"
     info = get_camera_model_info(model)
     if model.value not in IMPLEMENTED_MODELS:
@@ -148,7 +156,9 @@ def pack(cameras, images, tracks, options, native=True):
     min_len = options['min_num_view_per_track']
     track_keys = list(tracks.keys())
     track_vals = list(tracks.values())
+    mark("keys")
     got = packx().collect(track_vals, int(min_len)) if (native and packx() is not None) else None
+    mark("collect")
     if got is not None:
         lengths = np.frombuffer(got[0], np.int64)
         obs_valid = np.frombuffer(got[1], np.int64).reshape(-1, 2)
@@ -176,22 +186,27 @@ def pack(cameras, images, tracks, options, native=True):
     remaining = np.array([i for i in range(camera_params.shape[1]) if i not in pp_indices])
     camera_pps = camera_params[:, pp_indices]
     camera_params = camera_params[:, remaining]
+    mark("images")
     feats = [np.asarray(im.features).reshape(-1, 2) for im in images]
     foff = np.concatenate([[0], np.cumsum([f.shape[0] for f in feats])]).astype(np.int64)
     feat_all = np.ascontiguousarray(np.concatenate(feats), dtype=np.float64) if feats else np.zeros((0, 2))
     if got is not None:
         # :85-113 in C: registered filter, feature gather, cheirality z > 0.1, torch.unique compaction
         cp = np.ascontiguousarray(camera_params)
+        mark("features")
         r = packx().finish(obs_valid, lengths, int(min_len), registered.astype(np.uint8), feat_all, foff,
                           np.ascontiguousarray(points_3d), cp, cp.shape[1])
+        mark("finish")
         points_2d = np.frombuffer(r[0], np.float64).reshape(-1, 2)
         cam_inv, pt_inv = np.frombuffer(r[1], np.int64), np.frombuffer(r[2], np.int64)
         unique_cameras, unique_points = np.frombuffer(r[3], np.int64), np.frombuffer(r[4], np.int64)
-        return PackedProblem(model, points_2d, cam_inv, pt_inv, np.ascontiguousarray(camera_pps[unique_cameras]),
-                             np.ascontiguousarray(camera_params[unique_cameras]),
-                             np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points,
-                             track_keys, remaining, pp_indices, track_vals,
-                             (np.frombuffer(r[5], np.int32), np.frombuffer(r[6], np.int32)))
+        out = PackedProblem(model, points_2d, cam_inv, pt_inv, np.ascontiguousarray(camera_pps[unique_cameras]),
+                            np.ascontiguousarray(camera_params[unique_cameras]),
+                            np.ascontiguousarray(points_3d[unique_points]), unique_cameras, unique_points,
+                            track_keys, remaining, pp_indices, track_vals,
+                            (np.frombuffer(r[5], np.int32), np.frombuffer(r[6], np.int32)))
+        mark("outputs")
+        return out
     try:
         points_3d = np.concatenate(xyz).astype(np.float64, copy=False).reshape(-1, 3)
         if points_3d.shape[0] != len(xyz):
@@ -272,9 +287,10 @@ class TorchBA:
         steps, write-back) and the step count."""
         opts = BUNDLE_ADJUSTER_OPTIONS
         t0 = time.perf_counter()
-        packed = pack(cameras, images, tracks, opts)
+        phases = {}
+        packed = pack(cameras, images, tracks, opts, phases=phases)
         t1 = time.perf_counter()
-        self.timings = dict(pack_s=t1 - t0, create_s=0.0, steps_s=0.0, update_s=0.0, total_s=t1 - t0, steps=0,
+        self.timings = dict(pack_s=t1 - t0, pack_phases=phases, create_s=0.0, steps_s=0.0, update_s=0.0, total_s=t1 - t0, steps=0,
                             n_cams=int(packed.camera_params.shape[0]), n_points=int(packed.points_3d.shape[0]),
                             n_obs=int(packed.points_2d.shape[0]))
         if packed.points_2d.shape[0] == 0:
@@ -324,8 +340,11 @@ class TorchBA:
         self.loss_history = loss_history
         t3 = time.perf_counter()
         self.final_loss, self.final_rmse = eng.cost(cams_t, pts_t)
+        t3a = time.perf_counter()
         update(cameras, images, tracks, packed, cams_t, pts_t)
+        t3b = time.perf_counter()
         eng.close()
         t4 = time.perf_counter()
         self.timings.update(create_s=t2 - t1, steps_s=t3 - t2, update_s=t4 - t3, total_s=t4 - t0,
+                            update_phases=dict(cost=t3a - t3, write_back=t3b - t3a, close=t4 - t3b),
                             steps=len(loss_history), final_rmse=self.final_rmse)

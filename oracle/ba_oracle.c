@@ -294,6 +294,10 @@ typedef struct {
     double delta, radius0, rmax, rmin, up, down0, factor, high, low, cmin, cmax, pcg_tol;
     int max_rejects, pcg_max_iter, optimize_poses;
     int precond, cluster_size;   /* 0 block-Jacobi, 1 two-level (block-Jacobi + camera-cluster similarity coarse space) */
+    /* summation-order perturbation (test yardstick, 0 = off): order_seed != 0 visits each camera row's observations
+     * in ora_schur in a seeded pseudo-random order (the same terms summed in another order, as the GPU's LDS-atomic
+     * row accumulation does); order_mode bit 1 also sums the PCG's dot products in reverse chunk order */
+    int order_seed, order_mode;
     int *clab, nclust;           /* cluster label per camera, number of clusters */
     int *csize;                  /* cameras per cluster */
     double* lin_cams;            /* copy of the linearization point (coarse basis) */
@@ -315,22 +319,29 @@ typedef struct {
     double stats[8];
 } ora_t;
 
-static double det_sum(const double* v, size_t n) {
-    /* deterministic sum: fixed chunks, partial sums in order */
+static double det_sum_order(const double* v, size_t n, int reverse) {
+    /* deterministic sum: fixed chunks, partial sums in order (reverse: chunks and their elements backwards) */
     size_t nch = (n + CHUNK - 1) / CHUNK;
     double* part = (double*)malloc((nch ? nch : 1) * sizeof(double));
     #pragma omp parallel for schedule(static)
     for (long c = 0; c < (long)nch; ++c) {
         double s = 0;
         size_t e = (c + 1) * (size_t)CHUNK; if (e > n) e = n;
-        for (size_t i = (size_t)c * CHUNK; i < e; ++i) s += v[i];
+        if (reverse)
+            for (size_t i = e; i-- > (size_t)c * CHUNK;) s += v[i];
+        else
+            for (size_t i = (size_t)c * CHUNK; i < e; ++i) s += v[i];
         part[c] = s;
     }
     double s = 0;
-    for (size_t c = 0; c < nch; ++c) s += part[c];
+    if (reverse)
+        for (size_t c = nch; c-- > 0;) s += part[c];
+    else
+        for (size_t c = 0; c < nch; ++c) s += part[c];
     free(part);
     return s;
 }
+static double det_sum(const double* v, size_t n) { return det_sum_order(v, n, 0); }
 
 static int cmp_int(const void* a, const void* b) { int x = *(const int*)a, y = *(const int*)b; return (x > y) - (x < y); }
 
@@ -518,6 +529,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     h->cmax = dopt[10]; h->pcg_tol = dopt[11];
     h->max_rejects = iopt[0]; h->pcg_max_iter = iopt[1]; h->optimize_poses = iopt[2];
     h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 14;
+    h->order_seed = iopt[6]; h->order_mode = iopt[7];
 #ifdef _OPENMP
     if (iopt[3] > 0) omp_set_num_threads(iopt[3]);
 #endif
@@ -753,8 +765,20 @@ void ora_schur(ora_t* h, double f) {
             memset(Srow, 0, sizeof(double) * (size_t)(re - rb) * D * D);
             double bi[MAXD];
             for (int a = 0; a < D; ++a) bi[a] = h->gc[(size_t)i * D + a];
-            for (int e = h->cam_ptr[i]; e < h->cam_ptr[i + 1]; ++e) {
-                int o = h->cam_obs[e], p = h->pt[o];
+            const int eb = h->cam_ptr[i], ne = h->cam_ptr[i + 1] - eb;
+            int* perm = NULL;
+            if (h->order_seed && ne > 1) {  /* seeded Fisher-Yates over the row's observations (test yardstick) */
+                perm = (int*)malloc(sizeof(int) * (size_t)ne);
+                for (int k = 0; k < ne; ++k) perm[k] = k;
+                unsigned long long st = 0x9E3779B97F4A7C15ull * (unsigned long long)(h->order_seed * 1000003LL + i + 1);
+                for (int k = ne - 1; k > 0; --k) {
+                    st ^= st >> 12; st ^= st << 25; st ^= st >> 27;
+                    const int r = (int)((st * 0x2545F4914F6CDD1Dull) % (unsigned long long)(k + 1));
+                    const int tmp = perm[k]; perm[k] = perm[r]; perm[r] = tmp;
+                }
+            }
+            for (int e = eb; e < eb + ne; ++e) {
+                int o = h->cam_obs[perm ? eb + perm[e - eb] : e], p = h->pt[o];
                 const double* Wo = h->W + (size_t)o * D * 3;
                 const double* Vi = h->Vinv + 9 * (size_t)p;
                 const double* yp = h->y + 3 * (size_t)p;
@@ -773,6 +797,7 @@ void ora_schur(ora_t* h, double f) {
                             blk[a * D + bb] -= Wh[a * 3 + 0] * Wq[bb * 3 + 0] + Wh[a * 3 + 1] * Wq[bb * 3 + 1] + Wh[a * 3 + 2] * Wq[bb * 3 + 2];
                 }
             }
+            free(perm);
             /* + U_i with clamped, damped diagonal */
             const double* Ui = h->U + (size_t)i * D * D;
             for (int a = 0; a < D; ++a)
@@ -818,9 +843,10 @@ static void spmv_scaled(ora_t* h, const double* v, double* w) {
     }
 }
 
+static int g_dot_reverse = 0;  /* set per solve from order_mode bit 1 (test yardstick) */
 static double dot(const double* a, const double* b, size_t n, double* tmp) {
     for (size_t i = 0; i < n; ++i) tmp[i] = a[i] * b[i];
-    return det_sum(tmp, n);
+    return det_sum_order(tmp, n, g_dot_reverse);
 }
 
 /* Cholesky S_ii = L L^T (D x D, lower, row-major).  Returns -1 if not positive definite. */
@@ -1051,6 +1077,7 @@ static void coarse_apply(ora_t* h, const double* Zt, const double* Einv, double*
  * S is scaled in place.  Returns iterations >= 0, or -1 on breakdown (solver failure). */
 int ora_pcg(ora_t* h, double* xout) {
     int D = h->D, C = h->C;
+    g_dot_reverse = (h->order_mode & 2) != 0;
     size_t n = (size_t)C * D;
     size_t DD = (size_t)D * D;
     int bad = 0;

@@ -123,7 +123,8 @@ def retract_pose(x7, d6):
 
 DEFAULTS = dict(huber_delta=1.0, tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4,
                 tr_factor=0.25, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
-                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=14)
+                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=14,
+                order_seed=0, order_mode=0)
 
 
 class OracleBA:
@@ -143,7 +144,7 @@ class OracleBA:
         dopt = np.array([o['huber_delta'], o['tr_radius'], o['tr_max'], o['tr_min'], o['tr_up'], o['tr_down'],
                          o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
         iopt = np.array([o['max_rejects'], o['pcg_max_iter'], o['optimize_poses'], o['threads'], o['precond'],
-                         o['cluster_size']], np.int32)
+                         o['cluster_size'], o['order_seed'], o['order_mode']], np.int32)
         self.h = self.L.ora_create(self.model, self.C, self.P, self.N, _d(self.uv), _i(self.cam), _i(self.pt),
                                   _d(self.pp), _d(dopt), _i(iopt))
         if not self.h:
@@ -256,7 +257,7 @@ class OracleGP:
         self.D = 3
         dopt = np.array([o['huber_delta'], o['tr_radius'], o['tr_max'], o['tr_min'], o['tr_up'], o['tr_down'],
                          o['tr_factor'], o['tr_high'], o['tr_low'], o['clamp_min'], o['clamp_max'], o['pcg_tol']])
-        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], 1, o['threads'], o['precond'], o['cluster_size']],
+        iopt = np.array([o['max_rejects'], o['pcg_max_iter'], 1, o['threads'], o['precond'], o['cluster_size'], 0, 0],
                         np.int32)
         self.h = self.L.ora_gp_create(self.C, self.P, self.N, _d(self.t), _i(self.cam), _i(self.pt), _d(self.fcam),
                                      _i(self.sfree), _d(dopt), _i(iopt))

@@ -38,6 +38,21 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
 
 
+def y_records(ora, pt_idx, f, clamp_min=1e-6, clamp_max=1e32):
+    """The oracle's W_o turned into the GPU's stored records Y_o = W_o R_p^-T, R_p = chol(V_p damped by f)."""
+    Wo = ora.get(O.W)                        # [N, D, 3]
+    Vp = ora.get(O.V)                        # [P, 6] packed (xx xy xz yy yz zz)
+    full = np.empty((Vp.shape[0], 3, 3))
+    idx = [(0, 0, 0), (1, 0, 1), (2, 0, 2), (3, 1, 1), (4, 1, 2), (5, 2, 2)]
+    for k, a, b in idx:
+        full[:, a, b] = full[:, b, a] = Vp[:, k]
+    for a in range(3):
+        full[:, a, a] = np.clip(full[:, a, a], clamp_min, clamp_max) * f
+    R = np.linalg.cholesky(full)
+    Ri = np.linalg.inv(R)
+    return np.einsum("oak,ojk->oaj", Wo, Ri[np.asarray(pt_idx)])
+
+
 @pytest.mark.parametrize("model", MODELS)
 def test_linearize_parity(model):
     prob = make_problem(24, 600, seed=11, model=model)
@@ -45,7 +60,9 @@ def test_linearize_parity(model):
     eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
     ora.linearize(prob.cams_init, prob.points_init)
     N, P, C, D = prob.n_obs, prob.n_points, prob.n_cams, eng.D
-    assert rel(eng.debug_get(0, (N, 3, D)).transpose(0, 2, 1), ora.get(O.W)) < 1e-12  # stored [o][3][D]
+    # the stored records are the symmetric Y_o = W_o L_p (PointPrep in csrc/ba_kernels.hip): L_p = R_p^-T with R_p the
+    # Cholesky factor of the point block damped for the first trial (f = 1 + damping = 1 + 1e-4), stored [o][3][D]
+    assert rel(eng.debug_get(0, (N, 3, D)).transpose(0, 2, 1), y_records(ora, prob.pt_idx, 1.0 + 1e-4)) < 1e-12
     assert rel(eng.debug_get(1, (P, 6)), ora.get(O.V)) < 1e-12
     assert rel(eng.debug_get(2, (P, 3)), ora.get(O.GP)) < 1e-12
     assert rel(eng.debug_get(3, (C, D, D)), ora.get(O.U)) < 1e-10
@@ -268,48 +285,58 @@ def test_repeated_solves_lagged_coarse_inverse(model, det):
     """Consecutive solves on one engine under the lag rule: the first solve after a linearization runs with the coarse
     inverse of the previous solve (factorized on the side stream while that CG ran), retries at the same
     linearization use their own.  Every solve matches the oracle's (same rule): iterations, and dc in residual space
-    (||S (dc_gpu - dc_oracle)|| / ||b|| <= 1e-9, 4 decades inside the PCG's 1e-5 tolerance; 1e-8 for the lagged D = 16
-    solves) and in the energy norm (<= 1e-6; 1e-5 there); max-abs 1e-8 for own-E solves and 1e-6 for lagged ones with
-    D <= 12.  The coarse sizes here
-    (m = 45 / 65 / 85) end in a partial dense block.
+    (||S (dc_gpu - dc_oracle)|| / ||b||), energy norm and max-abs.  The coarse sizes here (m = 45 / 65 / 85) end in a
+    partial dense block.
 
-    FULL_OPENCV (D = 16) at k = 0 has exactly dependent distortion columns (k1..k3 vs k4..k6), held apart only by
-    the damping: cond(S) ~ 5e13, and a lagged solve's max-abs difference is set by rounding, not by the algorithm --
-    the oracle against itself built with other rounding moves 4e-6 there while agreeing to 1.6e-11 in residual space
-    (tests/test_oracle.py::test_pcg_rounding_sensitivity_lives_in_the_near_null_space).  So for D = 16 lagged solves
-    the residual-space and energy bounds are the parity check (max-abs is reported).  In the default mode the Schur
-    build's LDS-atomic order varies from run to run, and so does that residual: 27 runs of this test on the MI355X
-    (profiles/r3_v8/lag_*.log) gave 1e-10 .. 1.3e-8 for the lagged D = 16 solves (energy <= 1.2e-6), hence 5e-8
-    there; deterministic=1 (fixed-order sums) pins the same solves at the 1e-8 bound."""
+    The bound of each solve is derived in the test, not fitted: the oracle is re-run with the Schur row sums taken in
+    other orders (order_seed 1..3: each camera row's observations in a seeded permutation; order_mode 2: the PCG's dot
+    products in reverse order) -- the same arithmetic, only the summation order moved, which is what the GPU's
+    LDS-atomic row accumulation (and, in deterministic mode, its own fixed order) does.  The GPU must stay within 10x
+    the largest spread of those re-runs from the oracle, or within the fixed tolerances below where that spread is
+    smaller (resid 1e-9, energy 1e-6, max-abs 1e-8 for own-E solves and 1e-6 for lagged ones).  For FULL_OPENCV
+    (D = 16) at k = 0 the distortion columns k1..k3 and k4..k6 are exactly dependent, held apart only by the damping
+    (cond(S) ~ 5e13): there the order re-runs alone move a lagged solve by ~3e-9 in residual space and ~7e-5 in
+    max-abs, which is the bound's scale."""
     prob = make_problem(30, 800, seed=5, model=model)
     cams, pts = prob.cams_init.copy(), prob.points_init.copy()
-    ref = O.OracleBA(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
+    args = (prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
+    ref = O.OracleBA(*args)
     ref.linearize(cams, pts)
+    seq = [(1, 1 + 1e-4), (1, 1 + 5e-5), (1, 1 + 8e-4), (0, 1 + 1.3e-2), (0, 1.2), (1, 1 + 6e-4)]
+    # the oracle and its summation-order re-runs on the same sequence: per solve, the spread of the re-runs
+    base = O.OracleBA(*args, cluster_size=6)
+    pert = [O.OracleBA(*args, cluster_size=6, order_seed=sd, order_mode=2) for sd in (1, 2, 3)]
+    dc_ora, spread = [], []
+    for relin, f in seq:
+        if relin:
+            for o in [base] + pert:
+                o.linearize(cams, pts)
+        it = base.solve(f)
+        assert all(o.solve(f) == it for o in pert)
+        S, b = O.dense_reduced(ref, f)
+        dref = base.get(O.DC)
+        dc_ora.append(dref)
+        ds = [O.solve_differences(S, b, o.get(O.DC), dref) for o in pert]
+        spread.append({q: max(d[q] for d in ds) for q in ("resid", "energy", "max")})
     for rep in range(3):
         eng, ora = engines(prob, cluster_size=6, deterministic=det)
-        # (relinearize?, damping factor): LM-like sequences -- fresh trials change f by <= 16x, retries by more
-        for k, (relin, f) in enumerate([(1, 1 + 1e-4), (1, 1 + 5e-5), (1, 1 + 8e-4), (0, 1 + 1.3e-2), (0, 1.2),
-                                        (1, 1 + 6e-4)]):
+        for k, (relin, f) in enumerate(seq):
             if relin:
                 eng.debug_linearize(dev(cams), dev(pts))
                 ora.linearize(cams, pts)
             it_g = eng.debug_solve(f)
             it_o = ora.solve(f)
             assert it_g == it_o, (rep, k, it_g, it_o)
+            assert np.array_equal(ora.get(O.DC), dc_ora[k])  # (the oracle is deterministic)
             dc_g = eng.debug_get(7, (prob.n_cams, eng.D))
             S, b = O.dense_reduced(ref, f)
-            d = O.solve_differences(S, b, dc_g, ora.get(O.DC))
-            print(f"model {model} rep {rep} solve {k}: {d}")
+            d = O.solve_differences(S, b, dc_g, dc_ora[k])
             lagged = relin and k > 0
-            if lagged and eng.D == 16:
-                # the oracle against its own FMA-contracted build: 1.6e-11 / 2.6e-8 (see the docstring)
-                assert d["resid"] < (1e-8 if det else 5e-8) and d["energy"] < 1e-5, (rep, k, d)
-            else:
-                assert d["resid"] < 1e-9 and d["energy"] < 1e-6, (rep, k, d)
-            if not lagged:
-                assert d["max"] < 1e-8, (rep, k, d)
-            elif eng.D <= 12:
-                assert d["max"] < 1e-6, (rep, k, d)
+            bound = {"resid": max(1e-9, 10 * spread[k]["resid"]), "energy": max(1e-6, 10 * spread[k]["energy"]),
+                     "max": max(1e-6 if lagged else 1e-8, 10 * spread[k]["max"])}
+            print(f"model {model} det {det} rep {rep} solve {k}: {d}; order spread {spread[k]}")
+            for q in ("resid", "energy", "max"):
+                assert d[q] < bound[q], (rep, k, q, d, spread[k])
         eng.close()
 
 

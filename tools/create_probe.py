@@ -31,7 +31,8 @@ def main():
     torch.zeros(1, device=dev)
     for r in range(a.reps):
         t0 = time.perf_counter()
-        pk = BA.pack(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)
+        ph = {}
+        pk = BA.pack(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS, phases=ph)
         t1 = time.perf_counter()
         cam32, pt32 = pk.indices32()
         eng = BundleAdjuster(pk.model.value, pk.points_2d, cam32, pt32, pk.camera_pps,
@@ -47,7 +48,8 @@ def main():
         eng.close()
         t6 = time.perf_counter()
         print(f"rep {r}: pack {1e3 * (t1 - t0):.1f} ms, create {1e3 * (t2 - t1):.1f}, params H2D {1e3 * (t3 - t2):.1f}, "
-              f"1 step {1e3 * (t4 - t3):.1f}, update {1e3 * (t5 - t4):.1f}, close {1e3 * (t6 - t5):.1f}", flush=True)
+              f"1 step {1e3 * (t4 - t3):.1f}, update {1e3 * (t5 - t4):.1f}, close {1e3 * (t6 - t5):.1f}; pack phases "
+              + ", ".join(f"{k} {1e3 * v:.1f}" for k, v in ph.items()), flush=True)
 
 
 if __name__ == "__main__":

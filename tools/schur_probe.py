@@ -22,7 +22,8 @@ if os.environ.get("REORDER"):
     prob.uv, prob.cam_idx, prob.pt_idx = prob.uv[order], prob.cam_idx[order], newpt[order].astype(np.int32)
     prob.points_init = prob.points_init[perm].copy()
 dev = torch.device("cuda:0")
-eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev)
+eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
+                     deterministic=bool(os.environ.get("DET")))  # DET=1: the order-fixed one-wave-per-row k_schur
 cams = torch.from_numpy(prob.cams_init).to(dev)
 pts = torch.from_numpy(prob.points_init).to(dev)
 for _ in range(2):
@@ -33,5 +34,5 @@ losses = [eng.step(cams, pts)[0] for _ in range(8)]
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / 8
 us = eng.debug_time_kernel(1, 20)
-print(f"{os.path.basename(os.environ.get('INSFM_LIB', 'default'))}: k_schur {us:.1f} us, step {dt*1e3:.3f} ms, "
+print(f"{os.path.basename(os.environ.get('INSFM_LIB', 'default'))}{' det' if os.environ.get('DET') else ''}: k_schur {us:.1f} us, step {dt*1e3:.3f} ms, "
       f"loss {losses[-1]:.10e}", flush=True)
