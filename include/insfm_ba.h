@@ -134,6 +134,22 @@ int insfm_ba_cost(insfm_ba* h, const double* cam_params, const double* points, d
 int64_t insfm_ba_exchange_count(const insfm_ba* h);
 int insfm_ba_set_exchange(insfm_ba* h, double* dev_buf, int64_t count);
 
+/* Row-partitioned two-level CG across ranks (multi-rank handles with precond 1): each rank applies
+ * the reduced camera matrix to its own rows (whole camera clusters) and writes those rows' CG partials straight into
+ * every rank's exchange window over peer-to-peer mappings; the recurrence scalars and the coarse correction stay
+ * replicated, so the result is bitwise the replicated CG's.  After create (and set_exchange): insfm_ba_cg_window
+ * allocates this rank's window and returns its IPC handle (hipIpcMemHandle_t, 64 bytes) in ipc_handle; every rank then
+ * passes all ranks' handles (world_size x 64 bytes, in rank order) to insfm_ba_cg_attach before the first step.  Ranks
+ * must not destroy their handle while a peer may still write into its window (barrier first).  Replaces the replicated
+ * CG of the reference's PCG(tol=1e-5) solve (bundle_adjustment.py:117) on multi-rank runs.
+ * insfm_ba_cg_partition: this rank's rows as [begin, end) cluster-ordered positions. */
+int insfm_ba_cg_window(insfm_ba* h, void* ipc_handle);
+int insfm_ba_cg_attach(insfm_ba* h, const void* handles);
+int insfm_ba_cg_partition(const insfm_ba* h, int32_t* rows_begin_end);
+/* Collective timing probe of the partitioned CG's exchange: `reps` back-to-back flag exchanges with every peer (the
+ * k_xsignal / k_xwait pair each CG iteration pays), average microseconds per exchange into *us. */
+int insfm_ba_debug_time_xchg(insfm_ba* h, int32_t reps, double* us);
+
 /* A fresh LM on the same problem, as TorchBA builds one per Solve: forgets the cached loss, the damping / TrustRegion
  * state and the lagged coarse inverse of the two-level preconditioner (the next solve factorizes its own). */
 int insfm_ba_reset(insfm_ba* h);

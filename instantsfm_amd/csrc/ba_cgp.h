@@ -6,22 +6,23 @@
 // lane; NB blocks, 2 NB registers, most of them AGPRs at one wave per SIMD), so the operator is read from HBM once per
 // solve.  With the coarse correction written as  n = S~ m = m_i + sum_j S~_ij w_j + sum_c A_ic y_c  (m = w + Z~ y,
 // y = E^-1 Z~^T w, A_ic = sum_{j in c} S~_ij Z~_j over the row's off-diagonal blocks of neighbour cluster c, formed once
-// per solve from the register-resident blocks), an iteration needs two grid-wide hand-offs:
+// per solve from the register-resident blocks), an iteration needs one grid barrier:
 //   P1  every wave: gamma, delta, rho from the per-cluster atomic partials -> convergence, alpha, beta (k_tl_pc_cl's
 //       butterfly, so the same doubles in every wave); y_k = (E^-1 R)_k, coarse row k on wave k mod (waves of the
 //       grid), its row of E^-1 read from L2; every row: S~ w, the neighbours' w (the previous iteration's exchange) gathered
 //       eight blocks per load instruction into LDS;
-//   ---- grid barrier ----
-//   P2  y into LDS; every row: m_i, n_i, the recurrence update of the row (k_tl_pspmv's formulas), the partials of the
-//       next iteration (per-cluster atomics) and the row's new w into the exchange buffer;
+//   P2  y into LDS (each coarse row is published as two tagged 8-byte granules that are their own flag: the workgroups
+//       poll them, no grid barrier); every row: m_i, n_i, the recurrence update of the row (k_tl_pspmv's formulas), the
+//       partials of the next iteration (summed per cluster run of the workgroup in LDS, then per-cluster atomics into
+//       one of three buffers) and the row's new w into the exchange buffer of the next parity;
 //   ---- grid barrier ----
 // The recurrence is the oracle's (oracle/ba_oracle.c ora_pcg, pipelined two-level branch) and k_tl_pc_cl/k_tl_pspmv's;
 // only the summation order inside S~ m differs.  Every handed-off word is stored write-through (sc1) or added by an
 // agent-scope atomic and read with sc1 loads; every storing wave drains (vmcnt(0)) before the workgroup barrier behind
 // which one lane arrives (MI355X_MICROARCH.md, hand-off table row 1; cdna_hip_programming.md Guideline 16 R1).  The
-// grid barrier is two-level: arrivals per group of workgroups (blockIdx % 8: one XCD under round-robin placement, speed
-// only), the last of a group arrives at the top counter, the last there releases every group's generation word.  Every
-// spin is bounded; a timeout raises the abort word (status 4), which every waiting workgroup checks.
+// grid barrier counts arrivals per group of workgroups (blockIdx % 8: one XCD under round-robin placement, speed only)
+// and every workgroup polls the eight counters at once.  Every spin is bounded; a timeout raises the abort word
+// (status 4), which every waiting workgroup checks.
 // Host eligibility (ba_kernels.hip, create): single rank, atomic cluster sums (non-deterministic mode), D = 8, rows of at
 // most NB = 128 blocks stored in cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row,
 // and every workgroup resident at once (one per CU).
@@ -34,48 +35,97 @@ namespace insfm {
 constexpr int kCgpRows = 4;                      // camera rows per workgroup
 constexpr int kCgpWaves = kCgpRows;              // one wave per row, one per SIMD (the row's blocks spill into AGPRs)
 constexpr int kCgpThreads = 64 * kCgpWaves;
-constexpr int kCgpSegMax = 32;                   // neighbour-cluster segments per row (LDS table of A_ic)
+constexpr int kCgpSegMax = 40;                   // neighbour-cluster segments per row (LDS table of A_ic)
 constexpr int kCgpGroups = 8;                    // barrier arrival groups
-constexpr int kCgpSyncWords = (2 * kCgpGroups + 2) * 32;  // [group x 8][top][generation x 8][abort], 128-B apart
+constexpr int kCgpSyncWords = (kCgpGroups + 1) * 32;  // [group counter x 8][abort], 128 B apart
 constexpr unsigned kCgpSpinMax = 1u << 22;       // polls before a barrier gives up (~seconds; the host's stall limit is 10 s)
 
 __device__ __forceinline__ unsigned* cgp_grp(unsigned* s, int g) { return s + 32 * g; }
-__device__ __forceinline__ unsigned* cgp_top(unsigned* s) { return s + 32 * kCgpGroups; }
-__device__ __forceinline__ unsigned* cgp_gen(unsigned* s, int g) { return s + 32 * (kCgpGroups + 1 + g); }
-__device__ __forceinline__ unsigned* cgp_abort(unsigned* s) { return s + 32 * (2 * kCgpGroups + 1); }
+__device__ __forceinline__ unsigned* cgp_abort(unsigned* s) { return s + 32 * kCgpGroups; }
 
-// Grid barrier number `epoch` (1, 2, ...; the words are zeroed before the launch).  Every wave drains its own stores
-// and atomics (vmcnt(0)) before the workgroup barrier that orders them in front of lane 0's arrival.  Returns false in
-// every thread when the barrier timed out or another workgroup aborted.
+// Grid barrier number `epoch` (counting on from the barriers of earlier launches: the counters are zeroed at create
+// and after an abort only).  Every wave drains its own stores
+// and atomics (vmcnt(0)) before the workgroup barrier that orders them in front of lane 0's arrival, one no-return
+// agent-scope add on its group's counter (blockIdx % 8).  Wave 0 then polls all group counters at once (lane g loads
+// counter g with an sc1 load) until each has reached epoch x its group size: one atomic and one poll round trip per
+// barrier, no release step (a hierarchical arrive / release / generation barrier took ~3.7 us).  Returns false in
+// every thread when the spin limit passed or another workgroup aborted.
 __device__ __forceinline__ bool cgp_barrier(unsigned* sync, unsigned epoch, int* flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
-        const int G = gridDim.x, g = blockIdx.x % kCgpGroups;
-        const int ngroups = G < kCgpGroups ? G : kCgpGroups;
-        const unsigned gsize = (unsigned)((G - g + kCgpGroups - 1) / kCgpGroups);
-        const unsigned a = __hip_atomic_fetch_add(cgp_grp(sync, g), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-        if (a == epoch * gsize) {
-            const unsigned t = __hip_atomic_fetch_add(cgp_top(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-            if (t == epoch * (unsigned)ngroups)
-                for (int q = 0; q < ngroups; ++q)
-                    __hip_atomic_store(cgp_gen(sync, q), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+    const int G = gridDim.x;
+    if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(cgp_grp(sync, blockIdx.x % kCgpGroups), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+        const int g = threadIdx.x & (kCgpGroups - 1);
+        const unsigned need = epoch * (unsigned)((G - g + kCgpGroups - 1) / kCgpGroups);  // (0 for an empty group)
         int ok = 1;
-        for (unsigned spins = 0;
-             __hip_atomic_load(cgp_gen(sync, g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < epoch;) {
+        for (unsigned spins = 0;; ) {
+            const unsigned v = __hip_atomic_load(cgp_grp(sync, g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all(v >= need)) break;
             __builtin_amdgcn_s_sleep(1);
             if ((++spins & 255u) == 0u &&
                 (spins >= kCgpSpinMax || __hip_atomic_load(cgp_abort(sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-                __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (threadIdx.x == 0) __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = 0;
                 break;
             }
         }
-        *flag = ok;
+        if (threadIdx.x == 0) *flag = ok;
     }
     __syncthreads();
     return __builtin_amdgcn_readfirstlane(*flag) != 0;
+}
+
+// y_k of iteration `tag` as two tagged 8-byte granules {tag, low word} / {tag, high word}: the data is its own flag
+// (MI355X_MICROARCH.md hand-offs, R2), written by one lane with agent-scope (sc1) stores.
+__device__ __forceinline__ void put_y(unsigned long long* yg, int k, unsigned tag, double y) {
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(y), hi = (unsigned long long)tag << 32;
+    __hip_atomic_store(yg + 2 * k, hi | (bits & 0xffffffffull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(yg + 2 * k + 1, hi | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every thread of the workgroup: poll the granules of coarse rows t, t + 256, ... until both halves carry `tag`, then
+// y into LDS; the workgroup repeats until all of its threads hold theirs.  Bounded: false (abort word raised) past the
+// spin limit or when another workgroup aborted.
+__device__ __forceinline__ bool get_y(const unsigned long long* yg, double* ys, int m, unsigned tag, unsigned* sync) {
+    constexpr int RPT = (kCoarseMax + kCgpThreads - 1) / kCgpThreads;
+    const int t = threadIdx.x;
+    unsigned have = 0;
+    for (unsigned spins = 0;; ++spins) {
+        unsigned long long lo[RPT], hi[RPT];
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int k = min(t + q * kCgpThreads, m - 1);
+            lo[q] = hi[q] = 0;
+            if (!(have & (1u << q))) {
+                lo[q] = __hip_atomic_load(yg + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hi[q] = __hip_atomic_load(yg + 2 * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        int mine = 1;
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+            const int k = t + q * kCgpThreads;
+            if (k >= m || (have & (1u << q))) continue;
+            if ((unsigned)(lo[q] >> 32) == tag && (unsigned)(hi[q] >> 32) == tag) {
+                ys[k] = __longlong_as_double((long long)(((hi[q] & 0xffffffffull) << 32) | (lo[q] & 0xffffffffull)));
+                have |= 1u << q;
+            } else {
+                mine = 0;
+            }
+        }
+        if (__syncthreads_and(mine)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if ((spins & 255u) == 255u) {
+            const int stop = spins >= kCgpSpinMax ||
+                             (t == 0 && __hip_atomic_load(cgp_abort(sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (__syncthreads_or(stop)) {
+                if (t == 0) __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                return false;
+            }
+        }
+    }
 }
 
 // a wave-uniform double (every lane holds the same value) as a scalar: branches on it are scalar branches
@@ -85,40 +135,53 @@ __device__ __forceinline__ double uni(double v) {
     return __hiloint2double(hi, lo);
 }
 
-// NB: blocks per row held in registers (a multiple of 8).  sync: kCgpSyncWords zeroed words; wx: [C][8] the w
-// exchange (one buffer: P1 reads it before the barrier behind which P2 rewrites it); yx: [m] the coarse vector;
-// trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations.
+// NB: blocks per row held in registers (a multiple of 8).  wx: [2][C][8] the w exchange by iteration parity (a
+// workgroup's P2 may run while another is still gathering in P1); yg: [m][2] the tagged granules of y, tag0 the tag of
+// iteration 0 (tags never repeat on a handle); sync: kCgpSyncWords barrier words, epoch0: the barriers they have
+// counted so far (one per iteration of earlier launches); oseg: also write this solve's coarse segments tl.Oseg (the
+// E build behind the CG then skips k_tl_erow);
+// trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
+// of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
+// barriers (workgroup 0).
 template <int NB>
 __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __restrict__ nbr_ptr,
                                                           const int* __restrict__ nbr_j, const double* __restrict__ Sn,
                                                           const double* __restrict__ Lf, CgBufs cg, TlBufs tl,
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
-                                                          double* wx, double* yx, unsigned* sync, double* trace) {
+                                                          double* wx, unsigned long long* yg, unsigned tag0,
+                                                          unsigned* sync, unsigned epoch0, int oseg, double* trace) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
     constexpr int NG = NB / 8;                          // gather loads per wave and iteration
     constexpr int RPT = (kCoarseMax + kCgpThreads - 1) / kCgpThreads;  // coarse entries per thread (LDS fills)
     __shared__ double Aseg[kCgpRows][kCgpSegMax][BS];  // A_ic of the row's segments, a-major
     __shared__ double wg[kCgpWaves][NB][D];            // the neighbours' w of the wave's blocks (gathered per iteration)
-    __shared__ double rs[kCoarseMax];                  // the restriction R of the iteration, then y
+    __shared__ double rs[kCoarseMax];                  // the restriction R of the iteration
+    __shared__ double ys[kCoarseMax];                  // y of the iteration
     __shared__ double Lrow[kCgpRows][D * D];           // L_i (row a, column k)
     __shared__ double Zrow[kCgpRows][BS];              // Z~_i (row a, column k)
     __shared__ double vec[kCgpRows][8][D];             // the row's r u w z q s p x
     __shared__ int jn[kCgpWaves][NB];                  // neighbour of each register block
     __shared__ int segc[kCgpRows][kCgpSegMax];         // neighbour cluster of each segment
+    __shared__ double prt[kCgpRows][12];               // each row's partials: r.u, w.u, ||L r||^2, Z~_i^T w (9)
+    __shared__ int pcl[kCgpRows];                      // each row's cluster (-1: no row)
     __shared__ int bflag;
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (wave-uniform: the row's values live in SGPRs)
     const int a8 = lane >> 3, b8 = lane & 7;           // block entry (a, b) of this lane
     const int rl = wv;                                 // local row
-    const int row = blockIdx.x * kCgpRows + rl;
-    const bool has_row = row < C;
+    // the workgroup's rows are consecutive in cluster order (tl.cl_cams), so its rows mostly share one cluster and
+    // their CG partials are summed in LDS before the cluster's atomics
+    const int pos = blockIdx.x * kCgpRows + rl;
+    const bool has_row = pos < C;
+    const int row = has_row ? tl.cl_cams[pos] : 0;
     const int m = tl.m, nc = tl.nc;
     const int gw = blockIdx.x * kCgpWaves + wv;        // this wave's coarse row of E^-1 (if gw < m)
     const int n0 = has_row ? nbr_ptr[row] : 0;
     const int len = has_row ? nbr_ptr[row + 1] - n0 : 0;
     const int nk = min(len, NB);                       // blocks of the row (the host checks len <= NB)
     const int s0 = has_row ? tl.rseg_ptr[row] : 0, nseg = has_row ? tl.rseg_ptr[row + 1] - s0 : 0;
+    const long long t_start = wall_clock64();
     double* V = &vec[rl][0][0];
     enum { VR = 0, VU = 8, VW = 16, VZ = 24, VQ = 32, VS = 40, VP = 48, VX = 56 };
     // ---- setup ----
@@ -141,7 +204,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     }
     __syncthreads();
     // A_ic: lane (a, b) sums S~_ij[a][b] Z~_j[b][q] over the segment's blocks, then adds them into Aseg (LDS atomics).  Segment boundaries are wave-uniform; the Z~ rows
-    // of two blocks are loaded together ahead of their products.
+    // of eight blocks are loaded together ahead of their products.
     if (nk > 0) {
         int cur = 0;
         while (cur < nseg && tl.seg[s0 + cur].z <= 0) ++cur;
@@ -160,7 +223,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             ++cur;
             send = cur < nseg ? tl.seg[s0 + cur].z : 1 << 30;
         };
-        constexpr int CH = 2;
+        constexpr int CH = 8;
 #pragma unroll
         for (int k0 = 0; k0 < NB; k0 += CH) {
             if (k0 >= nk) continue;
@@ -184,29 +247,54 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         flush();
     }
     const int ci = has_row ? tl.clab[row] : 0;
+    if (lane == 0) pcl[rl] = has_row ? ci : -1;
     const bool use = tl.ok[0] != 0;
     const double* erow = Einv + (size_t)min(gw, m - 1) * m;  // this wave's coarse row of E^-1 (read from L2)
     double h_alpha = 1.0, h_gam = 1.0, h_bb = 1.0;
-    unsigned epoch = 0;
+    unsigned epoch = epoch0;
     bool alive = true;
     int it = 0;
     __syncthreads();  // Aseg complete
+    // the coarse matrix's row segments of this solve for the E build that runs behind the CG (k_tl_erow's outputs:
+    // Z~_i^T A_ic, plus Z~_i^T Z~_i on the own-cluster segment, in k_tl_erow's order of additions)
+    if (oseg && has_row) {
+        const int ns = min(nseg, kCgpSegMax);
+        for (int sg = 0; sg < ns; ++sg) {
+            const int own_seg = tl.seg[s0 + sg].w;
+            for (int o = lane; o < MC * MC; o += 64) {
+                const int k = o / MC, l = o % MC;
+                double v = 0.0;
+                if (own_seg) {
+#pragma unroll
+                    for (int a = 0; a < D; ++a) v += Zrow[rl][a * MC + k] * Zrow[rl][a * MC + l];
+                }
+#pragma unroll
+                for (int a = 0; a < D; ++a) v += Zrow[rl][a * MC + k] * Aseg[rl][sg][a * MC + l];
+                tl.Oseg[(size_t)(s0 + sg) * MC * MC + o] = v;
+            }
+        }
+    }
+    if (trace && blockIdx.x == 0 && t == 0) {
+        trace[256] = (double)t_start;
+        trace[257] = (double)wall_clock64();
+    }
     for (;; ++it) {
         // ======== P1 ========
         // every load of the phase is issued before the first wait: the scalar partials, this wave's gathers (lane
         // (a, b) loads entry b of the w of block 8 g + a), the restriction (all threads, into LDS), the E^-1 row
-        const double* G = tl.Gacc + (size_t)(it & 1) * 3 * nc;
+        const int b0 = it % 3;  // partial sums of this iteration (P2 of it - 1 added them)
+        const double* G = tl.Gacc + (size_t)b0 * 3 * nc;
         double gl[3][LNC];
 #pragma unroll
         for (int q = 0; q < LNC; ++q) {
             const int l = min(lane + 64 * q, nc - 1);
             gl[0][q] = ld_sc1(G + l); gl[1][q] = ld_sc1(G + nc + l); gl[2][q] = ld_sc1(G + 2 * nc + l);
         }
-        const double* wsrc = (it == 0 ? cg.w[0] : wx) + b8;
+        const double* wsrc = (it == 0 ? cg.w[0] : wx + (size_t)(it & 1) * C * D) + b8;
         double wv8[NG];
 #pragma unroll
         for (int g = 0; g < NG; ++g) wv8[g] = ld_sc1(wsrc + (size_t)jn[wv][8 * g + a8] * D);
-        const double* Rv = tl.Racc + (size_t)(it & 1) * m;
+        const double* Rv = tl.Racc + (size_t)b0 * m;
         double rv[RPT];
 #pragma unroll
         for (int q = 0; q < RPT; ++q) rv[q] = use ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
@@ -233,6 +321,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) {  // INSFM_DIAG=cgp_trace
             trace[4 * it] = gam; trace[4 * it + 1] = del; trace[4 * it + 2] = rho; trace[4 * it + 3] = done;
+            trace[258 + it] = (double)wall_clock64();
         }
         if (blockIdx.x == 0 && t == 0) {
             if (done) {
@@ -256,10 +345,11 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         if (it == 0) h_bb = bb;
         h_alpha = alpha;
         h_gam = gam;
-        // the partial buffers of iteration it + 1 (last read in P1 of it - 1) are cleared for this iteration's P2
+        // the partial buffers of iteration it + 2 (last read in P1 of it - 1, before the barrier ending P2 of it - 1;
+        // first added to in P2 of it + 1, behind the barrier ending this P2) are cleared now
         if (blockIdx.x == 0) {
-            double* Rn = tl.Racc + (size_t)((it + 1) & 1) * m;
-            double* Gn = tl.Gacc + (size_t)((it + 1) & 1) * 3 * nc;
+            double* Rn = tl.Racc + (size_t)((it + 2) % 3) * m;
+            double* Gn = tl.Gacc + (size_t)((it + 2) % 3) * 3 * nc;
             for (int q = t; q < m; q += kCgpThreads) st_sc1(Rn + q, 0.0);
             for (int q = t; q < 3 * nc; q += kCgpThreads) st_sc1(Gn + q, 0.0);
         }
@@ -278,7 +368,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             for (int q = 0; q < LPL; ++q)
                 if (lane + 64 * q < m) sy += ev[q] * rs[lane + 64 * q];
             const double y = wave_sum(sy);
-            if (lane == 0) st_sc1(yx + gw, y);
+            if (lane == 0) put_y(yg, gw, tag0 + (unsigned)it, y);
         }
         // more coarse rows than waves (small grids): the rest, E^-1 rows loaded here
         for (int g = gw + gridDim.x * kCgpWaves; use && g < m; g += gridDim.x * kCgpWaves) {
@@ -286,30 +376,29 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             double sy = 0.0;
             for (int l = lane; l < m; l += 64) sy += er[l] * rs[l];
             const double y = wave_sum(sy);
-            if (lane == 0) st_sc1(yx + g, y);
+            if (lane == 0) put_y(yg, g, tag0 + (unsigned)it, y);
         }
         // the row's S~ w (lane a < 8 ends with entry a)
         double sw = 0.0;
         if (has_row) {
-            double acc = 0.0;
+            double ac4[4] = {0.0, 0.0, 0.0, 0.0};  // four independent chains
 #pragma unroll
-            for (int k = 0; k < NB; ++k) acc += sreg[k] * wg[wv][k][b8];
+            for (int k = 0; k < NB; ++k) ac4[k & 3] += sreg[k] * wg[wv][k][b8];
+            double acc = (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
             acc += __shfl_xor(acc, 1, 64);
             acc += __shfl_xor(acc, 2, 64);
             acc += __shfl_xor(acc, 4, 64);
             sw = __shfl(acc, 8 * (lane & 7), 64);
         }
-        if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 0] = (double)wall_clock64();
         // ======== P2 ========
-        if (use) {
-            double yv[RPT];
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) yv[q] = ld_sc1(yx + min(t + q * kCgpThreads, m - 1));
-#pragma unroll
-            for (int q = 0; q < RPT; ++q)
-                if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = yv[q];
-            __syncthreads();
+        // y: every workgroup polls the tagged granules of all coarse rows until each carries this iteration's tag
+        // (no grid barrier between the phases)
+        if (use && !get_y(yg, ys, m, tag0 + (unsigned)it, sync)) {
+            alive = false;
+            break;
         }
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 1] = (double)wall_clock64();
         if (has_row) {
             const int la = lane & 7;
             const double w_ = V[VW + la];
@@ -317,15 +406,19 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (use) {
                 double sz = 0.0;
 #pragma unroll
-                for (int k = 0; k < MC; ++k) sz += Zrow[rl][la * MC + k] * rs[ci * MC + k];
+                for (int k = 0; k < MC; ++k) sz += Zrow[rl][la * MC + k] * ys[ci * MC + k];
                 mi += sz;
+                // lane (j, a) = (lane >> 3, lane & 7): row a of the segments j, j + 8, ..., then summed over j
                 const int ns = min(nseg, kCgpSegMax);
-                for (int sg = 0; sg < ns; ++sg) {
-                    const double* yc = rs + segc[rl][sg] * MC;
+                for (int sg = lane >> 3; sg < ns; sg += 8) {
+                    const double* yc = ys + segc[rl][sg] * MC;
                     const double* A = &Aseg[rl][sg][la * MC];
 #pragma unroll
                     for (int k = 0; k < MC; ++k) ay += A[k] * yc[k];
                 }
+                ay += __shfl_xor(ay, 8, 64);
+                ay += __shfl_xor(ay, 16, 64);
+                ay += __shfl_xor(ay, 32, 64);
             }
             const double prod = mi + (sw + ay);  // (the diagonal block of S~ is I)
             const double zn = prod + be * V[VZ + la];
@@ -362,17 +455,22 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 for (int a = 0; a < D; ++a) rr += Zrow[rl][a * MC + lane] * V[VW + a];
             }
             g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
-            const int bsel = (it + 1) & 1;
-            if (lane < MC) unsafeAtomicAdd(tl.Racc + (size_t)bsel * m + (size_t)ci * MC + lane, rr);
-            if (lane == 0) {
-                double* Gq = tl.Gacc + (size_t)bsel * 3 * nc;
-                unsafeAtomicAdd(Gq + ci, g0);
-                unsafeAtomicAdd(Gq + nc + ci, g1);
-                unsafeAtomicAdd(Gq + 2 * nc + ci, g2);
-            }
-            if (lane < D) st_sc1(wx + (size_t)row * D + lane, wn);
+            if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
+            if (lane < MC) prt[rl][3 + lane] = rr;
+            if (lane < D) st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, wn);
         }
+        __syncthreads();
+        // the first row of each cluster run of the workgroup adds the run's partials (rows in order) to the cluster
+        if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3 + MC) {
+            double v = prt[rl][lane];
+            for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
+            const int bsel = (it + 1) % 3;
+            if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)bsel * 3 * nc + (size_t)lane * nc + ci, v);
+            else unsafeAtomicAdd(tl.Racc + (size_t)bsel * m + (size_t)ci * MC + (lane - 3), v);
+        }
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 2] = (double)wall_clock64();
         if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 3] = (double)wall_clock64();
     }
     if (!alive && blockIdx.x == 0 && t == 0) {
         cg.status[1] = it;

@@ -1562,9 +1562,22 @@ struct insfm_ba {
     // [C][8], the coarse vector [kCoarseMax], the grid-barrier words; cgp_defer: the side chain of slot cgp_slot is
     // issued behind the CG (k_tl_cgp holds every SIMD of its CUs, so a chain beside it would crawl on the rest)
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
+    unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
     double* cgp_trace = nullptr;  // INSFM_DIAG=cgp_trace: [64][4] of the last solve, printed to stderr
-    double *cgp_wx = nullptr, *cgp_yx = nullptr;
+    // row-partitioned multi-rank CG (ba_xpart.h; insfm_ba_cg_window / insfm_ba_cg_attach)
+    bool xpart = false;
+    double* xwin = nullptr;            // own window (uncached): 2 x [vc C*D | gd 3C | rowR C*MC + 2], xg C*D, flags
+    size_t xwin_bytes = 0;
+    long long xoff_region[2]{}, xoff_xg = 0, xoff_flags = 0;  // in doubles from the window base
+    std::vector<void*> xopened;        // IPC-opened peer windows (closed at destroy)
+    double** xbases = nullptr;         // device [world] window bases (own included)
+    unsigned** xpflags = nullptr;      // device [world] flag blocks
+    unsigned* xcnt = nullptr;          // device exchange counters [2]
+    std::vector<int> xq;               // [world + 1] cluster-ordered row ranges of the ranks
+    double* cgp_wx = nullptr;           // [2][C][8]
+    unsigned long long* cgp_yg = nullptr;  // [kCoarseMax][2] tagged granules of y
+    unsigned cgp_tag = 1;               // tag of the next launch's first iteration
     unsigned* cgp_sync = nullptr;
     // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
     double *Ebuf[2]{}, *Einvbuf[2]{};
@@ -2030,14 +2043,15 @@ int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
 // per row it held CU / LDS slots the overlapping CG launches needed (config 3, round 1: grid 1000 / 512 / 384 / 256 /
 // 192 / 128 -> 593 / 616 / 612-615 / 603 / 594 LM it/s).
 constexpr int kErowGrid = 256;
-int run_tl_build(insfm_ba* h, int slot, hipStream_t stream) {
+int run_tl_build(insfm_ba* h, int slot, hipStream_t stream, bool have_oseg = false) {
     const int C = h->C, m = h->tl.m;
     TlBufs tl = h->tl;
     tl.E = h->Ebuf[slot];
     return with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         const int grid = stream != h->stream ? std::min(C, kErowGrid) : C;
-        k_tl_erow<DV><<<grid, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
+        if (!have_oseg)  // (k_tl_cgp wrote the segments of this solve)
+            k_tl_erow<DV><<<grid, kThreads, h->erow_lds, stream>>>(C, h->nbr_ptr, h->nbr_j, h->Sn, tl);
         k_tl_ereduce<DV><<<cdiv(m * m, kThreads), kThreads, 0, stream>>>(tl);
         return launch_err(h, "k_tl_erow/ereduce");
     });
@@ -2071,10 +2085,10 @@ constexpr int kCgAhead = CG_AHEAD;
 // solve's setup, while the GPU is still in k_lin_points / k_schur: the host is then ~0.6 ms ahead of the GPU, the
 // launches cost the GPU nothing, and the chain overlaps the CG.  (Round 2 issued it piecemeal from the CG poll loop,
 // and a chain deferred past the CG was measured too: both slower)
-int issue_side_chain(insfm_ba* h, int slot) {
+int issue_side_chain(insfm_ba* h, int slot, bool have_oseg = false) {
     hipStream_t fs = h->side;
     HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
-    if (int rc = run_tl_build(h, slot, fs)) return rc;
+    if (int rc = run_tl_build(h, slot, fs, have_oseg)) return rc;
     HIPCHK(hipEventRecord(h->ev_built, fs));
     h->built_pending = true;
     for (int u = 0; u <= gj_steps(h->tl.m); ++u)
@@ -2121,7 +2135,7 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
         k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
-                                                              h->cg, h->tl);
+                                                              h->cg, h->tl, XPart{});
     }
     if (h->tl.Racc)  // per-cluster atomic sums of the row partials (single rank, non-deterministic)
         k_tl_pc_cl<D><<<h->tl.nc, kPcThreads, 0, h->stream>>>(it, h->C, maxit, tol2, h->cg, h->tl, h->tl.Einv);
@@ -2129,7 +2143,59 @@ void launch_tl_iter(insfm_ba* h, int it, int maxit, double tol2) {
         k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                    h->tl.Einv);
     k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(it, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
-                                                          h->cg, h->tl);
+                                                          h->cg, h->tl, XPart{});
+}
+
+// TlBufs whose exchanged buffers (vc, gd, rowR) are window region q of a partitioned handle
+TlBufs tl_region(const insfm_ba* h, int q) {
+    TlBufs t = h->tl;
+    const int C = h->C, D = h->D, MC = D + 1;
+    double* base = h->xwin + h->xoff_region[q];
+    t.vc = base;
+    t.gd = base + (size_t)C * D;
+    t.rowR = base + (size_t)C * D + 3 * (size_t)C;
+    (void)MC;
+    return t;
+}
+
+XPart xpart_region(const insfm_ba* h, int q) {
+    XPart xp;
+    xp.win = h->xbases;
+    xp.world = h->d.world_size;
+    xp.q0 = h->xq[h->d.rank];
+    xp.off_vc = h->xoff_region[q];
+    xp.off_gd = xp.off_vc + (long long)h->C * h->D;
+    xp.off_rowR = xp.off_gd + 3LL * h->C;
+    return xp;
+}
+
+// One exchange of the partitioned CG (slot 0: iterations, skipped once the CG status is set; 1: solution gather)
+void launch_xchg(insfm_ba* h, int slot) {
+    k_xsignal<<<1, 64, 0, h->stream>>>(h->cg.status, h->xcnt, h->xpflags, h->d.world_size, h->d.rank, slot);
+    k_xwait<<<1, 64, 0, h->stream>>>(h->cg.status, h->cg.prog, h->xcnt,
+                                     reinterpret_cast<unsigned*>(h->xwin + h->xoff_flags), h->d.world_size, slot);
+}
+
+// launch_tl_iter for a row-partitioned handle: k_tl_pc replicated on region it & 1, this rank's rows of k_tl_pspmv
+// writing region (it + 1) & 1 of every window, then the exchange
+template <int D>
+void launch_tl_iter_x(insfm_ba* h, int it, int maxit, double tol2) {
+    const int nrows = h->xq[h->d.rank + 1] - h->xq[h->d.rank];
+    auto pspmv = [&](int i) {
+        if (nrows > 0)
+            k_tl_pspmv<D><<<nrows, kPspmvThreads, 0, h->stream>>>(i, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn,
+                                                                  h->Lf, h->cg, tl_region(h, i & 1),
+                                                                  xpart_region(h, (i + 1) & 1));
+        launch_xchg(h, 0);
+    };
+    if (it == 0) {  // setup (k_tl_basis wrote r0 and its restriction into region 1)
+        k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg,
+                                                                   tl_region(h, 1), h->tl.Einv);
+        pspmv(-1);
+    }
+    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(it, h->C, maxit, tol2, h->pc_rows, h->cg,
+                                                               tl_region(h, it & 1), h->tl.Einv);
+    pspmv(it);
 }
 
 // The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): the setup launches of
@@ -2139,11 +2205,15 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                h->tl.Einv);
     k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
-                                                          h->cg, h->tl);
-    HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+                                                          h->cg, h->tl, XPart{});
+    if (h->cgp_epochs > (1u << 24)) {  // (counter headroom: zero them now and then; an abort zeroes them too)
+        HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+        h->cgp_epochs = 0;
+    }
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->Sn,
-                           h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yx, h->cgp_sync, h->cgp_trace);
+                           h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg, h->cgp_tag, h->cgp_sync,
+                           h->cgp_epochs, h->cgp_defer ? 1 : 0, h->cgp_trace);
     };
     if (h->cgp_nb == 64) go(k_tl_cgp<64>);
     else go(k_tl_cgp<128>);
@@ -2199,7 +2269,10 @@ int run_tl_cg(insfm_ba* h, int* st) {
         if (h->cgp_nb) return from == 0 ? launch_tl_cgp(h, maxit, tol2) : 0;
         const int r = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
-            for (int k = from; k < to; ++k) launch_tl_iter<DV>(h, k, maxit, tol2);
+            for (int k = from; k < to; ++k) {
+                if (h->xpart) launch_tl_iter_x<DV>(h, k, maxit, tol2);
+                else launch_tl_iter<DV>(h, k, maxit, tol2);
+            }
             return launch_err(h, "k_tl_pc/k_tl_pspmv");
         });
         if (htrace) { const double dt = wall_seconds() - t0; t_enq += dt; m_enq = std::max(m_enq, dt / std::max(1, to - from)); n_enq += to - from; }
@@ -2217,7 +2290,7 @@ int run_tl_cg(insfm_ba* h, int* st) {
     if (int rc = enqueue(0, enq)) return rc;
     if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup)
         HIPCHK(hipEventRecord(h->ev_E, h->stream));
-        if (int rc = issue_side_chain(h, h->cgp_slot)) return rc;
+        if (int rc = issue_side_chain(h, h->cgp_slot, true)) return rc;
         h->cgp_defer = false;
     }
     CgPoll poll;
@@ -2266,13 +2339,28 @@ int run_tl_cg(insfm_ba* h, int* st) {
     }
     h->cg_launches += h->cgp_nb ? 1 : enq;
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
+    if (h->cgp_nb) {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
+        h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
+        if (st[0] == 1 || st[0] == 2) {
+            h->cgp_epochs += (unsigned)st[1];
+        } else {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+            h->cgp_epochs = 0;
+        }
+    }
     if (h->cgp_nb && h->cgp_trace) {
-        double tr[256];
+        double tr[256 + 2 + 64 + 4 * 64];
         HIPCHK(hipMemcpy(tr, h->cgp_trace, sizeof(tr), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d\n", st[0], st[1], st[2]);
-        for (int k = 0; k <= std::min(st[1], 63); ++k)
-            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g\n", k, tr[4 * k],
-                         tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3]);
+        const int n = std::min(st[1], 63);
+        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d: setup %.1f us, iterations %.1f us (%.2f us each)\n",
+                     st[0], st[1], st[2], 0.01 * (tr[257] - tr[256]), 0.01 * (tr[258 + n] - tr[257]),
+                     n > 0 ? 0.01 * (tr[258 + n] - tr[258]) / n : 0.0);
+        for (int k = 0; k <= n; ++k)
+            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g t %.1f us | P1 %.2f B1 %.2f P2 %.2f "
+                         "B2 %.2f\n", k, tr[4 * k], tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3], 0.01 * (tr[258 + k] - tr[256]),
+                         0.01 * (tr[322 + 4 * k] - tr[258 + k]), 0.01 * (tr[323 + 4 * k] - tr[322 + 4 * k]),
+                         0.01 * (tr[324 + 4 * k] - tr[323 + 4 * k]), 0.01 * (tr[325 + 4 * k] - tr[324 + 4 * k]));
     }
     return 0;
 }
@@ -2294,7 +2382,8 @@ int run_bj_cg(insfm_ba* h, int* st) {
             constexpr int DV = decltype(dc_)::value;
             for (int k = it; k < stop; ++k) {
                 if (h->tlon) {
-                    launch_tl_iter<DV>(h, k, maxit, tol2);
+                    if (h->xpart) launch_tl_iter_x<DV>(h, k, maxit, tol2);
+                    else launch_tl_iter<DV>(h, k, maxit, tol2);
                     continue;
                 }
                 if (k > 0) k_cg_dots<<<1, 64, 0, h->stream>>>(k, h->C, maxit, tol2, h->cg);
@@ -2401,15 +2490,34 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (rc) return rc;
         if (st[0] != 1) {
             h->err = std::string("PCG ") +
-                     (st[0] == 2 ? "breakdown" : st[0] == 4 ? "grid barrier timed out (k_tl_cgp)" : "did not finish") +
+                     (st[0] == 2 ? "breakdown"
+                      : st[0] == 4 ? "timed out (a k_tl_cgp grid barrier or a cross-rank exchange of the partitioned CG)"
+                                   : "did not finish") +
                      " at iteration " +
                      std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
                      (h->tlon ? std::to_string(st[2]) : std::string("off")) + ")";
-            return INSFM_BA_ESOLVER;
+            return st[0] == 4 ? INSFM_BA_EHIP : INSFM_BA_ESOLVER;
         }
         iters = st[1];
         h->coarse_used = h->tlon ? st[2] : 0;
         h->last_cg_iters = iters;
+        if (h->xpart) {  // partitioned CG: every rank's solution rows into every window, then into cg.x
+            const int n = h->xq[h->d.rank + 1] - h->xq[h->d.rank];
+            if (n > 0)
+                k_xput_x<<<cdiv((long long)n * D, 256), 256, 0, h->stream>>>(n, D, h->tl.cl_cams, h->cg.x,
+                                                                            xpart_region(h, 0), h->xoff_xg);
+            launch_xchg(h, 1);
+            HIPCHK(hipMemcpyAsync(h->cg.x, h->xwin + h->xoff_xg, sizeof(double) * (size_t)h->C * D,
+                                  hipMemcpyDeviceToDevice, h->stream));
+            if ((rc = launch_err(h, "partitioned CG gather"))) return rc;
+            int sw[2] = {0, 0};  // (prototype path: one synchronization to see a gather that timed out)
+            HIPCHK(hipMemcpyAsync(sw, h->cg.status, sizeof(sw), hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            if (sw[0] == 4) {
+                h->err = "partitioned CG: the solution gather across ranks timed out";
+                return INSFM_BA_EHIP;
+            }
+        }
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
@@ -2677,6 +2785,8 @@ void insfm_ba_destroy(insfm_ba* h) {
     for (hipStream_t st : {h->stream, h->side, h->xstream, h->aux})
         if (st) (void)hipStreamSynchronize(st);
     if (!h->stream) (void)hipDeviceSynchronize();
+    for (void* q : h->xopened) (void)hipIpcCloseMemHandle(q);  // (peers must be done writing: the caller's barrier)
+    if (h->xwin) (void)hipFree(h->xwin);
     dfree_all(h);
     if (h->host_res) (void)hipHostFree(h->host_res);
     if (h->prog_host) (void)hipHostFree(h->prog_host);
@@ -3444,10 +3554,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             tl.Racc = nullptr;
             tl.Gacc = nullptr;
             if (!desc->deterministic && desc->world_size <= 1 && !desc->allreduce) {
-                if ((rc = dd(&tl.Racc, 2 * (size_t)m))) return fail(rc, "");
-                if ((rc = dd(&tl.Gacc, 2 * 3 * (size_t)nc))) return fail(rc, "");
-                if (hipMemsetAsync(tl.Racc, 0, sizeof(double) * 2 * (size_t)m, h->stream) != hipSuccess ||
-                    hipMemsetAsync(tl.Gacc, 0, sizeof(double) * 6 * (size_t)nc, h->stream) != hipSuccess)
+                if ((rc = dd(&tl.Racc, 3 * (size_t)m))) return fail(rc, "");
+                if ((rc = dd(&tl.Gacc, 3 * 3 * (size_t)nc))) return fail(rc, "");
+                if (hipMemsetAsync(tl.Racc, 0, sizeof(double) * 3 * (size_t)m, h->stream) != hipSuccess ||
+                    hipMemsetAsync(tl.Gacc, 0, sizeof(double) * 9 * (size_t)nc, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "Racc clear");
             }
         }
@@ -3528,10 +3638,14 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 ce = hipOccupancyMaxActiveBlocksPerMultiprocessor(
                     &per_cu, nb == 64 ? (const void*)k_tl_cgp<64> : (const void*)k_tl_cgp<128>, kCgpThreads, 0);
             if (ce == hipSuccess && per_cu >= 1 && grid <= ncu) {
-                if ((rc = dd(&h->cgp_wx, cd))) return fail(rc, "");
-                if ((rc = dd(&h->cgp_yx, (size_t)kCoarseMax))) return fail(rc, "");
+                if ((rc = dd(&h->cgp_wx, 2 * cd))) return fail(rc, "");
+                if ((rc = dalloc(h, (void**)&h->cgp_yg, sizeof(unsigned long long) * 2 * kCoarseMax))) return fail(rc, "");
+                if (hipMemsetAsync(h->cgp_yg, 0, sizeof(unsigned long long) * 2 * kCoarseMax, h->stream) != hipSuccess)
+                    return fail(INSFM_BA_EHIP, "cgp granules");
                 if ((rc = dalloc(h, (void**)&h->cgp_sync, sizeof(unsigned) * kCgpSyncWords))) return fail(rc, "");
-                if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, 256))) return fail(rc, "");
+                if (hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream) != hipSuccess)
+                    return fail(INSFM_BA_EHIP, "cgp barrier words");
+                if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, 256 + 2 + 64 + 4 * 64))) return fail(rc, "");
                 h->cgp_nb = nb;
                 h->cgp_grid = grid;
                 if (diag("create"))
@@ -3574,6 +3688,105 @@ int insfm_ba_set_exchange(insfm_ba* h, double* buf, int64_t count) {
     h->gc = h->U + (size_t)C * D * D;
     h->scal = h->gc + (size_t)C * D;
     h->result = h->scal;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_cg_window(insfm_ba* h, void* ipc_handle) {
+    if (!h || !ipc_handle) return INSFM_BA_EINVAL;
+    if (h->kind != 0 || h->d.world_size < 2 || !h->tlon || h->tl.Racc || h->xwin || h->cgp_nb) {
+        h->err = "cg_window: needs a multi-rank two-level handle (precond 1) that has no window yet";
+        return INSFM_BA_EINVAL;
+    }
+    const int C = h->C, D = h->D, MC = D + 1, W = h->d.world_size;
+    const long long region = (long long)C * D + 3LL * C + (long long)C * MC + 2;
+    h->xoff_region[0] = 0;
+    h->xoff_region[1] = region;
+    h->xoff_xg = 2 * region;
+    h->xoff_flags = h->xoff_xg + (long long)C * D;
+    h->xwin_bytes = sizeof(double) * (size_t)h->xoff_flags + sizeof(unsigned) * kXFlagStride * 2 * (size_t)W;
+    // uncached device memory: peers write into it over their mappings, and no cache of this device keeps a stale line
+    hipError_t e = hipExtMallocWithFlags(reinterpret_cast<void**>(&h->xwin), h->xwin_bytes, hipDeviceMallocUncached);
+    if (e == hipSuccess) e = hipMemsetAsync(h->xwin, 0, h->xwin_bytes, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e == hipSuccess) e = hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(ipc_handle), h->xwin);
+    if (e != hipSuccess) {
+        h->err = std::string("cg_window: ") + hipGetErrorString(e);
+        return INSFM_BA_EHIP;
+    }
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_cg_attach(insfm_ba* h, const void* handles) {
+    if (!h || !handles || !h->xwin || h->xpart) return INSFM_BA_EINVAL;
+    const int W = h->d.world_size, C = h->C;
+    std::vector<double*> bases(W, nullptr);
+    std::vector<unsigned*> flags(W, nullptr);
+    for (int r = 0; r < W; ++r) {
+        if (r == h->d.rank) {
+            bases[r] = h->xwin;
+        } else {
+            void* q = nullptr;
+            hipIpcMemHandle_t hd;
+            std::memcpy(&hd, static_cast<const char*>(handles) + (size_t)r * sizeof(hipIpcMemHandle_t), sizeof(hd));
+            const hipError_t e = hipIpcOpenMemHandle(&q, hd, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+                h->err = std::string("cg_attach: rank ") + std::to_string(r) + ": " + hipGetErrorString(e);
+                return INSFM_BA_EHIP;
+            }
+            h->xopened.push_back(q);
+            bases[r] = static_cast<double*>(q);
+        }
+        flags[r] = reinterpret_cast<unsigned*>(bases[r] + h->xoff_flags);
+    }
+    int rc = 0;
+    if ((rc = dalloc(h, reinterpret_cast<void**>(&h->xbases), sizeof(double*) * W))) return rc;
+    if ((rc = dalloc(h, reinterpret_cast<void**>(&h->xpflags), sizeof(unsigned*) * W))) return rc;
+    if ((rc = dalloc(h, reinterpret_cast<void**>(&h->xcnt), sizeof(unsigned) * 2))) return rc;
+    HIPCHK(hipMemcpyAsync(h->xbases, bases.data(), sizeof(double*) * W, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->xpflags, flags.data(), sizeof(unsigned*) * W, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemsetAsync(h->xcnt, 0, sizeof(unsigned) * 2, h->stream));
+    // rows: the cluster-ordered positions split at cluster boundaries, rank r from the boundary nearest r C / W
+    const std::vector<int>& lab = h->clab_host;
+    std::vector<int> bnd;  // cluster-ordered boundaries (positions where a cluster starts), incl. 0 and C
+    {
+        std::vector<int> size(h->tl.nc, 0);
+        for (int i = 0; i < C; ++i) size[lab[i]]++;
+        int q = 0;
+        for (int c = 0; c < h->tl.nc; ++c) { bnd.push_back(q); q += size[c]; }
+        bnd.push_back(q);
+    }
+    h->xq.assign(W + 1, C);
+    h->xq[0] = 0;
+    for (int r = 1; r < W; ++r) {
+        const long long target = (long long)r * C / W;
+        int best = bnd[0];
+        for (int b : bnd)
+            if (std::llabs(b - target) < std::llabs(best - target)) best = b;
+        h->xq[r] = std::max(best, h->xq[r - 1]);
+    }
+    // the basis writes r0 and its restriction into region 1 (what the setup k_tl_pc reads)
+    h->tl = tl_region(h, 1);
+    HIPCHK(hipStreamSynchronize(h->stream));
+    h->xpart = true;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_debug_time_xchg(insfm_ba* h, int32_t reps, double* us) {
+    if (!h || !us || !h->xpart || reps < 1) return INSFM_BA_EINVAL;
+    HIPCHK(hipEventRecord(h->ev[10], h->stream));
+    for (int r = 0; r < reps; ++r) launch_xchg(h, 1);  // (slot 1: not gated by the CG status)
+    HIPCHK(hipEventRecord(h->ev[11], h->stream));
+    HIPCHK(hipEventSynchronize(h->ev[11]));
+    float ms = 0.0f;
+    HIPCHK(hipEventElapsedTime(&ms, h->ev[10], h->ev[11]));
+    *us = 1e3 * ms / reps;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_cg_partition(const insfm_ba* h, int32_t* rows_begin_end) {
+    if (!h || !rows_begin_end || !h->xpart) return INSFM_BA_EINVAL;
+    rows_begin_end[0] = h->xq[h->d.rank];
+    rows_begin_end[1] = h->xq[h->d.rank + 1];
     return INSFM_BA_OK;
 }
 
@@ -3709,7 +3922,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
         with_D(h->D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(0, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn,
-                                                                 h->Lf, h->cg, h->tl);
+                                                                 h->Lf, h->cg, h->tl, XPart{});
             return 0;
         });
     }
@@ -3721,7 +3934,7 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
                 launch_tl_iter<DV>(h, 1, h->d.pcg_max_iter, 0.0);
             } else if (which == 3) {
                 k_tl_pspmv<DV><<<h->C, kPspmvThreads, 0, h->stream>>>(1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf, h->cg,
-                                                                   h->tl);
+                                                                   h->tl, XPart{});
             } else if (which == 4) {
                 int rc2 = run_tl_basis(h, h->cams_cur, h->stream);
                 if (!rc2) rc2 = run_tl_build(h, 0, h->stream);

@@ -25,6 +25,7 @@
 #define COARSE_MAX_DIM 768
 #endif
 #include "ba_device.h"
+#include "ba_xpart.h"
 
 namespace insfm {
 
@@ -40,9 +41,10 @@ struct TlBufs {
     double* rowR;        // [C][MC] row partials of the restriction Z~_i^T w_i, rows in cluster-member order (cpos)
     // atomic cluster sums (single GPU, non-deterministic mode; nullptr otherwise): k_tl_pspmv adds each row's
     // restriction and scalar partials into its cluster's entries with no-return f64 atomics, double-buffered by
-    // iteration parity (k_tl_pc of iteration i reads buffer i & 1 and clears buffer (i + 1) & 1 for k_tl_pspmv)
-    double* Racc;        // [2][m]
-    double* Gacc;        // [2][3][nc]
+    // iteration parity (k_tl_pc of iteration i reads buffer i & 1 and clears buffer (i + 1) & 1 for k_tl_pspmv);
+    // k_tl_cgp uses three buffers (i mod 3)
+    double* Racc;        // [3][m]
+    double* Gacc;        // [3][3][nc]
     double* Oseg;        // [nseg][MC][MC] per (row, neighbour cluster) sums of Z~_i^T S~_ij Z~_j
     double* E;           // [ldE][ldE] coarse matrix padded to whole kGB blocks (pad: identity), inverted in place
     double* Einv;        // [m][m] compact E^-1 (k_tl_pc reads its cluster's rows)
@@ -752,10 +754,13 @@ __global__ __launch_bounds__(kPcThreads) void k_tl_pc(int it, int C, int maxit, 
     const int rb0 = tl.cl_ptr[tc], rb1 = tl.cl_ptr[tc + 1];
     const int ne = e1 - e0;
     if (tl.Racc != nullptr && blockIdx.x == 0) {  // clear the buffer this iteration's k_tl_pspmv adds into
-        double* R = tl.Racc + (size_t)((it + 1) & 1) * m;
-        double* G = tl.Gacc + (size_t)((it + 1) & 1) * 3 * tl.nc;
-        for (int q = t; q < m; q += kPcThreads) R[q] = 0.0;
-        for (int q = t; q < 3 * tl.nc; q += kPcThreads) G[q] = 0.0;
+        // (setup: buffers 0 and 1 -- k_tl_cgp's first iteration adds into buffer 1 with no barrier before it)
+        for (int bq = (it + 1) & 1; bq <= (setup ? 1 : ((it + 1) & 1)); ++bq) {
+            double* R = tl.Racc + (size_t)bq * m;
+            double* G = tl.Gacc + (size_t)bq * 3 * tl.nc;
+            for (int q = t; q < m; q += kPcThreads) R[q] = 0.0;
+            for (int q = t; q < 3 * tl.nc; q += kPcThreads) G[q] = 0.0;
+        }
     }
     if (st0 != 0 || ne < 0) return;  // (ne < 0 never holds: it makes the branch wait for the range loads as well)
     const bool use = okv != 0;
@@ -1028,7 +1033,7 @@ constexpr int kPspmvThreads = PSPMV_NT;
 template <int D, int NT = kPspmvThreads>
 __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, const int* __restrict__ nbr_ptr,
                                                  const int* __restrict__ nbr_j, const double* __restrict__ Sn,
-                                                 const double* __restrict__ Lf, CgBufs cg, TlBufs tl) {
+                                                 const double* __restrict__ Lf, CgBufs cg, TlBufs tl, XPart xp) {
     using G = CgGeom<D>;
     constexpr int NW = NT / 64;
     constexpr int DP = G::DP, HP = G::HP, PPB = G::PPB, BPW = G::BPW, PPL = G::PPL, BPR = BPW * NW, MC = D + 1;
@@ -1036,7 +1041,8 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     __shared__ double sv[2][D];  // r and w of the row after the update
     if (cg.status[0] != 0) return;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int row = blockIdx.x;
+    // partitioned across ranks (ba_xpart.h): this rank's rows are the cluster-ordered positions from xp.q0
+    const int row = xp.win ? tl.cl_cams[xp.q0 + blockIdx.x] : blockIdx.x;
     const bool setup = it < 0;
     const int bw = (PPB <= 64) ? lane / PPB : 0;
     const int pc0 = (PPB <= 64) ? lane - bw * PPB : lane;
@@ -1147,7 +1153,7 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
         }
         sv[0][a] = r_;
         sv[1][a] = w_;
-        tl.vc[(size_t)tl.cpos[row] * D + a] = w_;
+        xstore(xp, tl.vc + (size_t)tl.cpos[row] * D + a, xp.off_vc + (size_t)tl.cpos[row] * D + a, w_);
         g0 = r_ * u_;
         g1 = w_ * u_;
     }
@@ -1165,7 +1171,10 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
     } else if (lane < D + MC) {  // restriction of w: sum_a Z~[a][k] w_a
 #pragma unroll
         for (int a = 0; a < D; ++a) rr += tailop[a] * sv[1][a];
-        if (tl.Racc == nullptr) st_sc1(tl.rowR + (size_t)cp * MC + (lane - D), rr);
+        if (tl.Racc == nullptr) {
+            if (xp.win) xstore(xp, nullptr, xp.off_rowR + (size_t)cp * MC + (lane - D), rr);
+            else st_sc1(tl.rowR + (size_t)cp * MC + (lane - D), rr);
+        }
     }
     g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
     if (tl.Racc != nullptr) {  // cluster sums by atomics (order varies run to run; single GPU, non-deterministic)
@@ -1180,7 +1189,15 @@ __global__ __launch_bounds__(NT) void k_tl_pspmv(int it, int C, int stride, cons
         }
         return;
     }
-    if (lane == 0) { st_sc1(tl.gd + cp, g0); st_sc1(tl.gd + C + cp, g1); st_sc1(tl.gd + 2 * C + cp, g2); }
+    if (lane == 0) {
+        if (xp.win) {
+            xstore(xp, nullptr, xp.off_gd + cp, g0);
+            xstore(xp, nullptr, xp.off_gd + C + cp, g1);
+            xstore(xp, nullptr, xp.off_gd + 2 * C + cp, g2);
+        } else {
+            st_sc1(tl.gd + cp, g0); st_sc1(tl.gd + C + cp, g1); st_sc1(tl.gd + 2 * C + cp, g2);
+        }
+    }
 }
 
 }  // namespace insfm

@@ -189,6 +189,29 @@ class BundleAdjuster:
         except Exception:
             pass
 
+    def partition_cg(self, process_group=None):
+        """Switch a multi-rank two-level handle to the row-partitioned CG (insfm_ba_cg_window / _attach, DESIGN.md
+        section 5): every rank exports its exchange window, the IPC handles are all-gathered over ``process_group``
+        (any backend: the handles are host bytes), and every rank maps its peers' windows.  Collective; call before
+        the first step.  Returns this rank's [begin, end) cluster-ordered camera rows."""
+        import torch.distributed as dist
+        L = _capi.load()
+        hbuf = ctypes.create_string_buffer(64)
+        _capi.check(self._h, L.insfm_ba_cg_window(self._h, hbuf))
+        world = dist.get_world_size(process_group)
+        handles = [None] * world
+        dist.all_gather_object(handles, bytes(hbuf.raw), group=process_group)
+        _capi.check(self._h, L.insfm_ba_cg_attach(self._h, b"".join(handles)))
+        rows = (ctypes.c_int32 * 2)()
+        _capi.check(self._h, L.insfm_ba_cg_partition(self._h, rows))
+        return int(rows[0]), int(rows[1])
+
+    def debug_time_exchange(self, reps=200):
+        """Collective: microseconds per flag exchange of the partitioned CG (insfm_ba_debug_time_xchg)."""
+        us = ctypes.c_double()
+        _capi.check(self._h, _capi.load().insfm_ba_debug_time_xchg(self._h, int(reps), ctypes.byref(us)))
+        return us.value
+
     def last_error(self):
         """The handle's last error message (e.g. why a step reported ``failed``)."""
         return _capi.load().insfm_ba_last_error(self._h).decode() if getattr(self, "_h", None) is not None else ""

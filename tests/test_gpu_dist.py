@@ -72,3 +72,19 @@ def test_rccl_exchange_one_rank(chunks):
     assert out["backend"] == "nccl" and out["world"] == 1
     assert out["exchange_calls"] >= 4 * 3, out  # per step: [U|g_c], [S|b] per trial, the 5 result scalars
     assert out["loss_rel"] < 1e-12 and out["cams_rel"] < 1e-12 and out["points_rel"] < 1e-12, out
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("extra", [["--small", "--steps", "4"], ["--config", "2", "--steps", "3"]])
+def test_partitioned_cg_matches_replicated(extra):
+    """Row-partitioned CG (insfm_ba_cg_window / _attach: each rank applies S~ to its own camera rows and writes their
+    CG partials into every rank's IPC exchange window; 2 ranks sharing the one MI355X) against the replicated CG on the
+    same shards: bitwise the same losses and parameters on every rank, and the usual agreement with one GPU."""
+    rep = _run(2, "gloo", extra)
+    part = _run(2, "gloo", extra + ["--cg-partition"])
+    assert part["cg_partition"] and part["rows"][0] == 0 and 0 < part["rows"][1], part
+    assert part["losses_hex"] == rep["losses_hex"], (part["losses_hex"], rep["losses_hex"])
+    assert part["params_sha"] == rep["params_sha"], (part, rep)
+    assert part["pcg_iters"] == rep["pcg_iters"], (part["pcg_iters"], rep["pcg_iters"])
+    assert part["cams_equal_across_ranks"], part
+    assert part["loss_rel"] < 1e-9 and part["cams_rel"] < 1e-7, part

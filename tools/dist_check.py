@@ -10,6 +10,7 @@ re-runs the problem on one GPU and prints the largest relative differences as on
 ranks may share one GPU (the 1-GPU test box); with nccl (RCCL) each rank needs its own GPU.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -82,6 +83,8 @@ def main():
     ap.add_argument("--gp", action="store_true", help="global positioning (insfm_gp) instead of BA")
     ap.add_argument("--force-exchange", action="store_true",
                     help="install the all-reduce callback even with one rank (drives the RCCL branch on one GPU)")
+    ap.add_argument("--cg-partition", action="store_true",
+                    help="row-partitioned CG (each rank applies S~ to its own rows, partials exchanged over IPC windows)")
     ap.add_argument("--exchange-chunks", type=int, default=4,
                     help="row chunks of the [S | b] exchange behind the Schur build (1: one all-reduce after it)")
     args = ap.parse_args()
@@ -102,11 +105,15 @@ def main():
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
                          world_size=world, rank=rank, shard=shards[rank], deterministic=True,
                          force_exchange=args.force_exchange, exchange_chunks=args.exchange_chunks)
+    rows = eng.partition_cg() if args.cg_partition else None
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
     pts = torch.from_numpy(prob.points_init.copy()).to(dev)
-    losses = []
+    losses, iters = [], []
     for _ in range(args.steps):
-        losses.append(eng.step(cams, pts)[0])
+        loss, st = eng.step(cams, pts)
+        losses.append(loss)
+        iters.append(int(st["pcg_total"]))
+    xchg_us = eng.debug_time_exchange(200) if args.cg_partition else None
     loss, rmse = eng.cost(cams, pts)
     # every rank updated only its own tracks: assemble the full point array
     p0, p1 = shards[rank]
@@ -139,6 +146,9 @@ def main():
                    loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
                    cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
                    rmse=rmse, ref_rmse=ref_rmse, exchange_calls=eng.exchange_calls[0], n_obs=int(prob.n_obs),
+                   cg_partition=bool(args.cg_partition), rows=rows, pcg_iters=iters, xchg_us=xchg_us,
+                   losses_hex=[float(x).hex() for x in losses],
+                   params_sha=hashlib.sha256(cams.cpu().numpy().tobytes() + full.numpy().tobytes()).hexdigest(),
                    cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all) if cams_all else None)
         print(json.dumps(out), flush=True)
         ok = out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7
