@@ -134,6 +134,13 @@ int insfm_ba_cost(insfm_ba* h, const double* cam_params, const double* points, d
 int64_t insfm_ba_exchange_count(const insfm_ba* h);
 int insfm_ba_set_exchange(insfm_ba* h, double* dev_buf, int64_t count);
 
+/* Multi-rank runs: how many ranks of the group (this one included) share this rank's GPU; every rank passes the same
+ * count before the first step.  The replicated two-level CG runs as one persistent launch per solve (k_tl_cgp) only
+ * when that many of its grids fit on the device at once (else the ranks' workgroups could hold each other off the CUs
+ * until a grid barrier times out); otherwise every rank takes the launch-per-iteration CG, so that all ranks round
+ * alike.  Default 1 (one GPU per rank). */
+int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks);
+
 /* Row-partitioned two-level CG across ranks (multi-rank handles with precond 1): each rank applies
  * the reduced camera matrix to its own rows (whole camera clusters) and writes those rows' CG partials straight into
  * every rank's exchange window over peer-to-peer mappings; the recurrence scalars and the coarse correction stay

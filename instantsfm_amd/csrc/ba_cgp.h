@@ -22,10 +22,14 @@
 // which one lane arrives (MI355X_MICROARCH.md, hand-off table row 1; cdna_hip_programming.md Guideline 16 R1).  The
 // grid barrier counts arrivals per group of workgroups (blockIdx % 8: one XCD under round-robin placement, speed only)
 // and every workgroup polls the eight counters at once.  Every spin is bounded; a timeout raises the abort word
-// (status 4), which every waiting workgroup checks.
-// Host eligibility (ba_kernels.hip, create): single rank, atomic cluster sums (non-deterministic mode), D = 8, rows of at
-// most NB = 128 blocks stored in cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row,
-// and every workgroup resident at once (one per CU).
+// (status 4), which every waiting workgroup checks; a single-rank host then repeats the solve on the launch path and
+// stays there.
+// Two variants: per-cluster atomic partial sums (single rank, non-deterministic), and DET, a fixed summation order
+// (deterministic mode and every rank of the replicated multi-rank CG: cluster owners sum the workgroups' run partials
+// in order and publish them as tagged granules).
+// Host eligibility (ba_kernels.hip, create): D = 8, host-mapped progress word, rows of at most NB = 128 blocks stored in
+// cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row, and every workgroup resident at
+// once (one per CU) -- for ranks sharing a GPU, all of their grids at once.
 #pragma once
 #include "ba_common.h"
 #include "ba_twolevel.h"
@@ -38,6 +42,10 @@ constexpr int kCgpThreads = 64 * kCgpWaves;
 constexpr int kCgpSegMax = 40;                   // neighbour-cluster segments per row (LDS table of A_ic)
 constexpr int kCgpGroups = 8;                    // barrier arrival groups
 constexpr int kCgpSyncWords = (kCgpGroups + 1) * 32;  // [group counter x 8][abort], 128 B apart
+constexpr int kCgpMaxClusters = kCoarseMax / 9;   // clusters of a D = 8 handle (m = 9 nc <= kCoarseMax)
+constexpr int kCgpRunBatch = 8;                  // cluster runs (or setup rows) an owner loads at once
+constexpr int kCgpTraceIt = 5;                   // INSFM_DIAG=cgp_trace: every workgroup's times of this iteration
+constexpr int kCgpTraceLen = 772 + 2 * 256;
 constexpr unsigned kCgpSpinMax = 1u << 22;       // polls before a barrier gives up (~seconds; the host's stall limit is 10 s)
 
 __device__ __forceinline__ unsigned* cgp_grp(unsigned* s, int g) { return s + 32 * g; }
@@ -85,11 +93,13 @@ __device__ __forceinline__ void put_y(unsigned long long* yg, int k, unsigned ta
     __hip_atomic_store(yg + 2 * k + 1, hi | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Every thread of the workgroup: poll the granules of coarse rows t, t + 256, ... until both halves carry `tag`, then
-// y into LDS; the workgroup repeats until all of its threads hold theirs.  Bounded: false (abort word raised) past the
-// spin limit or when another workgroup aborted.
-__device__ __forceinline__ bool get_y(const unsigned long long* yg, double* ys, int m, unsigned tag, unsigned* sync) {
-    constexpr int RPT = (kCoarseMax + kCgpThreads - 1) / kCgpThreads;
+// Every thread of the workgroup: poll the granule pairs of entries t, t + 256, ... (entry k at pair map(k)) until both
+// halves carry `tag`, then the value into LDS; the workgroup repeats until all of its threads hold theirs.  Bounded:
+// false (abort word raised) past the spin limit or when another workgroup aborted.
+template <int CAP = kCoarseMax, class Map>
+__device__ __forceinline__ bool poll_tagged(const unsigned long long* yg, Map map, double* ys, int m, unsigned tag,
+                                            unsigned* sync) {
+    constexpr int RPT = (CAP + kCgpThreads - 1) / kCgpThreads;
     const int t = threadIdx.x;
     unsigned have = 0;
     for (unsigned spins = 0;; ++spins) {
@@ -99,8 +109,8 @@ __device__ __forceinline__ bool get_y(const unsigned long long* yg, double* ys, 
             const int k = min(t + q * kCgpThreads, m - 1);
             lo[q] = hi[q] = 0;
             if (!(have & (1u << q))) {
-                lo[q] = __hip_atomic_load(yg + 2 * k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                hi[q] = __hip_atomic_load(yg + 2 * k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lo[q] = __hip_atomic_load(yg + 2 * map(k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                hi[q] = __hip_atomic_load(yg + 2 * map(k) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         int mine = 1;
@@ -128,6 +138,38 @@ __device__ __forceinline__ bool get_y(const unsigned long long* yg, double* ys, 
     }
 }
 
+__device__ __forceinline__ bool get_y(const unsigned long long* yg, double* ys, int m, unsigned tag, unsigned* sync) {
+    return poll_tagged(yg, [](int k) { return k; }, ys, m, tag, sync);
+}
+
+// One wave: poll the granule pairs g[idx[q]] (q < n, lane-varying indices) until every lane's all carry `tag`.
+template <int N>
+__device__ __forceinline__ bool poll_wave(const unsigned long long* g, const int (&idx)[N], double (&out)[N], unsigned tag,
+                                          unsigned* sync, unsigned have = 0) {
+    for (unsigned spins = 0;; ++spins) {
+        int mine = 1;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+            if (have & (1u << q)) continue;
+            const unsigned long long lo = __hip_atomic_load(g + 2 * idx[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long hi = __hip_atomic_load(g + 2 * idx[q] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((unsigned)(lo >> 32) == tag && (unsigned)(hi >> 32) == tag) {
+                out[q] = __longlong_as_double((long long)(((hi & 0xffffffffull) << 32) | (lo & 0xffffffffull)));
+                have |= 1u << q;
+            } else {
+                mine = 0;
+            }
+        }
+        if (__all(mine)) return true;
+        __builtin_amdgcn_s_sleep(1);
+        if ((spins & 255u) == 255u &&
+            (spins >= kCgpSpinMax || __hip_atomic_load(cgp_abort(sync), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+            __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+}
+
 // a wave-uniform double (every lane holds the same value) as a scalar: branches on it are scalar branches
 __device__ __forceinline__ double uni(double v) {
     const int lo = __builtin_amdgcn_readfirstlane(__double2loint(v));
@@ -138,25 +180,28 @@ __device__ __forceinline__ double uni(double v) {
 // NB: blocks per row held in registers (a multiple of 8).  wx: [2][C][8] the w exchange by iteration parity (a
 // workgroup's P2 may run while another is still gathering in P1); yg: [m][2] the tagged granules of y, tag0 the tag of
 // iteration 0 (tags never repeat on a handle); sync: kCgpSyncWords barrier words, epoch0: the barriers they have
-// counted so far (one per iteration of earlier launches); oseg: also write this solve's coarse segments tl.Oseg (the
-// E build behind the CG then skips k_tl_erow);
+// counted so far (one per iteration of earlier launches); oseg bit 0: also write this solve's coarse segments tl.Oseg
+// (the E build behind the CG then skips k_tl_erow), bit 1 (tests, INSFM_DIAG=cgp_fault): the last workgroup leaves
+// at iteration 2 as if a barrier had timed out;
 // trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
 // of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
 // barriers (workgroup 0).
-template <int NB>
+template <int NB, bool DET>
 __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __restrict__ nbr_ptr,
                                                           const int* __restrict__ nbr_j, const double* __restrict__ Sn,
                                                           const double* __restrict__ Lf, CgBufs cg, TlBufs tl,
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
                                                           double* wx, unsigned long long* yg, unsigned tag0,
-                                                          unsigned* sync, unsigned epoch0, int oseg, double* trace) {
+                                                          unsigned* sync, unsigned epoch0, int oseg, unsigned long long* rung,
+                                                          unsigned long long* cgran, double* trace) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
     constexpr int NG = NB / 8;                          // gather loads per wave and iteration
     constexpr int RPT = (kCoarseMax + kCgpThreads - 1) / kCgpThreads;  // coarse entries per thread (LDS fills)
     __shared__ double Aseg[kCgpRows][kCgpSegMax][BS];  // A_ic of the row's segments, a-major
     __shared__ double wg[kCgpWaves][NB][D];            // the neighbours' w of the wave's blocks (gathered per iteration)
-    __shared__ double rs[kCoarseMax];                  // the restriction R of the iteration
+    // the restriction R of the iteration; DET: the 12 cluster sums (gamma, delta, rho partials, R) of every cluster
+    __shared__ double rs[DET ? 12 * kCgpMaxClusters : kCoarseMax];
     __shared__ double ys[kCoarseMax];                  // y of the iteration
     __shared__ double Lrow[kCgpRows][D * D];           // L_i (row a, column k)
     __shared__ double Zrow[kCgpRows][BS];              // Z~_i (row a, column k)
@@ -203,9 +248,15 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
     }
     __syncthreads();
-    // A_ic: lane (a, b) sums S~_ij[a][b] Z~_j[b][q] over the segment's blocks, then adds them into Aseg (LDS atomics).  Segment boundaries are wave-uniform; the Z~ rows
-    // of eight blocks are loaded together ahead of their products.
+    if (trace && blockIdx.x == 0 && t == 0) trace[578] = (double)wall_clock64();  // (blocks issued, LDS tables in)
+    // A_ic: lane (a, b) sums S~_ij[a][b] Z~_j[b][q] over the segment's blocks (segment boundaries are wave-uniform); at
+    // the segment's end the eight b lanes are summed by a fixed butterfly and lane (a, 0) writes row a of A_ic (one wave
+    // per row: each segment is written once, in a fixed order).  The Z~_j rows of ZC blocks at a time are staged in the
+    // wave's gather buffer by coalesced loads (all in flight together), then read back per lane.
     if (nk > 0) {
+        constexpr int ZC = NB * D / BS;            // blocks per staging chunk (14 for NB = 128)
+        constexpr int ZU = (ZC * BS + 63) / 64;    // coalesced loads per lane and chunk
+        double* zs = &wg[wv][0][0];
         int cur = 0;
         while (cur < nseg && tl.seg[s0 + cur].z <= 0) ++cur;
         int send = cur < nseg ? tl.seg[s0 + cur].z : 1 << 30;
@@ -216,33 +267,60 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (cur < kCgpSegMax) {
 #pragma unroll
                 for (int q = 0; q < MC; ++q) {
-                    __hip_atomic_fetch_add(&Aseg[rl][cur][a8 * MC + q], za[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    double v = za[q];
+                    v += __shfl_xor(v, 1, 64);
+                    v += __shfl_xor(v, 2, 64);
+                    v += __shfl_xor(v, 4, 64);
+                    if (b8 == 0) Aseg[rl][cur][a8 * MC + q] = v;
                     za[q] = 0.0;
                 }
             }
             ++cur;
             send = cur < nseg ? tl.seg[s0 + cur].z : 1 << 30;
         };
-        constexpr int CH = 8;
+        // (the blocks are re-read from memory here -- L2 / MALL-hot behind the register loads above: a loop over the
+        // register copies would have to be unrolled over all NB blocks, too large with the segment flushes)
+        for (int k0 = 0; k0 < nk; k0 += ZC) {
+            double zl[ZU], sv[ZC];
 #pragma unroll
-        for (int k0 = 0; k0 < NB; k0 += CH) {
-            if (k0 >= nk) continue;
-            double zv[CH][MC];
-#pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                const double* zr = tl.Zt + ((size_t)jn[wv][k0 + c] * D + b8) * MC;
-#pragma unroll
-                for (int q = 0; q < MC; ++q) zv[c][q] = zr[q];
+            for (int u = 0; u < ZU; ++u) {
+                const int e = min(lane + 64 * u, ZC * BS - 1), c = e / BS;
+                zl[u] = tl.Zt[(size_t)jn[wv][min(k0 + c, NB - 1)] * BS + (e - c * BS)];
             }
 #pragma unroll
-            for (int c = 0; c < CH; ++c) {
-                const int k = k0 + c;
-                if (k < nk) {
-                    while (k >= send) flush();
+            for (int c = 0; c < ZC; ++c) sv[c] = Sn[(size_t)(n0 + min(k0 + c, nk - 1)) * (D * D) + lane];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
-                    for (int q = 0; q < MC; ++q) za[q] += sreg[k] * zv[c][q];
-                }
+            for (int u = 0; u < ZU; ++u)
+                if (lane + 64 * u < ZC * BS) zs[lane + 64 * u] = zl[u];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // two blocks' Z~ rows read ahead of their products (see P2)
+#pragma unroll
+            for (int c = 0; c < ZC; c += 2) {
+                const int c1 = min(c + 1, ZC - 1);
+                const double* zr0 = zs + c * BS + b8 * MC;
+                const double* zr1 = zs + c1 * BS + b8 * MC;
+                double z0[MC], z1[MC];
+#pragma unroll
+                for (int q = 0; q < MC; ++q) { z0[q] = zr0[q]; z1[q] = zr1[q]; }
+                __builtin_amdgcn_sched_barrier(0);
+                const int kk = k0 + c;
+                if (kk >= nk) break;
+                while (kk >= send) flush();
+#pragma unroll
+                for (int q = 0; q < MC; ++q) za[q] += sv[c] * z0[q];
+                if (c + 1 >= ZC || kk + 1 >= nk) break;
+                while (kk + 1 >= send) flush();
+#pragma unroll
+                for (int q = 0; q < MC; ++q) za[q] += sv[c1] * z1[q];
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         flush();
     }
@@ -255,9 +333,10 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     bool alive = true;
     int it = 0;
     __syncthreads();  // Aseg complete
+    if (trace && blockIdx.x == 0 && t == 0) trace[579] = (double)wall_clock64();  // (A_ic complete)
     // the coarse matrix's row segments of this solve for the E build that runs behind the CG (k_tl_erow's outputs:
     // Z~_i^T A_ic, plus Z~_i^T Z~_i on the own-cluster segment, in k_tl_erow's order of additions)
-    if (oseg && has_row) {
+    if ((oseg & 1) && has_row) {
         const int ns = min(nseg, kCgpSegMax);
         for (int sg = 0; sg < ns; ++sg) {
             const int own_seg = tl.seg[s0 + sg].w;
@@ -279,16 +358,83 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         trace[257] = (double)wall_clock64();
     }
     for (;; ++it) {
+        if ((oseg & 2) && it == 2 && blockIdx.x == gridDim.x - 1) {  // (fault injection: see above)
+            if (t == 0) __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            alive = false;
+            break;
+        }
+        if (trace && t == 0 && it == kCgpTraceIt && blockIdx.x < 256) trace[772 + blockIdx.x] = (double)wall_clock64();
         // ======== P1 ========
         // every load of the phase is issued before the first wait: the scalar partials, this wave's gathers (lane
         // (a, b) loads entry b of the w of block 8 g + a), the restriction (all threads, into LDS), the E^-1 row
         const int b0 = it % 3;  // partial sums of this iteration (P2 of it - 1 added them)
-        const double* G = tl.Gacc + (size_t)b0 * 3 * nc;
+        const unsigned tg = tag0 + (unsigned)it;
         double gl[3][LNC];
+        if constexpr (DET) {
+            // cluster owners (wave c for cluster c): the cluster's 12 partials of this iteration summed in a fixed order
+            // (iteration 0: the setup's row partials in cluster order; then the tagged partials of the cluster's
+            // workgroup runs, in run order, kCgpRunBatch loads in flight), published as tagged granules in the
+            // iteration's parity buffer.  No grid barrier: a workgroup holding every cluster's sums of this iteration
+            // knows every row finished the previous one (each stored its w before its run's partials).
+            unsigned long long* cgi = cgran + (size_t)(it & 1) * 2 * 12 * kCgpMaxClusters;
+            const int l12 = min(lane, 11);
+            bool ok = true;
+            for (int c = gw; ok && c < nc; c += gridDim.x * kCgpWaves) {
+                const int p0 = tl.cl_ptr[c], p1 = tl.cl_ptr[c + 1];
+                double v = 0.0;
+                if (it == 0) {
+                    for (int pb = p0; pb < p1; pb += kCgpRunBatch) {
+                        double x[kCgpRunBatch];
 #pragma unroll
-        for (int q = 0; q < LNC; ++q) {
-            const int l = min(lane + 64 * q, nc - 1);
-            gl[0][q] = ld_sc1(G + l); gl[1][q] = ld_sc1(G + nc + l); gl[2][q] = ld_sc1(G + 2 * nc + l);
+                        for (int q = 0; q < kCgpRunBatch; ++q) {
+                            const int p = min(pb + q, p1 - 1);
+                            x[q] = l12 < 3 ? tl.gd[(size_t)l12 * C + p] : tl.rowR[(size_t)p * MC + (l12 - 3)];
+                        }
+#pragma unroll
+                        for (int q = 0; q < kCgpRunBatch; ++q)
+                            if (pb + q < p1) v += x[q];
+                    }
+                } else {
+                    for (int pb = p0; pb < p1;) {
+                        int hp[kCgpRunBatch], idx[kCgpRunBatch];
+                        double x[kCgpRunBatch];
+                        unsigned skip = 0;
+                        int p = pb;
+#pragma unroll
+                        for (int q = 0; q < kCgpRunBatch; ++q) {  // run heads: p0, then every multiple of kCgpRows
+                            hp[q] = p;
+                            idx[q] = min(p, p1 - 1) * 12 + l12;
+                            x[q] = 0.0;
+                            if (p >= p1) skip |= 1u << q;
+                            else p = (p / kCgpRows + 1) * kCgpRows;
+                        }
+                        if (!poll_wave(rung, idx, x, tg, sync, skip)) { ok = false; break; }
+#pragma unroll
+                        for (int q = 0; q < kCgpRunBatch; ++q)
+                            if (hp[q] < p1) v += x[q];
+                        pb = p;
+                    }
+                }
+                if (ok && lane < 12) put_y(cgi, c * 12 + lane, tg, v);
+            }
+            if (__syncthreads_or(!ok)) { alive = false; break; }
+            // every workgroup: all clusters' sums into LDS (rs), one poll for the scalars and the restriction
+            if (!poll_tagged<12 * kCgpMaxClusters>(cgi, [](int k) { return k; }, rs, 12 * nc, tg, sync)) {
+                alive = false;
+                break;
+            }
+#pragma unroll
+            for (int q = 0; q < LNC; ++q) {
+                const int c = min(lane + 64 * q, nc - 1);
+                gl[0][q] = rs[c * 12]; gl[1][q] = rs[c * 12 + 1]; gl[2][q] = rs[c * 12 + 2];
+            }
+        } else {
+            const double* G = tl.Gacc + (size_t)b0 * 3 * nc;
+#pragma unroll
+            for (int q = 0; q < LNC; ++q) {
+                const int l = min(lane + 64 * q, nc - 1);
+                gl[0][q] = ld_sc1(G + l); gl[1][q] = ld_sc1(G + nc + l); gl[2][q] = ld_sc1(G + 2 * nc + l);
+            }
         }
         const double* wsrc = (it == 0 ? cg.w[0] : wx + (size_t)(it & 1) * C * D) + b8;
         double wv8[NG];
@@ -297,7 +443,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         const double* Rv = tl.Racc + (size_t)b0 * m;
         double rv[RPT];
 #pragma unroll
-        for (int q = 0; q < RPT; ++q) rv[q] = use ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
+        for (int q = 0; q < RPT; ++q) rv[q] = (use && !DET) ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
         double ev[LPL];
         if (use && gw < m) {
 #pragma unroll
@@ -323,20 +469,18 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             trace[4 * it] = gam; trace[4 * it + 1] = del; trace[4 * it + 2] = rho; trace[4 * it + 3] = done;
             trace[258 + it] = (double)wall_clock64();
         }
+        // the status for the host (the progress word only every 8th iteration: it serves the host's stall deadline,
+        // and a store to host memory holds the storing wave's next vmcnt(0) for a PCIe round trip)
         if (blockIdx.x == 0 && t == 0) {
             if (done) {
                 cg.status[1] = it;
                 cg.status[0] = done;
-            } else {
-                cg.hist[2 * it] = alpha;
-                cg.hist[2 * it + 1] = gam;
-                if (it == 0) cg.hist[2 * (maxit + 1)] = bb;
             }
             if (cg.prog) {
                 if (done) {
                     __hip_atomic_store(cg.prog + 2, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __hip_atomic_store(cg.prog + 1, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-                } else {
+                } else if ((it & 7) == 0) {
                     __hip_atomic_store(cg.prog + 0, it + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 }
             }
@@ -347,26 +491,34 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         h_gam = gam;
         // the partial buffers of iteration it + 2 (last read in P1 of it - 1, before the barrier ending P2 of it - 1;
         // first added to in P2 of it + 1, behind the barrier ending this P2) are cleared now
-        if (blockIdx.x == 0) {
+        if (!DET) {  // (spread over the workgroups: at most one store per thread)
             double* Rn = tl.Racc + (size_t)((it + 2) % 3) * m;
             double* Gn = tl.Gacc + (size_t)((it + 2) % 3) * 3 * nc;
-            for (int q = t; q < m; q += kCgpThreads) st_sc1(Rn + q, 0.0);
-            for (int q = t; q < 3 * nc; q += kCgpThreads) st_sc1(Gn + q, 0.0);
+            for (int q = blockIdx.x * kCgpThreads + t; q < m + 3 * nc; q += gridDim.x * kCgpThreads)
+                st_sc1(q < m ? Rn + q : Gn + (q - m), 0.0);
         }
 #pragma unroll
         for (int g = 0; g < NG; ++g) wg[wv][8 * g + a8][b8] = wv8[g];
-        if (use) {
+        if (use && !DET) {
 #pragma unroll
             for (int q = 0; q < RPT; ++q)
                 if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
         }
         __syncthreads();
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[580 + 3 * it] = (double)wall_clock64();
         // coarse row gw: y = E^-1 R (k_tl_pc_cl's products and butterfly)
         if (use && gw < m) {
+            double rq[LPL];
+#pragma unroll
+            for (int q = 0; q < LPL; ++q) {  // (DET: entry k of R is record k / 9's value 3 + k % 9)
+                const int k = min(lane + 64 * q, m - 1);
+                rq[q] = rs[DET ? (k / 9) * 12 + 3 + k % 9 : k];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             double sy = 0.0;
 #pragma unroll
             for (int q = 0; q < LPL; ++q)
-                if (lane + 64 * q < m) sy += ev[q] * rs[lane + 64 * q];
+                if (lane + 64 * q < m) sy += ev[q] * rq[q];
             const double y = wave_sum(sy);
             if (lane == 0) put_y(yg, gw, tag0 + (unsigned)it, y);
         }
@@ -378,12 +530,23 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             const double y = wave_sum(sy);
             if (lane == 0) put_y(yg, g, tag0 + (unsigned)it, y);
         }
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[581 + 3 * it] = (double)wall_clock64();
         // the row's S~ w (lane a < 8 ends with entry a)
         double sw = 0.0;
         if (has_row) {
+            // the gathered w read back 16 blocks at a time, all reads in flight before their products (one read
+            // per block waited on its own left the LDS latency in series: 2.5 us per iteration)
             double ac4[4] = {0.0, 0.0, 0.0, 0.0};  // four independent chains
 #pragma unroll
-            for (int k = 0; k < NB; ++k) ac4[k & 3] += sreg[k] * wg[wv][k][b8];
+            for (int k0 = 0; k0 < NB; k0 += 16) {
+                double w16[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) w16[c] = wg[wv][k0 + c][b8];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) ac4[c & 3] += sreg[k0 + c] * w16[c];
+                __builtin_amdgcn_sched_barrier(0);
+            }
             double acc = (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
             acc += __shfl_xor(acc, 1, 64);
             acc += __shfl_xor(acc, 2, 64);
@@ -404,30 +567,43 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             const double w_ = V[VW + la];
             double mi = w_, ay = 0.0;
             if (use) {
+                // (LDS operands read as a batch ahead of their products, here and below: under this kernel's register
+                // pressure the compiler otherwise waits on each read before issuing the next)
+                double z9[MC], y9[MC];
+#pragma unroll
+                for (int k = 0; k < MC; ++k) { z9[k] = Zrow[rl][la * MC + k]; y9[k] = ys[ci * MC + k]; }
+                __builtin_amdgcn_sched_barrier(0);
                 double sz = 0.0;
 #pragma unroll
-                for (int k = 0; k < MC; ++k) sz += Zrow[rl][la * MC + k] * ys[ci * MC + k];
+                for (int k = 0; k < MC; ++k) sz += z9[k] * y9[k];
                 mi += sz;
                 // lane (j, a) = (lane >> 3, lane & 7): row a of the segments j, j + 8, ..., then summed over j
                 const int ns = min(nseg, kCgpSegMax);
                 for (int sg = lane >> 3; sg < ns; sg += 8) {
                     const double* yc = ys + segc[rl][sg] * MC;
                     const double* A = &Aseg[rl][sg][la * MC];
+                    double a9[MC], c9[MC];
 #pragma unroll
-                    for (int k = 0; k < MC; ++k) ay += A[k] * yc[k];
+                    for (int k = 0; k < MC; ++k) { a9[k] = A[k]; c9[k] = yc[k]; }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int k = 0; k < MC; ++k) ay += a9[k] * c9[k];
                 }
                 ay += __shfl_xor(ay, 8, 64);
                 ay += __shfl_xor(ay, 16, 64);
                 ay += __shfl_xor(ay, 32, 64);
             }
+            const double vz = V[VZ + la], vq = V[VQ + la], vs = V[VS + la], vu = V[VU + la], vp = V[VP + la];
+            const double vx = V[VX + la], vr = V[VR + la];
+            __builtin_amdgcn_sched_barrier(0);
             const double prod = mi + (sw + ay);  // (the diagonal block of S~ is I)
-            const double zn = prod + be * V[VZ + la];
-            const double qn = mi + be * V[VQ + la];
-            const double sn = w_ + be * V[VS + la];
-            const double pn = V[VU + la] + be * V[VP + la];
-            const double xn = V[VX + la] + alpha * pn;
-            const double rn = V[VR + la] - alpha * sn;
-            const double un = V[VU + la] - alpha * qn;
+            const double zn = prod + be * vz;
+            const double qn = mi + be * vq;
+            const double sn = w_ + be * vs;
+            const double pn = vu + be * vp;
+            const double xn = vx + alpha * pn;
+            const double rn = vr - alpha * sn;
+            const double un = vu - alpha * qn;
             const double wn = w_ - alpha * zn;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -435,41 +611,63 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (lane < D) {
                 V[VZ + la] = zn; V[VQ + la] = qn; V[VS + la] = sn; V[VP + la] = pn;
                 V[VX + la] = xn; V[VR + la] = rn; V[VU + la] = un; V[VW + la] = wn;
+                // the row's new w for the neighbours (first: its write-back overlaps the partials below)
+                st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, wn);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // partials of iteration it + 1: r.u, w.u, ||L r||^2 and the restriction Z~_i^T w (k_tl_pspmv's order)
             double g0 = 0.0, g1 = 0.0, g2 = 0.0, rr = 0.0;
-            if (lane < D) {
-                g0 = rn * un;
-                g1 = wn * un;
-                double lr = 0.0;
+            {
+                const int lc = min(lane, MC - 1);
+                double l8[D], r8[D], z8[D], w8[D];
 #pragma unroll
-                for (int k = 0; k < D; ++k)
-                    if (k <= lane) lr += Lrow[rl][lane * D + k] * V[VR + k];
-                g2 = lr * lr;
-            }
-            if (lane < MC) {
+                for (int k = 0; k < D; ++k) {
+                    l8[k] = Lrow[rl][la * D + k];
+                    r8[k] = V[VR + k];
+                    z8[k] = Zrow[rl][k * MC + lc];
+                    w8[k] = V[VW + k];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (lane < D) {
+                    g0 = rn * un;
+                    g1 = wn * un;
+                    double lr = 0.0;
 #pragma unroll
-                for (int a = 0; a < D; ++a) rr += Zrow[rl][a * MC + lane] * V[VW + a];
+                    for (int k = 0; k < D; ++k)
+                        if (k <= lane) lr += l8[k] * r8[k];
+                    g2 = lr * lr;
+                }
+                if (lane < MC) {
+#pragma unroll
+                    for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
+                }
             }
             g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
             if (lane < MC) prt[rl][3 + lane] = rr;
-            if (lane < D) st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, wn);
         }
+        // DET: every wave's w stores complete before its run's partials are published (the consumers read w once they
+        // hold every cluster's sums of the next iteration)
+        if constexpr (DET) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // the first row of each cluster run of the workgroup adds the run's partials (rows in order) to the cluster
         if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3 + MC) {
             double v = prt[rl][lane];
             for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
-            const int bsel = (it + 1) % 3;
-            if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)bsel * 3 * nc + (size_t)lane * nc + ci, v);
-            else unsafeAtomicAdd(tl.Racc + (size_t)bsel * m + (size_t)ci * MC + (lane - 3), v);
+            if constexpr (DET) {
+                put_y(rung, pos * 12 + lane, tg + 1, v);  // (at the run's head position: read by the owner of ci)
+            } else {
+                const int bsel = (it + 1) % 3;
+                if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)bsel * 3 * nc + (size_t)lane * nc + ci, v);
+                else unsafeAtomicAdd(tl.Racc + (size_t)bsel * m + (size_t)ci * MC + (lane - 3), v);
+            }
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 2] = (double)wall_clock64();
-        if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
+        if (trace && t == 0 && it == kCgpTraceIt && blockIdx.x < 256) trace[1028 + blockIdx.x] = (double)wall_clock64();
+        if constexpr (!DET)
+            if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 3] = (double)wall_clock64();
     }
     if (!alive && blockIdx.x == 0 && t == 0) {
@@ -480,8 +678,9 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             __hip_atomic_store(cg.prog + 1, 4, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    // the scaled solution for k_cg_finish, and the vectors as the launch path leaves them
-    if (has_row) {
+    // the scaled solution for k_cg_finish, and the vectors as the launch path leaves them (not after an abort: the
+    // host repeats the solve on the launch path from r0, which this kernel left untouched)
+    if (has_row && alive) {
         double* dst = lane < 8 ? cg.r[0] : lane < 16 ? tl.u : lane < 24 ? cg.w[0] : lane < 32 ? cg.w[1]
                     : lane < 40 ? cg.r[1] : lane < 48 ? cg.s[0] : lane < 56 ? cg.p : cg.x;
         dst[own] = V[lane];

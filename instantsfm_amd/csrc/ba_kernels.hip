@@ -1562,8 +1562,13 @@ struct insfm_ba {
     // [C][8], the coarse vector [kCoarseMax], the grid-barrier words; cgp_defer: the side chain of slot cgp_slot is
     // issued behind the CG (k_tl_cgp holds every SIMD of its CUs, so a chain beside it would crawl on the rest)
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
+    bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
+    unsigned long long* cgp_runs = nullptr;   // [grid * 4][12] tagged granule pairs: the cluster runs' partials (cgp_det)
+    unsigned long long* cgp_cgran = nullptr;  // [2][kCgpMaxClusters][12] granule pairs of the cluster sums (cgp_det)
     unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
+    int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
+    bool cgp_lost = false;        // the last k_tl_cgp timed out at a grid barrier (another process holds CUs)
     double* cgp_trace = nullptr;  // INSFM_DIAG=cgp_trace: [64][4] of the last solve, printed to stderr
     // row-partitioned multi-rank CG (ba_xpart.h; insfm_ba_cg_window / insfm_ba_cg_attach)
     bool xpart = false;
@@ -2202,21 +2207,33 @@ void launch_tl_iter_x(insfm_ba* h, int it, int maxit, double tol2) {
 // launch_tl_iter(0), the barrier words cleared, one launch for every iteration.
 int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     constexpr int D = 8;
-    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
+    // the fixed-order variant starts from the setup's row partials (tl.gd / tl.rowR), also on a handle that has the
+    // atomic cluster buffers
+    TlBufs t0 = h->tl;
+    if (h->cgp_det) t0.Racc = t0.Gacc = nullptr;
+    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, t0,
                                                                h->tl.Einv);
     k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
-                                                          h->cg, h->tl, XPart{});
+                                                          h->cg, t0, XPart{});
     if (h->cgp_epochs > (1u << 24)) {  // (counter headroom: zero them now and then; an abort zeroes them too)
         HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
         h->cgp_epochs = 0;
     }
+    // INSFM_DIAG=cgp_fault (tests): the first launch of the process aborts at iteration 2
+    static std::atomic<int> faults{diag("cgp_fault") ? 1 : 0};
+    const bool fault = faults.load() > 0 && faults.fetch_sub(1) > 0;
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->Sn,
                            h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg, h->cgp_tag, h->cgp_sync,
-                           h->cgp_epochs, h->cgp_defer ? 1 : 0, h->cgp_trace);
+                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_cgran, h->cgp_trace);
     };
-    if (h->cgp_nb == 64) go(k_tl_cgp<64>);
-    else go(k_tl_cgp<128>);
+    if (h->cgp_det) {
+        if (h->cgp_nb == 64) go(k_tl_cgp<64, true>);
+        else go(k_tl_cgp<128, true>);
+    } else {
+        if (h->cgp_nb == 64) go(k_tl_cgp<64, false>);
+        else go(k_tl_cgp<128, false>);
+    }
     return launch_err(h, "k_tl_cgp");
 }
 
@@ -2342,25 +2359,57 @@ int run_tl_cg(insfm_ba* h, int* st) {
     if (h->cgp_nb) {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
         h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
         if (st[0] == 1 || st[0] == 2) {
-            h->cgp_epochs += (unsigned)st[1];
+            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1];  // (the DET variant has no grid barrier)
         } else {
             HIPCHK(hipStreamSynchronize(h->stream));
             HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
             h->cgp_epochs = 0;
+            // a barrier timed out: the grid was not resident at once (another process's kernels held CUs).  A single
+            // rank drops the persistent CG for good and run_solve repeats this solve on the launch path; a rank of a
+            // replicated multi-rank CG cannot (its peers would compute a dc that differs in rounding) and reports it.
+            if (st[0] == 4 && h->d.world_size <= 1) {
+                std::fprintf(stderr, "[insfm] k_tl_cgp: a grid barrier timed out (the GPU is shared with another "
+                                     "process?); this handle continues on the launch-per-iteration CG\n");
+                h->cgp_nb = 0;
+                h->cgp_lost = true;
+            }
         }
     }
     if (h->cgp_nb && h->cgp_trace) {
-        double tr[256 + 2 + 64 + 4 * 64];
+        double tr[kCgpTraceLen];
         HIPCHK(hipMemcpy(tr, h->cgp_trace, sizeof(tr), hipMemcpyDeviceToHost));
         const int n = std::min(st[1], 63);
-        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d: setup %.1f us, iterations %.1f us (%.2f us each)\n",
-                     st[0], st[1], st[2], 0.01 * (tr[257] - tr[256]), 0.01 * (tr[258 + n] - tr[257]),
+        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d: setup %.1f us (blocks + tables %.1f, A %.1f, "
+                     "rest %.1f), iterations %.1f us (%.2f us each)\n",
+                     st[0], st[1], st[2], 0.01 * (tr[257] - tr[256]), 0.01 * (tr[578] - tr[256]),
+                     0.01 * (tr[579] - tr[578]), 0.01 * (tr[257] - tr[579]), 0.01 * (tr[258 + n] - tr[257]),
                      n > 0 ? 0.01 * (tr[258 + n] - tr[258]) / n : 0.0);
-        for (int k = 0; k <= n; ++k)
-            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g t %.1f us | P1 %.2f B1 %.2f P2 %.2f "
-                         "B2 %.2f\n", k, tr[4 * k], tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3], 0.01 * (tr[258 + k] - tr[256]),
+        for (int k = 0; k <= n; ++k) {
+            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g t %.1f us | loads %.2f P1 %.2f y %.2f "
+                         "P2 %.2f B2 %.2f\n", k, tr[4 * k], tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3], 0.01 * (tr[258 + k] - tr[256]),
+                         k > 0 ? 0.01 * (tr[258 + k] - tr[322 + 4 * (k - 1) + 3]) : 0.0,
                          0.01 * (tr[322 + 4 * k] - tr[258 + k]), 0.01 * (tr[323 + 4 * k] - tr[322 + 4 * k]),
                          0.01 * (tr[324 + 4 * k] - tr[323 + 4 * k]), 0.01 * (tr[325 + 4 * k] - tr[324 + 4 * k]));
+            if (k < n)
+                std::fprintf(stderr, "[insfm cgp]        P1 split: fills + workgroup barrier %.2f, y %.2f, S~w %.2f\n",
+                             0.01 * (tr[580 + 3 * k] - tr[258 + k]), 0.01 * (tr[581 + 3 * k] - tr[580 + 3 * k]),
+                             0.01 * (tr[322 + 4 * k] - tr[581 + 3 * k]));
+        }
+        const int G = std::min(h->cgp_grid, 256);
+        if (st[1] > kCgpTraceIt + 1 && G > 0) {  // every workgroup's start and end of iteration kCgpTraceIt
+            double s0 = tr[772], s1 = tr[772];
+            for (int b = 0; b < G; ++b) { s0 = std::min(s0, tr[772 + b]); s1 = std::max(s1, tr[772 + b]); }
+            std::vector<int> ord(G);
+            for (int b = 0; b < G; ++b) ord[b] = b;
+            std::sort(ord.begin(), ord.end(), [&](int a, int b) { return tr[1028 + a] > tr[1028 + b]; });
+            std::fprintf(stderr, "[insfm cgp] it %d per workgroup: starts within %.2f us; arrival at the barrier "
+                         "(us after the first start): median %.2f, last %.2f; latest:", kCgpTraceIt, 0.01 * (s1 - s0),
+                         0.01 * (tr[1028 + ord[G / 2]] - s0), 0.01 * (tr[1028 + ord[0]] - s0));
+            for (int q = 0; q < std::min(G, 8); ++q)
+                std::fprintf(stderr, " wg %d (%.2f, start %.2f)", ord[q], 0.01 * (tr[1028 + ord[q]] - s0),
+                             0.01 * (tr[772 + ord[q]] - s0));
+            std::fprintf(stderr, "\n");
+        }
     }
     return 0;
 }
@@ -2488,6 +2537,11 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         int* st = reinterpret_cast<int*>(h->host_res + 8);
         rc = (h->tlon && h->prog_host) ? run_tl_cg(h, st) : run_bj_cg(h, st);
         if (rc) return rc;
+        if (h->cgp_lost) {  // k_tl_cgp aborted (it left r0 alone): the CG again from the basis, launch path
+            h->cgp_lost = false;
+            HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+            if ((rc = run_tl_basis(h, cams, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
+        }
         if (st[0] != 1) {
             h->err = std::string("PCG ") +
                      (st[0] == 2 ? "breakdown"
@@ -3630,13 +3684,20 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             std::fprintf(stderr, "[insfm create] k_tl_cgp eligibility: D %d, atomic sums %d, progress %d, max row %d, "
                          "cluster order %d, max segments %d\n", D, tl.Racc != nullptr, h->prog_host != nullptr, maxlen,
                          (int)in_order, maxseg);
-        if (D == 8 && tl.Racc && h->prog_host && nb && in_order && maxseg <= kCgpSegMax && !diag("no_cgp")) {
+        // non-deterministic single rank: per-cluster atomic sums (tl.Racc); otherwise (deterministic mode, or every
+        // rank of a replicated multi-rank CG) the fixed-order variant
+        // (INSFM_DIAG=cgp_det: the fixed-order variant on a non-deterministic handle too, for A/B runs)
+        const bool det = tl.Racc == nullptr || diag("cgp_det");
+        if (D == 8 && h->prog_host && nb && in_order && maxseg <= kCgpSegMax && !diag("no_cgp")) {
             int dev = 0, ncu = 0, per_cu = 0;
             hipError_t ce = hipGetDevice(&dev);
             if (ce == hipSuccess) ce = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             if (ce == hipSuccess)
                 ce = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &per_cu, nb == 64 ? (const void*)k_tl_cgp<64> : (const void*)k_tl_cgp<128>, kCgpThreads, 0);
+                    &per_cu,
+                    det ? (nb == 64 ? (const void*)k_tl_cgp<64, true> : (const void*)k_tl_cgp<128, true>)
+                        : (nb == 64 ? (const void*)k_tl_cgp<64, false> : (const void*)k_tl_cgp<128, false>),
+                    kCgpThreads, 0);
             if (ce == hipSuccess && per_cu >= 1 && grid <= ncu) {
                 if ((rc = dd(&h->cgp_wx, 2 * cd))) return fail(rc, "");
                 if ((rc = dalloc(h, (void**)&h->cgp_yg, sizeof(unsigned long long) * 2 * kCoarseMax))) return fail(rc, "");
@@ -3645,9 +3706,20 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 if ((rc = dalloc(h, (void**)&h->cgp_sync, sizeof(unsigned) * kCgpSyncWords))) return fail(rc, "");
                 if (hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "cgp barrier words");
-                if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, 256 + 2 + 64 + 4 * 64))) return fail(rc, "");
+                if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, kCgpTraceLen))) return fail(rc, "");
+                if (det) {
+                    const size_t nr = sizeof(unsigned long long) * 2 * 12 * (size_t)grid * kCgpRows;
+                    const size_t ng = sizeof(unsigned long long) * 2 * 2 * 12 * (size_t)kCgpMaxClusters;
+                    if ((rc = dalloc(h, (void**)&h->cgp_runs, nr)) || (rc = dalloc(h, (void**)&h->cgp_cgran, ng)))
+                        return fail(rc, "");
+                    if (hipMemsetAsync(h->cgp_runs, 0, nr, h->stream) != hipSuccess ||
+                        hipMemsetAsync(h->cgp_cgran, 0, ng, h->stream) != hipSuccess)
+                        return fail(INSFM_BA_EHIP, "cgp cluster granules");
+                }
+                h->cgp_det = det;
                 h->cgp_nb = nb;
                 h->cgp_grid = grid;
+                h->cgp_slots = per_cu * ncu;
                 if (diag("create"))
                     std::fprintf(stderr, "[insfm create] k_tl_cgp<%d>: %d workgroups, %d CUs, %d per CU\n", nb, grid, ncu,
                                  per_cu);
@@ -3691,12 +3763,24 @@ int insfm_ba_set_exchange(insfm_ba* h, double* buf, int64_t count) {
     return INSFM_BA_OK;
 }
 
+int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks) {
+    if (!h || ranks < 1) return INSFM_BA_EINVAL;
+    if (h->cgp_nb && (long long)ranks * h->cgp_grid > (long long)h->cgp_slots) {
+        if (diag("create"))
+            std::fprintf(stderr, "[insfm create] %d ranks per GPU: k_tl_cgp would need %lld of %d workgroup slots; "
+                         "launch path\n", ranks, (long long)ranks * h->cgp_grid, h->cgp_slots);
+        h->cgp_nb = 0;
+    }
+    return INSFM_BA_OK;
+}
+
 int insfm_ba_cg_window(insfm_ba* h, void* ipc_handle) {
     if (!h || !ipc_handle) return INSFM_BA_EINVAL;
-    if (h->kind != 0 || h->d.world_size < 2 || !h->tlon || h->tl.Racc || h->xwin || h->cgp_nb) {
+    if (h->kind != 0 || h->d.world_size < 2 || !h->tlon || h->tl.Racc || h->xwin) {
         h->err = "cg_window: needs a multi-rank two-level handle (precond 1) that has no window yet";
         return INSFM_BA_EINVAL;
     }
+    h->cgp_nb = 0;  // (the partitioned launch path replaces the replicated persistent CG)
     const int C = h->C, D = h->D, MC = D + 1, W = h->d.world_size;
     const long long region = (long long)C * D + 3LL * C + (long long)C * MC + 2;
     h->xoff_region[0] = 0;

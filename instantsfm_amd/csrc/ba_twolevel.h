@@ -330,7 +330,8 @@ __device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __res
 // every lane reads it back (one 16-B read per column pair, all lanes the same address); 2: timing only (no inversion,
 // results wrong); 3: all 256 threads, four entries each, the matrix ping-ponged through LDS; 4: one wave, 16 entries
 // per lane, pivot row / column through LDS without a workgroup barrier.  0, 1, 3 and 4 perform the same arithmetic in
-// the same order.
+// the same order.  (Round 4: a variant exchanging the pivot row and column by lane permutes instead of LDS was bitwise
+// equal and 8-10 % slower at m = 567-747, profiles/r4_v2/gj_pinv4_vs_pinv5.log, and was removed.)
 #ifndef GJ_PINV
 #define GJ_PINV 4
 #endif
@@ -412,44 +413,6 @@ __device__ bool gj_invert_block(double (*M)[kGS]) {
             }
             double piv = prow[par][p];
             const double aip = pcol[par][r];
-            if (!(piv > 0.0)) { bad = true; piv = 1.0; }
-            const double inv = 1.0 / piv;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (cb + j == p) {
-                    a[j] = (r == p) ? inv : -aip * inv;
-                } else {
-                    const double rpc = pr[j] * inv;
-                    a[j] = (r == p) ? rpc : __builtin_fma(-aip, rpc, a[j]);
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) M[r][cb + j] = a[j];
-    }
-    __syncthreads();
-    return bad;
-#elif GJ_PINV == 5
-    // one wave, the layout of variant 4 (lane l: row l & 31, columns 16 (l >> 5) .. +15), the pivot row and column
-    // exchanged by lane permutes (ds_bpermute) instead of LDS stores, a fence and loads: per pivot p every lane reads
-    // the pivot row's entries of its column half from lane p + 32 h and its row's pivot-column entry from lane
-    // r + 32 (p >> 4); the same arithmetic in the same order as variants 3 and 4.
-    static_assert(kGB == 32, "64 lanes = 32 rows x 2 column halves");
-    __syncthreads();
-    bool bad = false;
-    if (threadIdx.x < 64) {
-        const int l = threadIdx.x, r = l & 31, h = l >> 5, cb = 16 * h;
-        double a[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) a[j] = M[r][cb + j];
-#pragma unroll
-        for (int p = 0; p < kGB; ++p) {
-            const int hp = p >> 4, jp = p & 15;
-            double pr[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) pr[j] = __shfl(a[j], p + 32 * h, 64);
-            const double aip = __shfl(a[jp], r + 32 * hp, 64);
-            double piv = readlane_d(a[jp], p + 32 * hp);
             if (!(piv > 0.0)) { bad = true; piv = 1.0; }
             const double inv = 1.0 / piv;
 #pragma unroll

@@ -18,6 +18,19 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
                    pcg_max_iter=500, precond=1, cluster_size=14, exchange_chunks=4)
 
 
+def ranks_per_device(device, group=None):
+    """The most ranks of ``group`` that run on one GPU (host name + PCI address of each rank's device, all-gathered):
+    insfm_ba_set_ranks_per_device keeps the persistent CG only when that many of its grids fit on a GPU at once."""
+    import socket
+
+    import torch.distributed as dist
+    p = torch.cuda.get_device_properties(device)
+    me = (socket.gethostname(), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+    ids = [None] * dist.get_world_size(group)
+    dist.all_gather_object(ids, me, group=group)
+    return max(ids.count(x) for x in ids)
+
+
 def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
     """The C ABI's allreduce callback (insfm_ba_allreduce_fn) over torch.distributed.
 
@@ -176,6 +189,9 @@ class BundleAdjuster:
             n = L.insfm_ba_exchange_count(h)
             self._xbuf = torch.zeros(int(n), dtype=torch.float64, device=self.device)
             _capi.check(h, L.insfm_ba_set_exchange(h, ctypes.c_void_p(self._xbuf.data_ptr()), n))
+        if world_size > 1:
+            self.ranks_per_device = ranks_per_device(self.device, process_group)
+            _capi.check(h, L.insfm_ba_set_ranks_per_device(h, self.ranks_per_device))
 
     # ------------------------------------------------------------------------------------------------------------
     def close(self):

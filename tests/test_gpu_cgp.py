@@ -22,10 +22,10 @@ if not torch.cuda.is_available():  # pragma: no cover
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(diag):
+def run(diag, *extra, scenes="small,fine,config2"):
     env = dict(os.environ, INSFM_DIAG=diag)
-    p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cgp_check.py"), "--scenes", "small,fine,config2",
-                        "--steps", "4"], capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cgp_check.py"), "--scenes", scenes,
+                        "--steps", "4", *extra], capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
     assert p.returncode == 0, p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])["scenes"]
 
@@ -43,3 +43,36 @@ def test_cgp_matches_launch_path():
         for k, (la, lb) in enumerate(zip(sa["losses"], sb["losses"])):
             assert abs(la - lb) <= 1e-8 * abs(lb), (name, k, la, lb)
         assert all(abs(x - y) <= 1 for x, y in zip(sa["iters"], sb["iters"])), (name, sa["iters"], sb["iters"])
+
+
+def test_cgp_deterministic_variant():
+    """deterministic=True runs the fixed-order k_tl_cgp (cluster owners sum the workgroups' partials in a fixed order
+    and publish them as tagged granules; no atomics): two runs of each scene are bitwise equal, one launch per solve,
+    and the launch path's deterministic CG agrees to rounding (losses 1e-8, PCG iterations within one per step)."""
+    a = run("", "--det", "--repeat", "2", scenes="small,config2")
+    b = run("no_cgp", "--det", scenes="small,config2")
+    for name in ("small", "config2"):
+        s1, s2, sb = a[name], a[name + "#1"], b[name]
+        assert s1["launches"] == s1["trials"], s1
+        assert s1["losses_hex"] == s2["losses_hex"] and s1["params_sha"] == s2["params_sha"], (s1, s2)
+        for la, lb in zip(s1["losses"], sb["losses"]):
+            assert abs(la - lb) <= 1e-8 * abs(lb), (name, la, lb)
+        assert all(abs(x - y) <= 1 for x, y in zip(s1["iters"], sb["iters"])), (s1["iters"], sb["iters"])
+
+
+def test_cgp_abort_falls_back_to_launch_path():
+    """A k_tl_cgp whose grid barrier times out (INSFM_DIAG=cgp_fault: the process's first launch, the warm-up step's,
+    loses a workgroup at iteration 2 as if another process held its CU) raises the abort word; every workgroup leaves
+    without touching the CG vectors, the host repeats that solve on the launch path from the basis and keeps the
+    handle there.  The run then follows the launch path's trajectory (losses 1e-9 against INSFM_DIAG=no_cgp)."""
+    env = dict(os.environ, INSFM_DIAG="cgp_fault")
+    p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "cgp_check.py"), "--scenes", "config2", "--steps",
+                        "4"], capture_output=True, text=True, timeout=170, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "grid barrier timed out" in p.stderr, p.stderr[-3000:]
+    a = json.loads(p.stdout.strip().splitlines()[-1])["scenes"]["config2"]
+    b = run("no_cgp", scenes="config2")["config2"]
+    assert not any(a["failed"]), a
+    assert all(l > t for l, t in zip(a["launches"], a["trials"])), a  # launch path after the abort
+    for la, lb in zip(a["losses"], b["losses"]):
+        assert abs(la - lb) <= 1e-9 * abs(lb), (la, lb)

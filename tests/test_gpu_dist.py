@@ -22,11 +22,13 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run(nproc, backend, extra, timeout=600):
+def _run(nproc, backend, extra, timeout=600, diag=None):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc), "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(REPO, "tools", "dist_check.py"), "--backend", backend,
            "--same-device", *extra]
     env = dict(os.environ, OMP_NUM_THREADS="4")
+    if diag is not None:
+        env["INSFM_DIAG"] = diag
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=REPO)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-3000:]
     line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1]
@@ -79,8 +81,10 @@ def test_rccl_exchange_one_rank(chunks):
 def test_partitioned_cg_matches_replicated(extra):
     """Row-partitioned CG (insfm_ba_cg_window / _attach: each rank applies S~ to its own camera rows and writes their
     CG partials into every rank's IPC exchange window; 2 ranks sharing the one MI355X) against the replicated CG on the
-    same shards: bitwise the same losses and parameters on every rank, and the usual agreement with one GPU."""
-    rep = _run(2, "gloo", extra)
+    same shards: bitwise the same losses and parameters on every rank, and the usual agreement with one GPU.  The
+    partitioned CG is the launch-per-iteration path, so the replicated reference runs that path too (INSFM_DIAG=no_cgp:
+    the persistent k_tl_cgp sums S~ m in another order)."""
+    rep = _run(2, "gloo", extra, diag="no_cgp")
     part = _run(2, "gloo", extra + ["--cg-partition"])
     assert part["cg_partition"] and part["rows"][0] == 0 and 0 < part["rows"][1], part
     assert part["losses_hex"] == rep["losses_hex"], (part["losses_hex"], rep["losses_hex"])

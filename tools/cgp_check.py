@@ -4,6 +4,7 @@ read once per process): run this twice, once with each setting, and compare the 
 PCG iterations of a few non-deterministic steps, the CG launches per step (k_tl_cgp: one per trial), wall-clock LM
 steps per second.  Used by tests/test_gpu_cgp.py; `--steps` / `--scenes` for timing runs."""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -35,11 +36,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scenes", default="small,fine,config2")
     ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--det", action="store_true", help="deterministic mode (the fixed-order k_tl_cgp variant)")
+    ap.add_argument("--repeat", type=int, default=1, help="run each scene this many times (bitwise reproducibility)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     out = dict(env=os.environ.get("INSFM_DIAG", ""), scenes={})
-    for name in a.scenes.split(","):
+    for name in [n for n in a.scenes.split(",") for _ in range(a.repeat)]:
         prob, opts = scene(name)
+        if a.det:
+            opts = dict(opts, deterministic=True)
         eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                              device=dev, **opts)
         cg = torch.from_numpy(prob.cams_init.copy()).to(dev)
@@ -60,10 +65,12 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         _, nc = eng.clusters()
-        out["scenes"][name] = dict(losses=losses, iters=iters, launches=launches, trials=trials, failed=failed, nc=nc,
+        key = name if name not in out["scenes"] else f"{name}#{sum(k.split('#')[0] == name for k in out['scenes'])}"
+        out["scenes"][key] = dict(params_sha=hashlib.sha256(cg.cpu().numpy().tobytes() + pg.cpu().numpy().tobytes()).hexdigest(),
+                                   losses_hex=[float(x).hex() for x in losses],losses=losses, iters=iters, launches=launches, trials=trials, failed=failed, nc=nc,
                                    steps_per_s=a.steps / dt, D=eng.D)
         eng.close()
-        print(json.dumps(dict(scene=name, **out["scenes"][name])), file=sys.stderr, flush=True)
+        print(json.dumps(dict(scene=key, **out["scenes"][key])), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
 
 
