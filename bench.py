@@ -469,12 +469,21 @@ def solve_end_to_end(prob, dev):
     from instantsfm_amd.config.colmap import BUNDLE_ADJUSTER_OPTIONS
     from instantsfm_amd.processors.bundle_adjustment import TorchBA
     from instantsfm_amd.synth import to_scene
-    cams, ims, tracks = to_scene(prob)
-    ba = TorchBA(device=str(dev))
-    ba.Solve(cams, ims, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
+    # Two Solves on fresh copies of the scene: the first of a process maps fresh device memory and loads code objects
+    # (reported as first_*); the second is the steady state a caller that solves repeatedly (the mapper) sees, its
+    # engine taking the device buffers the first one parked in the library's cache.
+    first = None
+    for rep in range(2):
+        cams, ims, tracks = to_scene(prob)
+        ba = TorchBA(device=str(dev))
+        ba.Solve(cams, ims, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
+        if rep == 0:
+            first = dict(ba.timings)
     t = ba.timings
     host = t["pack_s"] + t["create_s"] + t["update_s"]
-    return {"solve_total_s": round(t["total_s"], 4), "pack_s": round(t["pack_s"], 4),
+    return {"first_solve_total_s": round(first["total_s"], 4), "first_create_s": round(first["create_s"], 4),
+            "first_update_s": round(first["update_s"], 4),
+            "solve_total_s": round(t["total_s"], 4), "pack_s": round(t["pack_s"], 4),
             "create_s": round(t["create_s"], 4), "steps_s": round(t["steps_s"], 4),
             "update_s": round(t["update_s"], 4), "steps": t["steps"], "host_frac": round(host / t["total_s"], 4),
             "pack_phases_ms": {k: round(1e3 * v, 2) for k, v in t.get("pack_phases", {}).items()},

@@ -438,8 +438,14 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
         const double* wsrc = (it == 0 ? cg.w[0] : wx + (size_t)(it & 1) * C * D) + b8;
         double wv8[NG];
+        {
+            int jr[NG];  // (the neighbour indices read from LDS as one batch, then every gather issued)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) wv8[g] = ld_sc1(wsrc + (size_t)jn[wv][8 * g + a8] * D);
+            for (int g = 0; g < NG; ++g) jr[g] = jn[wv][8 * g + a8];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) wv8[g] = ld_sc1(wsrc + (size_t)jr[g] * D);
+        }
         const double* Rv = tl.Racc + (size_t)b0 * m;
         double rv[RPT];
 #pragma unroll
@@ -454,6 +460,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         for (int q = 0; q < LNC; ++q)
             if (lane + 64 * q < nc) { ga0 += gl[0][q]; ga1 += gl[1][q]; ga2 += gl[2][q]; }
         const double gam = uni(wave_sum(ga0)), del = uni(wave_sum(ga1)), rho = uni(wave_sum(ga2));
+        if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[582 + 3 * it] = (double)wall_clock64();
         const double bb = (it == 0) ? rho : h_bb;
         double alpha = 0.0, be = 0.0;
         int done = 0;
@@ -526,7 +533,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         for (int g = gw + gridDim.x * kCgpWaves; use && g < m; g += gridDim.x * kCgpWaves) {
             const double* er = Einv + (size_t)g * m;
             double sy = 0.0;
-            for (int l = lane; l < m; l += 64) sy += er[l] * rs[l];
+            for (int l = lane; l < m; l += 64) sy += er[l] * rs[DET ? (l / 9) * 12 + 3 + l % 9 : l];
             const double y = wave_sum(sy);
             if (lane == 0) put_y(yg, g, tag0 + (unsigned)it, y);
         }

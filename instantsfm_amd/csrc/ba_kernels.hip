@@ -1451,13 +1451,15 @@ __global__ void k_zero_words(int* __restrict__ flags, int* __restrict__ status) 
 // trial is copied there in the same launch; the test is lm_step's accept rule on the same doubles (not SPD -> fail;
 // last < loss with rejects left -> reject; otherwise accept), and the decision is published in pub[5] for the host to
 // check against its own.
-__global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__ result, double* pub, unsigned seq, double last,
+__global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__ result, const int* __restrict__ cgst,
+                                                      double* pub, unsigned seq, double last,
                                                       int can_reject, const double* __restrict__ cams_new,
                                                       double* __restrict__ cams_cur, long long ncam,
                                                       const double* __restrict__ pts_new, double* __restrict__ pts_cur,
                                                       long long npts) {
     const double loss = result[0];
-    const bool acc = result[4] == 0.0 && !(last < loss && can_reject);
+    // cgst (a k_tl_cgp solve whose status the host reads afterwards): only a converged CG's trial can be accepted
+    const bool acc = result[4] == 0.0 && !(last < loss && can_reject) && (cgst == nullptr || cgst[0] == 1);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int k = 0; k < 5; ++k) pub[k] = result[k];
         pub[5] = acc ? 1.0 : 0.0;
@@ -1568,6 +1570,8 @@ struct insfm_ba {
     unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
     int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
+    bool cg_async = false;        // lm_step: a k_tl_cgp solve's status is read after the trial's k_publish
+    bool cgp_pending = false;     // a k_tl_cgp launch whose status the host has not read yet (cgp_complete)
     bool cgp_lost = false;        // the last k_tl_cgp timed out at a grid barrier (another process holds CUs)
     double* cgp_trace = nullptr;  // INSFM_DIAG=cgp_trace: [64][4] of the last solve, printed to stderr
     // row-partitioned multi-rank CG (ba_xpart.h; insfm_ba_cg_window / insfm_ba_cg_attach)
@@ -2267,6 +2271,72 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
     });
 }
 
+// The k_tl_cgp launch of this solve has finished (the host saw its status word, or the trial's k_publish behind
+// it): its status {status, iterations, coarse used} into st, the barrier bookkeeping, an abort's fallback, the trace.
+int cgp_complete(insfm_ba* h, int* st) {
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    volatile int* pg = h->prog_host;
+    st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
+    {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
+        if (st[0] == 1 || st[0] == 2) {
+            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1];  // (the DET variant has no grid barrier)
+        } else {
+            HIPCHK(hipStreamSynchronize(h->stream));
+            HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+            h->cgp_epochs = 0;
+            // a barrier timed out: the grid was not resident at once (another process's kernels held CUs).  A single
+            // rank drops the persistent CG for good and run_solve repeats this solve on the launch path; a rank of a
+            // replicated multi-rank CG cannot (its peers would compute a dc that differs in rounding) and reports it.
+            if (st[0] == 4 && h->d.world_size <= 1 && !h->xpart) {
+                std::fprintf(stderr, "[insfm] k_tl_cgp: a grid barrier timed out (the GPU is shared with another "
+                                     "process?); this handle continues on the launch-per-iteration CG\n");
+                h->cgp_nb = 0;
+                h->cgp_lost = true;
+            }
+        }
+    }
+    if (h->cgp_trace) {
+        double tr[kCgpTraceLen];
+        HIPCHK(hipMemcpy(tr, h->cgp_trace, sizeof(tr), hipMemcpyDeviceToHost));
+        const int n = std::min(st[1], 63);
+        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d: setup %.1f us (blocks + tables %.1f, A %.1f, "
+                     "rest %.1f), iterations %.1f us (%.2f us each)\n",
+                     st[0], st[1], st[2], 0.01 * (tr[257] - tr[256]), 0.01 * (tr[578] - tr[256]),
+                     0.01 * (tr[579] - tr[578]), 0.01 * (tr[257] - tr[579]), 0.01 * (tr[258 + n] - tr[257]),
+                     n > 0 ? 0.01 * (tr[258 + n] - tr[258]) / n : 0.0);
+        for (int k = 0; k <= n; ++k) {
+            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g t %.1f us | loads %.2f P1 %.2f y %.2f "
+                         "P2 %.2f B2 %.2f\n", k, tr[4 * k], tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3], 0.01 * (tr[258 + k] - tr[256]),
+                         k > 0 ? 0.01 * (tr[258 + k] - tr[322 + 4 * (k - 1) + 3]) : 0.0,
+                         0.01 * (tr[322 + 4 * k] - tr[258 + k]), 0.01 * (tr[323 + 4 * k] - tr[322 + 4 * k]),
+                         0.01 * (tr[324 + 4 * k] - tr[323 + 4 * k]), 0.01 * (tr[325 + 4 * k] - tr[324 + 4 * k]));
+            if (k < n)
+                std::fprintf(stderr, "[insfm cgp]        P1 split: fills + workgroup barrier %.2f, y %.2f, S~w %.2f; "
+                             "scalar partials in %.2f after the barrier\n",
+                             0.01 * (tr[580 + 3 * k] - tr[258 + k]), 0.01 * (tr[581 + 3 * k] - tr[580 + 3 * k]),
+                             0.01 * (tr[322 + 4 * k] - tr[581 + 3 * k]),
+                             k > 0 ? 0.01 * (tr[582 + 3 * k] - tr[322 + 4 * (k - 1) + 3]) : 0.0);
+        }
+        const int G = std::min(h->cgp_grid, 256);
+        if (st[1] > kCgpTraceIt + 1 && G > 0) {  // every workgroup's start and end of iteration kCgpTraceIt
+            double s0 = tr[772], s1 = tr[772];
+            for (int b = 0; b < G; ++b) { s0 = std::min(s0, tr[772 + b]); s1 = std::max(s1, tr[772 + b]); }
+            std::vector<int> ord(G);
+            for (int b = 0; b < G; ++b) ord[b] = b;
+            std::sort(ord.begin(), ord.end(), [&](int a, int b) { return tr[1028 + a] > tr[1028 + b]; });
+            std::fprintf(stderr, "[insfm cgp] it %d per workgroup: starts within %.2f us; arrival at the barrier "
+                         "(us after the first start): median %.2f, last %.2f; latest:", kCgpTraceIt, 0.01 * (s1 - s0),
+                         0.01 * (tr[1028 + ord[G / 2]] - s0), 0.01 * (tr[1028 + ord[0]] - s0));
+            for (int q = 0; q < std::min(G, 8); ++q)
+                std::fprintf(stderr, " wg %d (%.2f, start %.2f)", ord[q], 0.01 * (tr[1028 + ord[q]] - s0),
+                             0.01 * (tr[772 + ord[q]] - s0));
+            std::fprintf(stderr, "\n");
+        }
+    }
+    return 0;
+}
+
+
 // The two-level CG (precond 1): iterations enqueued from a host poll loop, no stream sync inside the CG.  k_tl_pc's
 // lead workgroup publishes its progress into host-mapped memory; more iterations are enqueued while the GPU has fewer
 // than kCgAhead pending, and the loop ends when the status word turns non-zero.  The few iterations enqueued past
@@ -2305,10 +2375,22 @@ int run_tl_cg(insfm_ba* h, int* st) {
     int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
     if (h->cgp_nb) enq = maxit + 2;  // k_tl_cgp: one launch runs every iteration
     if (int rc = enqueue(0, enq)) return rc;
+    if (h->cgp_nb) h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
     if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup)
         HIPCHK(hipEventRecord(h->ev_E, h->stream));
         if (int rc = issue_side_chain(h, h->cgp_slot, true)) return rc;
         h->cgp_defer = false;
+    }
+    if (h->cgp_nb && h->cg_async) {
+        // one launch runs the whole CG and the kernels behind it need no host decision: the host queues them at once
+        // and reads the CG status after the trial's k_publish (cgp_complete), which accepts the trial only for a
+        // converged CG.  (Waiting here for the status word cost a host round trip and a launch from an idle queue
+        // between the CG and k_cg_finish.)
+        rec(h, 9);
+        h->cg_launches += 1;
+        h->cgp_pending = true;
+        st[0] = 1; st[1] = 0; st[2] = 1;
+        return 0;
     }
     CgPoll poll;
     poll.enq = enq;
@@ -2355,62 +2437,8 @@ int run_tl_cg(insfm_ba* h, int* st) {
         acc_time(h, 8, 9, 5);
     }
     h->cg_launches += h->cgp_nb ? 1 : enq;
+    if (h->cgp_nb) return cgp_complete(h, st);
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
-    if (h->cgp_nb) {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
-        h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
-        if (st[0] == 1 || st[0] == 2) {
-            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1];  // (the DET variant has no grid barrier)
-        } else {
-            HIPCHK(hipStreamSynchronize(h->stream));
-            HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
-            h->cgp_epochs = 0;
-            // a barrier timed out: the grid was not resident at once (another process's kernels held CUs).  A single
-            // rank drops the persistent CG for good and run_solve repeats this solve on the launch path; a rank of a
-            // replicated multi-rank CG cannot (its peers would compute a dc that differs in rounding) and reports it.
-            if (st[0] == 4 && h->d.world_size <= 1) {
-                std::fprintf(stderr, "[insfm] k_tl_cgp: a grid barrier timed out (the GPU is shared with another "
-                                     "process?); this handle continues on the launch-per-iteration CG\n");
-                h->cgp_nb = 0;
-                h->cgp_lost = true;
-            }
-        }
-    }
-    if (h->cgp_nb && h->cgp_trace) {
-        double tr[kCgpTraceLen];
-        HIPCHK(hipMemcpy(tr, h->cgp_trace, sizeof(tr), hipMemcpyDeviceToHost));
-        const int n = std::min(st[1], 63);
-        std::fprintf(stderr, "[insfm cgp] status %d iterations %d coarse %d: setup %.1f us (blocks + tables %.1f, A %.1f, "
-                     "rest %.1f), iterations %.1f us (%.2f us each)\n",
-                     st[0], st[1], st[2], 0.01 * (tr[257] - tr[256]), 0.01 * (tr[578] - tr[256]),
-                     0.01 * (tr[579] - tr[578]), 0.01 * (tr[257] - tr[579]), 0.01 * (tr[258 + n] - tr[257]),
-                     n > 0 ? 0.01 * (tr[258 + n] - tr[258]) / n : 0.0);
-        for (int k = 0; k <= n; ++k) {
-            std::fprintf(stderr, "[insfm cgp]   it %d gamma %.17g delta %.17g rho %.17g done %g t %.1f us | loads %.2f P1 %.2f y %.2f "
-                         "P2 %.2f B2 %.2f\n", k, tr[4 * k], tr[4 * k + 1], tr[4 * k + 2], tr[4 * k + 3], 0.01 * (tr[258 + k] - tr[256]),
-                         k > 0 ? 0.01 * (tr[258 + k] - tr[322 + 4 * (k - 1) + 3]) : 0.0,
-                         0.01 * (tr[322 + 4 * k] - tr[258 + k]), 0.01 * (tr[323 + 4 * k] - tr[322 + 4 * k]),
-                         0.01 * (tr[324 + 4 * k] - tr[323 + 4 * k]), 0.01 * (tr[325 + 4 * k] - tr[324 + 4 * k]));
-            if (k < n)
-                std::fprintf(stderr, "[insfm cgp]        P1 split: fills + workgroup barrier %.2f, y %.2f, S~w %.2f\n",
-                             0.01 * (tr[580 + 3 * k] - tr[258 + k]), 0.01 * (tr[581 + 3 * k] - tr[580 + 3 * k]),
-                             0.01 * (tr[322 + 4 * k] - tr[581 + 3 * k]));
-        }
-        const int G = std::min(h->cgp_grid, 256);
-        if (st[1] > kCgpTraceIt + 1 && G > 0) {  // every workgroup's start and end of iteration kCgpTraceIt
-            double s0 = tr[772], s1 = tr[772];
-            for (int b = 0; b < G; ++b) { s0 = std::min(s0, tr[772 + b]); s1 = std::max(s1, tr[772 + b]); }
-            std::vector<int> ord(G);
-            for (int b = 0; b < G; ++b) ord[b] = b;
-            std::sort(ord.begin(), ord.end(), [&](int a, int b) { return tr[1028 + a] > tr[1028 + b]; });
-            std::fprintf(stderr, "[insfm cgp] it %d per workgroup: starts within %.2f us; arrival at the barrier "
-                         "(us after the first start): median %.2f, last %.2f; latest:", kCgpTraceIt, 0.01 * (s1 - s0),
-                         0.01 * (tr[1028 + ord[G / 2]] - s0), 0.01 * (tr[1028 + ord[0]] - s0));
-            for (int q = 0; q < std::min(G, 8); ++q)
-                std::fprintf(stderr, " wg %d (%.2f, start %.2f)", ord[q], 0.01 * (tr[1028 + ord[q]] - s0),
-                             0.01 * (tr[772 + ord[q]] - s0));
-            std::fprintf(stderr, "\n");
-        }
-    }
     return 0;
 }
 
@@ -2455,6 +2483,55 @@ int run_bj_cg(insfm_ba* h, int* st) {
 
 // Build S/b for factor f, solve, back-substitute and form the trial parameters.  Returns PCG iterations (>= 0),
 // INSFM_BA_ESOLVER on breakdown, or another negative code.
+// After the CG of a solve: its status (breakdown -> ESOLVER), the partitioned CG's solution gather, dc = L^-T x.
+// Returns the PCG iterations (0 while a k_tl_cgp status is still pending) or an error.
+int cg_tail(insfm_ba* h, int* st) {
+    const int D = h->D;
+    int rc = 0;
+    if (st[0] != 1) {
+        h->err = std::string("PCG ") +
+                 (st[0] == 2 ? "breakdown"
+                  : st[0] == 4 ? "timed out (a k_tl_cgp grid barrier or a cross-rank exchange of the partitioned CG)"
+                               : "did not finish") +
+                 " at iteration " +
+                 std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
+                 (h->tlon ? std::to_string(st[2]) : std::string("off")) + ")";
+        return st[0] == 4 ? INSFM_BA_EHIP : INSFM_BA_ESOLVER;
+    }
+    if (!h->cgp_pending) {
+        h->coarse_used = h->tlon ? st[2] : 0;
+        h->last_cg_iters = st[1];
+    }
+    if (h->xpart) {  // partitioned CG: every rank's solution rows into every window, then into cg.x
+        const int n = h->xq[h->d.rank + 1] - h->xq[h->d.rank];
+        if (n > 0)
+            k_xput_x<<<cdiv((long long)n * D, 256), 256, 0, h->stream>>>(n, D, h->tl.cl_cams, h->cg.x,
+                                                                        xpart_region(h, 0), h->xoff_xg);
+        launch_xchg(h, 1);
+        HIPCHK(hipMemcpyAsync(h->cg.x, h->xwin + h->xoff_xg, sizeof(double) * (size_t)h->C * D,
+                              hipMemcpyDeviceToDevice, h->stream));
+        if ((rc = launch_err(h, "partitioned CG gather"))) return rc;
+        int sw[2] = {0, 0};  // (prototype path: one synchronization to see a gather that timed out)
+        HIPCHK(hipMemcpyAsync(sw, h->cg.status, sizeof(sw), hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipStreamSynchronize(h->stream));
+        if (sw[0] == 4) {
+            h->err = "partitioned CG: the solution gather across ranks timed out";
+            return INSFM_BA_EHIP;
+        }
+    }
+    rc = with_D(D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
+                                                                                        h->dc);
+        return launch_err(h, "k_cg_finish");
+    });
+    if (rc) return rc;
+    hmark(h, "cg_finish");
+    return h->cgp_pending ? 0 : st[1];
+}
+
+int solve_tail(insfm_ba* h, double f, const double* cams, const double* pts_local, const double* dcp);
+
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
     // the point preparation of the linearization covers this solve when it runs at the prepared damping factor
@@ -2542,46 +2619,18 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
             if ((rc = run_tl_basis(h, cams, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
         }
-        if (st[0] != 1) {
-            h->err = std::string("PCG ") +
-                     (st[0] == 2 ? "breakdown"
-                      : st[0] == 4 ? "timed out (a k_tl_cgp grid barrier or a cross-rank exchange of the partitioned CG)"
-                                   : "did not finish") +
-                     " at iteration " +
-                     std::to_string(st[1]) + " (status " + std::to_string(st[0]) + ", coarse " +
-                     (h->tlon ? std::to_string(st[2]) : std::string("off")) + ")";
-            return st[0] == 4 ? INSFM_BA_EHIP : INSFM_BA_ESOLVER;
-        }
-        iters = st[1];
-        h->coarse_used = h->tlon ? st[2] : 0;
-        h->last_cg_iters = iters;
-        if (h->xpart) {  // partitioned CG: every rank's solution rows into every window, then into cg.x
-            const int n = h->xq[h->d.rank + 1] - h->xq[h->d.rank];
-            if (n > 0)
-                k_xput_x<<<cdiv((long long)n * D, 256), 256, 0, h->stream>>>(n, D, h->tl.cl_cams, h->cg.x,
-                                                                            xpart_region(h, 0), h->xoff_xg);
-            launch_xchg(h, 1);
-            HIPCHK(hipMemcpyAsync(h->cg.x, h->xwin + h->xoff_xg, sizeof(double) * (size_t)h->C * D,
-                                  hipMemcpyDeviceToDevice, h->stream));
-            if ((rc = launch_err(h, "partitioned CG gather"))) return rc;
-            int sw[2] = {0, 0};  // (prototype path: one synchronization to see a gather that timed out)
-            HIPCHK(hipMemcpyAsync(sw, h->cg.status, sizeof(sw), hipMemcpyDeviceToHost, h->stream));
-            HIPCHK(hipStreamSynchronize(h->stream));
-            if (sw[0] == 4) {
-                h->err = "partitioned CG: the solution gather across ranks timed out";
-                return INSFM_BA_EHIP;
-            }
-        }
-        rc = with_D(D, [&](auto dc_) -> int {
-            constexpr int DV = decltype(dc_)::value;
-            k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
-                                                                                            h->dc);
-            return launch_err(h, "k_cg_finish");
-        });
-        if (rc) return rc;
+        const int ci = cg_tail(h, st);
+        if (ci < 0) return ci;
+        iters = ci;
         dcp = h->dc;
-        hmark(h, "cg_finish");
     }
+    if (int rb = solve_tail(h, f, cams, pts_local, dcp)) return rb;
+    return iters;
+}
+
+// The back-substitution and the trial parameters of a solve (dcp: the camera step, null for a points-only solve).
+int solve_tail(insfm_ba* h, double f, const double* cams, const double* pts_local, const double* dcp) {
+    const bool gpk = h->kind == 1;
     rec(h, 3);
     if (gpk) {
         if (h->Pl > 0)
@@ -2591,7 +2640,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         k_gp_update_cams<<<cdiv(3 * h->C, kThreads), kThreads, 0, h->stream>>>(3 * h->C, cams, dcp, h->cams_new);
         int rc = launch_err(h, "k_gp_backsub/update");
         if (rc) return rc;
-        return iters;
+        return 0;
     }
     if (int rc0 = lin_join(h)) return rc0;  // the camera update reads U / g_c (points-only solves skip the factor)
     const int rc = with_model(h->model, [&](auto mc) -> int {
@@ -2604,7 +2653,17 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
     });
     if (rc) return rc;
     hmark(h, "backsub");
-    return iters;
+    return 0;
+}
+
+// A step that ended in an error with a k_tl_cgp status unread: wait for the launch and restart the barrier counters
+// (the next launch's epochs would otherwise not match what this one counted).
+void cgp_drop_pending(insfm_ba* h) {
+    if (!h->cgp_pending) return;
+    h->cgp_pending = false;
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream);
+    h->cgp_epochs = 0;
 }
 
 // lm_step's accept rule for the trial being costed (k_publish copies an accepted trial into the caller's buffers)
@@ -2628,7 +2687,8 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     const bool copy = ta != nullptr && h->ext_cur && h->kind == 0;
     const long long ncam = copy ? (long long)h->C * h->stride : 0, npts = copy ? (long long)h->Pl * 3 : 0;
     const int grid = copy ? std::max(1, std::min(1024, cdiv(std::max(ncam, npts / 2 + 1), kThreads))) : 1;
-    k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->pub_dev, seq, ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
+    k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->cgp_pending ? h->cg.status : nullptr, h->pub_dev, seq,
+                                               ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
                                                h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
     if (int rc = launch_err(h, "k_publish")) return rc;
     hmark(h, "publish");
@@ -2719,15 +2779,47 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
     rec(h, 1);
     double f = 1.0;
     int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
+    cgp_drop_pending(h);
     for (;;) {
         f *= (1.0 + h->damping);
         ++trials;
-        const int it = run_solve(h, f, h->cams_cur, h->pts_cur);
+        h->cg_async = true;  // (a k_tl_cgp solve: its status is read after the trial's cost, below)
+        int it = run_solve(h, f, h->cams_cur, h->pts_cur);
+        h->cg_async = false;
         if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
         if (it < 0) return it;
         rec(h, 4);
         const TrialAccept ta{last, rejects < h->d.max_rejects ? 1 : 0};
         if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new, &ta))) return rc;  // waits for the result
+        if (h->cgp_pending) {  // the k_tl_cgp launch finished before the k_publish the host just saw
+            h->cgp_pending = false;
+            int cst[3];
+            if ((rc = cgp_complete(h, cst))) return rc;
+            if (h->timing) acc_time(h, 8, 9, 5);
+            if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
+            if (cst[0] == 4 && h->cgp_lost) {
+                // single rank: a grid barrier timed out (cgp_complete switched the handle to the launch path); this
+                // trial's CG again from the basis, then its back-substitution and cost (k_publish rejected the first)
+                h->cgp_lost = false;
+                HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+                int* st = reinterpret_cast<int*>(h->host_res + 8);
+                if ((rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
+                it = cg_tail(h, st);
+                if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
+                if (it < 0) return it;
+                if ((rc = solve_tail(h, f, h->cams_cur, h->pts_cur, h->dc))) return rc;
+                if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new, &ta))) return rc;
+            } else if (cst[0] != 1) {
+                h->err = std::string("PCG ") + (cst[0] == 2 ? "breakdown" : "timed out (a k_tl_cgp grid barrier)") +
+                         " at iteration " + std::to_string(cst[1]) + " (status " + std::to_string(cst[0]) + ")";
+                if (cst[0] == 2) { failed = 1; h->loss = last; break; }
+                return INSFM_BA_EHIP;
+            } else {
+                it = cst[1];
+                h->coarse_used = cst[2];
+                h->last_cg_iters = it;
+            }
+        }
         rec(h, 5);
         if (h->timing) {
             (void)hipEventSynchronize(h->ev[5]);
@@ -3881,6 +3973,7 @@ int insfm_ba_reset(insfm_ba* h) {
     h->have_loss = false;
     // a fresh LM: the first solve after the reset factorizes its own coarse matrix (no lagged E^-1 of an earlier solve
     // survives) and the CG's first batch is sized as for a new handle
+    cgp_drop_pending(h);
     if (int rc = side_flush(h)) return rc;
     h->tl_solves = 0;
     h->tl_fresh = false;
@@ -3890,6 +3983,7 @@ int insfm_ba_reset(insfm_ba* h) {
 
 int insfm_ba_cost(insfm_ba* h, const double* cams, const double* pts, double* loss, double* rmse) {
     if (!h || !cams || !pts || h->kind != 0) return INSFM_BA_EINVAL;
+    cgp_drop_pending(h);
     HIPCHK(hipMemsetAsync(h->flags, 0, sizeof(int) * 4, h->stream));
     int rc = run_cost(h, cams, pts + 3 * (size_t)h->p0, false);
     if (rc) return rc;
@@ -3917,6 +4011,7 @@ int insfm_ba_step(insfm_ba* h, double* cams_user, double* pts_user, insfm_ba_sta
 
 int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts) {
     if (!h || !cams || !pts || h->kind != 0) return INSFM_BA_EINVAL;
+    cgp_drop_pending(h);
     h->keep_S = 1;
     HIPCHK(hipMemcpyAsync(h->cams_cur, cams, sizeof(double) * (size_t)h->C * h->stride, hipMemcpyDeviceToDevice, h->stream));
     if (h->Pl)
@@ -3931,6 +4026,7 @@ int insfm_ba_debug_linearize(insfm_ba* h, const double* cams, const double* pts)
 
 int insfm_ba_debug_solve(insfm_ba* h, double f) {
     if (!h) return INSFM_BA_EINVAL;
+    cgp_drop_pending(h);
     h->keep_S = 1;
     // solves around the parameters last passed to insfm_ba_debug_linearize
     int it = run_solve(h, f, h->cams_cur, h->pts_cur);

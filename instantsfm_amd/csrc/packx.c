@@ -323,17 +323,25 @@ static PyObject* assign_xyz(PyObject* self, PyObject* args) {
     char* base = (char*)PyArray_DATA(ap);
     const npy_intp n = PyArray_DIM(ap, 0);
     npy_intp dims[1] = {3};
+    PyArray_Descr* d8 = PyArray_DescrFromType(NPY_FLOAT64);  /* (one lookup; each view takes a reference) */
+    if (!d8) { Py_DECREF(fast); return NULL; }
     for (npy_intp i = 0; i < n; ++i) {
-        if (idx[i] < 0 || idx[i] >= T) { PyErr_SetString(PyExc_IndexError, "assign_xyz: track index"); Py_DECREF(fast); return NULL; }
-        PyObject* row = PyArray_New(&PyArray_Type, 1, dims, NPY_FLOAT64, NULL, base + 24 * i, 0,
-                                    NPY_ARRAY_CARRAY, NULL);
-        if (!row) { Py_DECREF(fast); return NULL; }
+        if (idx[i] < 0 || idx[i] >= T) {
+            PyErr_SetString(PyExc_IndexError, "assign_xyz: track index");
+            Py_DECREF(d8);
+            Py_DECREF(fast);
+            return NULL;
+        }
+        Py_INCREF(d8);
+        PyObject* row = PyArray_NewFromDescr(&PyArray_Type, d8, 1, dims, NULL, base + 24 * i, NPY_ARRAY_CARRAY, NULL);
+        if (!row) { Py_DECREF(d8); Py_DECREF(fast); return NULL; }
         Py_INCREF(o_pts);
-        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) { Py_DECREF(row); Py_DECREF(fast); return NULL; }
+        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) { Py_DECREF(row); Py_DECREF(d8); Py_DECREF(fast); return NULL; }
         const int r = PyObject_SetAttr(items[idx[i]], s_xyz, row);
         Py_DECREF(row);
-        if (r < 0) { Py_DECREF(fast); return NULL; }
+        if (r < 0) { Py_DECREF(d8); Py_DECREF(fast); return NULL; }
     }
+    Py_DECREF(d8);
     Py_DECREF(fast);
     Py_RETURN_NONE;
 }

@@ -91,3 +91,25 @@ def _shard_worker(rank, world, port, cfg):
 @pytest.mark.parametrize("cfg", [0, 1])
 def test_track_sharding_decomposes_camera_system(cfg):
     _run(_shard_worker, 2, cfg)
+
+
+class _Props:
+    def __init__(self, bus):
+        self.pci_domain_id, self.pci_bus_id, self.pci_device_id = 0, bus, 0
+
+
+def _rpd_worker(rank, world, port, buses, expect):
+    _init(rank, world, port)
+    from instantsfm_amd import engine
+    torch.cuda.get_device_properties = lambda device: _Props(buses[rank])  # (no GPU here: the rank's PCI address)
+    got = engine.ranks_per_device(None)
+    assert got == expect, (rank, got, expect)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("buses,expect", [([3, 3, 3, 3], 4), ([1, 2, 3, 4], 1), ([1, 1, 2, 3], 2)])
+def test_ranks_per_device(buses, expect):
+    """engine.ranks_per_device: the most ranks on one GPU, from every rank's (host name, PCI address) -- the count the
+    engine passes to insfm_ba_set_ranks_per_device (the persistent CG stays on only if that many grids fit on a GPU;
+    every rank gets the same count, so every rank takes the same CG path)."""
+    _run(_rpd_worker, len(buses), buses, expect)

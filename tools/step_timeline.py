@@ -29,3 +29,27 @@ for r in rows[i0:i1]:
 print("step span us", (int(rows[i1]["Start_Timestamp"]) - t0) / 1000)
 for n, v in sorted(agg.items(), key=lambda x: -x[1])[:12]:
     print(f"  {n:30s} {v:8.1f}")
+
+# every step of the trace: the main queue's (k_lin_points') busy fraction and the union of all queues' kernels
+qm = rows[idx[0]]["Queue_Id"]
+fr, un = [], []
+for a, b in zip(idx[:-1], idx[1:]):
+    s0, s1 = int(rows[a]["Start_Timestamp"]), int(rows[b]["Start_Timestamp"])
+    busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b] if r["Queue_Id"] == qm)
+    iv = sorted((int(r["Start_Timestamp"]), min(int(r["End_Timestamp"]), s1)) for r in rows[a:b])
+    tot, cur_s, cur_e = 0, None, None
+    for s, e in iv:
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    fr.append(busy / (s1 - s0))
+    un.append(tot / (s1 - s0))
+if fr:
+    fr_s, un_s = sorted(fr), sorted(un)
+    print(f"steps {len(fr)}: main queue busy median {fr_s[len(fr) // 2]:.3f} (min {fr_s[0]:.3f}, max {fr_s[-1]:.3f}); "
+          f"any queue busy median {un_s[len(un) // 2]:.3f}")
