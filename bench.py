@@ -469,17 +469,19 @@ def solve_end_to_end(prob, dev):
     from instantsfm_amd.config.colmap import BUNDLE_ADJUSTER_OPTIONS
     from instantsfm_amd.processors.bundle_adjustment import TorchBA
     from instantsfm_amd.synth import to_scene
-    # Two Solves on fresh copies of the scene: the first of a process maps fresh device memory and loads code objects
-    # (reported as first_*); the second is the steady state a caller that solves repeatedly (the mapper) sees, its
-    # engine taking the device buffers the first one parked in the library's cache.
-    first = None
-    for rep in range(2):
+    # Four Solves on fresh copies of the scene: the first of a process maps fresh device memory and loads code objects
+    # (reported as first_*); the others are the steady state a caller that solves repeatedly (the mapper) sees, its
+    # engine taking the device buffers the previous one parked in the library's cache -- the median of those three by
+    # total time is reported (the host phases vary by several ms from Solve to Solve on a shared host).
+    runs = []
+    for rep in range(4):
         cams, ims, tracks = to_scene(prob)
         ba = TorchBA(device=str(dev))
         ba.Solve(cams, ims, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
-        if rep == 0:
-            first = dict(ba.timings)
-    t = ba.timings
+        runs.append(dict(ba.timings))
+        del cams, ims, tracks, ba
+    first = runs[0]
+    t = sorted(runs[1:], key=lambda r: r["total_s"])[1]
     host = t["pack_s"] + t["create_s"] + t["update_s"]
     return {"first_solve_total_s": round(first["total_s"], 4), "first_create_s": round(first["create_s"], 4),
             "first_update_s": round(first["update_s"], 4),

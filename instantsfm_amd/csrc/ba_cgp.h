@@ -459,7 +459,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
         for (int q = 0; q < LNC; ++q)
             if (lane + 64 * q < nc) { ga0 += gl[0][q]; ga1 += gl[1][q]; ga2 += gl[2][q]; }
-        const double gam = uni(wave_sum(ga0)), del = uni(wave_sum(ga1)), rho = uni(wave_sum(ga2));
+        wave_sum3(ga0, ga1, ga2);
+        const double gam = uni(ga0), del = uni(ga1), rho = uni(ga2);
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[582 + 3 * it] = (double)wall_clock64();
         const double bb = (it == 0) ? rho : h_bb;
         double alpha = 0.0, be = 0.0;
@@ -651,7 +652,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
             }
-            g0 = wave_sum(g0); g1 = wave_sum(g1); g2 = wave_sum(g2);
+            wave_sum3(g0, g1, g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
             if (lane < MC) prt[rl][3 + lane] = rr;
         }

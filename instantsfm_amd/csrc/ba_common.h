@@ -13,6 +13,18 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// three wave_sums with their butterfly steps interleaved: the same additions in the same order per value (bitwise
+// wave_sum's results), one cross-lane latency per step instead of three
+__device__ __forceinline__ void wave_sum3(double& a, double& b, double& c) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double ta = __shfl_xor(a, off, 64), tb = __shfl_xor(b, off, 64), tc = __shfl_xor(c, off, 64);
+        a += ta;
+        b += tb;
+        c += tc;
+    }
+}
+
 
 struct CgBufs {
     double* r[2];

@@ -2118,13 +2118,16 @@ int run_tl_setup(insfm_ba* h, const double* cams) {
     const int slot = (int)(h->tl_solves & 1);
     int rc = run_tl_basis(h, cams, h->stream);
     if (rc) return rc;
-    HIPCHK(hipEventRecord(h->ev_E, h->stream));
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
-    // k_tl_cgp under the lag rule: this solve's chain runs after the CG (run_tl_cg); else it runs now and the CG waits
+    // k_tl_cgp under the lag rule: this solve's chain runs after the CG (run_tl_cg records ev_E behind the CG; an
+    // event record here as well would only cost the main queue a marker); else it runs now and the CG waits
     h->cgp_defer = h->cgp_nb && use != slot;
     h->cgp_slot = slot;
-    if (!h->cgp_defer && (rc = issue_side_chain(h, slot))) return rc;
+    if (!h->cgp_defer) {
+        HIPCHK(hipEventRecord(h->ev_E, h->stream));
+        if ((rc = issue_side_chain(h, slot))) return rc;
+    }
     // a lagged solve's coarse inverse normally finished long ago: a completed event needs no wait marker in the main
     // queue (each one idles it a few us; always queueing it measured 659-665 vs 659-664 LM it/s, round 2)
     if (use == slot || hipEventQuery(h->ev_fact[use]) != hipSuccess)
