@@ -353,11 +353,101 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             }
         }
     }
+    // ---- iteration 0's operator product (k_tl_pspmv's setup, folded in): w0 = u0 + S~ u0 with u0 = M~^-1 r0 from
+    // k_tl_pc's setup launch, z0 = q0 = 0; w0 into the exchange buffer of parity 0 and the partials of iteration 0
+    // (r0.u0, w0.u0, ||L r0||^2, Z~^T w0) published like P2's (atomic buffer 0 / runs tagged with iteration 0)
+    {
+        double uv8[NG];
+        {
+            int jr[NG];
+#pragma unroll
+            for (int g = 0; g < NG; ++g) jr[g] = jn[wv][8 * g + a8];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int g = 0; g < NG; ++g) uv8[g] = tl.u[(size_t)jr[g] * D + b8];
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) wg[wv][8 * g + a8][b8] = uv8[g];
+        __syncthreads();
+        if (has_row) {
+            double ac4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int k0 = 0; k0 < NB; k0 += 16) {
+                double w16[16];
+#pragma unroll
+                for (int c = 0; c < 16; ++c) w16[c] = wg[wv][k0 + c][b8];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int c = 0; c < 16; ++c) ac4[c & 3] += sreg[k0 + c] * w16[c];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            double acc = (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
+            acc += __shfl_xor(acc, 1, 64);
+            acc += __shfl_xor(acc, 2, 64);
+            acc += __shfl_xor(acc, 4, 64);
+            const double su = __shfl(acc, 8 * (lane & 7), 64);
+            const int la = lane & 7;
+            const double u_ = V[VU + la], r_ = V[VR + la];
+            const double w0 = u_ + su;  // (the diagonal block of S~ is I)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < D) {
+                V[VW + la] = w0; V[VZ + la] = 0.0; V[VQ + la] = 0.0;
+                st_sc1(wx + (size_t)row * D + lane, w0);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double g0 = 0.0, g1 = 0.0, g2 = 0.0, rr = 0.0;
+            {
+                const int lc = min(lane, MC - 1);
+                double l8[D], r8[D], z8[D], w8[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    l8[k] = Lrow[rl][la * D + k];
+                    r8[k] = V[VR + k];
+                    z8[k] = Zrow[rl][k * MC + lc];
+                    w8[k] = V[VW + k];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (lane < D) {
+                    g0 = r_ * u_;
+                    g1 = w0 * u_;
+                    double lr = 0.0;
+#pragma unroll
+                    for (int k = 0; k < D; ++k)
+                        if (k <= lane) lr += l8[k] * r8[k];
+                    g2 = lr * lr;
+                }
+                if (lane < MC) {
+#pragma unroll
+                    for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
+                }
+            }
+            wave_sum3(g0, g1, g2);
+            if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
+            if (lane < MC) prt[rl][3 + lane] = rr;
+        }
+        if constexpr (DET) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (w0 before the runs' partials)
+        __syncthreads();
+        if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3 + MC) {
+            double v = prt[rl][lane];
+            for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
+            if constexpr (DET) {
+                put_y(rung, pos * 12 + lane, tag0, v);
+            } else {
+                if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)lane * nc + ci, v);
+                else unsafeAtomicAdd(tl.Racc + (size_t)ci * MC + (lane - 3), v);
+            }
+        }
+        if constexpr (!DET) alive = cgp_barrier(sync, ++epoch, &bflag);
+    }
     if (trace && blockIdx.x == 0 && t == 0) {
         trace[256] = (double)t_start;
         trace[257] = (double)wall_clock64();
     }
-    for (;; ++it) {
+    for (; alive; ++it) {
         if ((oseg & 2) && it == 2 && blockIdx.x == gridDim.x - 1) {  // (fault injection: see above)
             if (t == 0) __hip_atomic_store(cgp_abort(sync), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             alive = false;
@@ -372,8 +462,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         double gl[3][LNC];
         if constexpr (DET) {
             // cluster owners (wave c for cluster c): the cluster's 12 partials of this iteration summed in a fixed order
-            // (iteration 0: the setup's row partials in cluster order; then the tagged partials of the cluster's
-            // workgroup runs, in run order, kCgpRunBatch loads in flight), published as tagged granules in the
+            // (the tagged partials of the cluster's workgroup runs, in run order, kCgpRunBatch loads in flight;
+            // iteration 0's from the setup above), published as tagged granules in the
             // iteration's parity buffer.  No grid barrier: a workgroup holding every cluster's sums of this iteration
             // knows every row finished the previous one (each stored its w before its run's partials).
             unsigned long long* cgi = cgran + (size_t)(it & 1) * 2 * 12 * kCgpMaxClusters;
@@ -382,19 +472,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             for (int c = gw; ok && c < nc; c += gridDim.x * kCgpWaves) {
                 const int p0 = tl.cl_ptr[c], p1 = tl.cl_ptr[c + 1];
                 double v = 0.0;
-                if (it == 0) {
-                    for (int pb = p0; pb < p1; pb += kCgpRunBatch) {
-                        double x[kCgpRunBatch];
-#pragma unroll
-                        for (int q = 0; q < kCgpRunBatch; ++q) {
-                            const int p = min(pb + q, p1 - 1);
-                            x[q] = l12 < 3 ? tl.gd[(size_t)l12 * C + p] : tl.rowR[(size_t)p * MC + (l12 - 3)];
-                        }
-#pragma unroll
-                        for (int q = 0; q < kCgpRunBatch; ++q)
-                            if (pb + q < p1) v += x[q];
-                    }
-                } else {
+                {
                     for (int pb = p0; pb < p1;) {
                         int hp[kCgpRunBatch], idx[kCgpRunBatch];
                         double x[kCgpRunBatch];
@@ -436,7 +514,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 gl[0][q] = ld_sc1(G + l); gl[1][q] = ld_sc1(G + nc + l); gl[2][q] = ld_sc1(G + 2 * nc + l);
             }
         }
-        const double* wsrc = (it == 0 ? cg.w[0] : wx + (size_t)(it & 1) * C * D) + b8;
+        const double* wsrc = wx + (size_t)(it & 1) * C * D + b8;
         double wv8[NG];
         {
             int jr[NG];  // (the neighbour indices read from LDS as one batch, then every gather issued)

@@ -2210,18 +2210,14 @@ void launch_tl_iter_x(insfm_ba* h, int it, int maxit, double tol2) {
     pspmv(it);
 }
 
-// The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): the setup launches of
-// launch_tl_iter(0), the barrier words cleared, one launch for every iteration.
+// The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): k_tl_pc's setup launch (u0),
+// then one launch for the operator product of the setup and every iteration.
 int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     constexpr int D = 8;
-    // the fixed-order variant starts from the setup's row partials (tl.gd / tl.rowR), also on a handle that has the
-    // atomic cluster buffers
-    TlBufs t0 = h->tl;
-    if (h->cgp_det) t0.Racc = t0.Gacc = nullptr;
-    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, t0,
+    // u0 = M~^-1 r0 (k_tl_pc's setup, which also clears the atomic partial buffers 0 and 1); k_tl_cgp forms
+    // w0 = S~ u0 and iteration 0's partials itself (the launch path's k_tl_pspmv setup launch streamed S~ once more)
+    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
                                                                h->tl.Einv);
-    k_tl_pspmv<D><<<h->C, kPspmvThreads, 0, h->stream>>>(-1, h->C, h->nbr_stride, h->nbr_ptr, h->nbr_j, h->Sn, h->Lf,
-                                                          h->cg, t0, XPart{});
     if (h->cgp_epochs > (1u << 24)) {  // (counter headroom: zero them now and then; an abort zeroes them too)
         HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
         h->cgp_epochs = 0;
@@ -2282,7 +2278,8 @@ int cgp_complete(insfm_ba* h, int* st) {
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
     {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
         if (st[0] == 1 || st[0] == 2) {
-            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1];  // (the DET variant has no grid barrier)
+            // (the setup's barrier and one per completed iteration; the DET variant has no grid barrier)
+            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1] + 1u;
         } else {
             HIPCHK(hipStreamSynchronize(h->stream));
             HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
