@@ -43,6 +43,9 @@ def test_two_ranks_match_single_gpu(extra):
     assert out["loss_rel"] < 1e-9, out
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
     assert out["cams_equal_across_ranks"], out
+    if extra[0] == "--small":  # two 6-workgroup persistent grids fit on the shared GPU: the replicated fixed-order
+        assert out["ranks_per_device"] == 2, out  # k_tl_cgp on both ranks, one launch per solve, bitwise-equal ranks
+        assert out["cg_launches"] == out["trials"], out
     assert abs(out["rmse"] - out["ref_rmse"]) < 1e-6, out
     if "scales_rel" in out:
         assert out["scales_rel"] < 1e-7, out
@@ -55,6 +58,10 @@ def test_config4_sharded_config3_scene(nproc):
     (gloo, ranks sharing the one MI355X of the test box) vs the single-GPU LM: loss 1e-9, parameters 1e-7, every rank
     holds bitwise-equal cameras (the replicated CG computed the same dc), RMSE |delta| <= 1e-4 px."""
     out = _run(nproc, "gloo", ["--config", "3", "--steps", "3"], timeout=850)
+    # nproc ranks on the one GPU: nproc persistent grids of 250 workgroups do not fit, so every rank runs the
+    # launch-per-iteration CG (insfm_ba_set_ranks_per_device), several launches per solve
+    assert out["ranks_per_device"] == nproc, out
+    assert all(l > t for l, t in zip(out["cg_launches"], out["trials"])), out
     assert out["world"] == nproc and len(out["shards"]) == nproc
     assert out["loss_rel"] < 1e-9, out
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out

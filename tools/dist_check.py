@@ -108,11 +108,13 @@ def main():
     rows = eng.partition_cg() if args.cg_partition else None
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
     pts = torch.from_numpy(prob.points_init.copy()).to(dev)
-    losses, iters = [], []
+    losses, iters, launches, trials = [], [], [], []
     for _ in range(args.steps):
         loss, st = eng.step(cams, pts)
         losses.append(loss)
         iters.append(int(st["pcg_total"]))
+        launches.append(int(st["cg_launches"]))
+        trials.append(int(st["trials"]))
     xchg_us = eng.debug_time_exchange(200) if args.cg_partition else None
     loss, rmse = eng.cost(cams, pts)
     # every rank updated only its own tracks: assemble the full point array
@@ -147,6 +149,7 @@ def main():
                    cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
                    rmse=rmse, ref_rmse=ref_rmse, exchange_calls=eng.exchange_calls[0], n_obs=int(prob.n_obs),
                    cg_partition=bool(args.cg_partition), rows=rows, pcg_iters=iters, xchg_us=xchg_us,
+                   ranks_per_device=getattr(eng, "ranks_per_device", 1), cg_launches=launches, trials=trials,
                    losses_hex=[float(x).hex() for x in losses],
                    params_sha=hashlib.sha256(cams.cpu().numpy().tobytes() + full.numpy().tobytes()).hexdigest(),
                    cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all) if cams_all else None)
