@@ -1665,9 +1665,10 @@ struct DeviceCache {
     struct Buf {
         size_t bytes;
         int dev;
+        bool uc;  // uncached device memory (hipDeviceMallocUncached)
     };
     std::mutex m;
-    std::map<std::pair<int, size_t>, std::vector<void*>> free;  // (device, size) -> pointers
+    std::map<std::pair<int, size_t>, std::vector<void*>> free;  // (2 * device + uncached, size) -> pointers
     size_t bytes = 0;
     std::unordered_map<void*, Buf> info;  // every pointer dalloc handed out (cached or fresh)
 };
@@ -1692,7 +1693,7 @@ size_t release_cache() {
         std::lock_guard<std::mutex> lk(c.m);
         for (auto& kv : c.free)
             for (void* q : kv.second) {
-                drop.emplace_back(q, kv.first.first);
+                drop.emplace_back(q, kv.first.first / 2);
                 c.info.erase(q);
             }
         c.free.clear();
@@ -1710,17 +1711,20 @@ size_t release_cache() {
     return n;
 }
 
-int dalloc(insfm_ba* h, void** p, size_t bytes) {
+// uc: uncached device memory (the CG's cross-workgroup hand-off buffers: their loads, stores and atomics skip the L2s,
+// config 3: 10.4-11.0 -> 9.3-9.7 us per k_tl_cgp iteration; profiles/r4_v7/)
+int dalloc(insfm_ba* h, void** p, size_t bytes, bool uc = false) {
     if (bytes == 0) bytes = 16;
     bytes = (bytes + 255) & ~(size_t)255;
     DeviceCache& c = device_cache();
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const int key = 2 * dev + (uc ? 1 : 0);
     bool hit = false;
     {
         std::lock_guard<std::mutex> lk(c.m);
-        auto it = c.free.lower_bound(std::make_pair(dev, bytes));
-        if (it != c.free.end() && it->first.first == dev && it->first.second <= 2 * bytes && !it->second.empty()) {
+        auto it = c.free.lower_bound(std::make_pair(key, bytes));
+        if (it != c.free.end() && it->first.first == key && it->first.second <= 2 * bytes && !it->second.empty()) {
             *p = it->second.back();
             it->second.pop_back();
             c.bytes -= it->first.second;
@@ -1733,11 +1737,12 @@ int dalloc(insfm_ba* h, void** p, size_t bytes) {
         if (diag("poison")) (void)hipMemset(*p, 0xff, bytes);
         return 0;
     }
-    hipError_t e = hipMalloc(p, bytes);
+    auto alloc = [&] { return uc ? hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached) : hipMalloc(p, bytes); };
+    hipError_t e = alloc();
     if (e == hipErrorOutOfMemory) {  // give the parked buffers back and try once more
         (void)hipGetLastError();
         release_cache();
-        e = hipMalloc(p, bytes);
+        e = alloc();
     }
     if (e != hipSuccess) {
         h->err = std::string("hipMalloc(") + std::to_string(bytes) + ") failed: " + hipGetErrorString(e);
@@ -1745,7 +1750,7 @@ int dalloc(insfm_ba* h, void** p, size_t bytes) {
     }
     {
         std::lock_guard<std::mutex> lk(c.m);
-        c.info[*p] = DeviceCache::Buf{bytes, dev};
+        c.info[*p] = DeviceCache::Buf{bytes, dev, uc};
     }
     h->allocs.push_back(*p);
     if (diag("poison")) (void)hipMemset(*p, 0xff, bytes);
@@ -1767,7 +1772,7 @@ void dfree_all(insfm_ba* h) {
                 c.info.erase(it);
                 drop.push_back(q);
             } else {
-                c.free[std::make_pair(b.dev, b.bytes)].push_back(q);
+                c.free[std::make_pair(2 * b.dev + (b.uc ? 1 : 0), b.bytes)].push_back(q);
                 c.bytes += b.bytes;
             }
         }
@@ -3476,6 +3481,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     }
     if ((rc = upload(h, &h->work, work.data(), work.size()))) return fail(rc, "");
     auto dd = [&](double** p, size_t n) { return dalloc(h, (void**)p, n * sizeof(double)); };
+    // the CG's cross-workgroup hand-off buffers (atomic partial sums, exchanged w, tagged granules, barrier words) in
+    // uncached device memory (INSFM_DIAG=cgp_cached: ordinary memory, for A/B runs)
+    const bool uc = !diag("cgp_cached");
+    auto hand = [&](void** p, size_t bytes) { return dalloc(h, p, bytes, uc); };
     // W: [3][D] records per observation (global positioning: its 32-B {u, beta^2} records fit in the same buffer)
     if ((rc = dd(&h->W, (size_t)Nl * D * 3 + 2))) return fail(rc, "");
     if ((rc = dd(&h->V, (size_t)Pl * 6))) return fail(rc, "");
@@ -3700,8 +3709,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
             tl.Racc = nullptr;
             tl.Gacc = nullptr;
             if (!desc->deterministic && desc->world_size <= 1 && !desc->allreduce) {
-                if ((rc = dd(&tl.Racc, 3 * (size_t)m))) return fail(rc, "");
-                if ((rc = dd(&tl.Gacc, 3 * 3 * (size_t)nc))) return fail(rc, "");
+                if ((rc = hand((void**)&tl.Racc, sizeof(double) * 3 * (size_t)m))) return fail(rc, "");
+                if ((rc = hand((void**)&tl.Gacc, sizeof(double) * 3 * 3 * (size_t)nc))) return fail(rc, "");
                 if (hipMemsetAsync(tl.Racc, 0, sizeof(double) * 3 * (size_t)m, h->stream) != hipSuccess ||
                     hipMemsetAsync(tl.Gacc, 0, sizeof(double) * 9 * (size_t)nc, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "Racc clear");
@@ -3791,18 +3800,18 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                         : (nb == 64 ? (const void*)k_tl_cgp<64, false> : (const void*)k_tl_cgp<128, false>),
                     kCgpThreads, 0);
             if (ce == hipSuccess && per_cu >= 1 && grid <= ncu) {
-                if ((rc = dd(&h->cgp_wx, 2 * cd))) return fail(rc, "");
-                if ((rc = dalloc(h, (void**)&h->cgp_yg, sizeof(unsigned long long) * 2 * kCoarseMax))) return fail(rc, "");
+                if ((rc = hand((void**)&h->cgp_wx, sizeof(double) * 2 * cd))) return fail(rc, "");
+                if ((rc = hand((void**)&h->cgp_yg, sizeof(unsigned long long) * 2 * kCoarseMax))) return fail(rc, "");
                 if (hipMemsetAsync(h->cgp_yg, 0, sizeof(unsigned long long) * 2 * kCoarseMax, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "cgp granules");
-                if ((rc = dalloc(h, (void**)&h->cgp_sync, sizeof(unsigned) * kCgpSyncWords))) return fail(rc, "");
+                if ((rc = hand((void**)&h->cgp_sync, sizeof(unsigned) * kCgpSyncWords))) return fail(rc, "");
                 if (hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "cgp barrier words");
                 if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, kCgpTraceLen))) return fail(rc, "");
                 if (det) {
                     const size_t nr = sizeof(unsigned long long) * 2 * 12 * (size_t)grid * kCgpRows;
                     const size_t ng = sizeof(unsigned long long) * 2 * 2 * 12 * (size_t)kCgpMaxClusters;
-                    if ((rc = dalloc(h, (void**)&h->cgp_runs, nr)) || (rc = dalloc(h, (void**)&h->cgp_cgran, ng)))
+                    if ((rc = hand((void**)&h->cgp_runs, nr)) || (rc = hand((void**)&h->cgp_cgran, ng)))
                         return fail(rc, "");
                     if (hipMemsetAsync(h->cgp_runs, 0, nr, h->stream) != hipSuccess ||
                         hipMemsetAsync(h->cgp_cgran, 0, ng, h->stream) != hipSuccess)
