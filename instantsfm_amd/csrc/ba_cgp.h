@@ -25,8 +25,8 @@
 // (status 4), which every waiting workgroup checks; a single-rank host then repeats the solve on the launch path and
 // stays there.
 // Two variants: per-cluster atomic partial sums (single rank, non-deterministic), and DET, a fixed summation order
-// (deterministic mode and every rank of the replicated multi-rank CG: cluster owners sum the workgroups' run partials
-// in order and publish them as tagged granules).
+// (deterministic mode and every rank of the replicated multi-rank CG): each workgroup run's partials are stored in a
+// parity buffer before the grid barrier, and after it every workgroup sums each cluster's runs itself in run order.
 // Host eligibility (ba_kernels.hip, create): D = 8, host-mapped progress word, rows of at most NB = 128 blocks stored in
 // cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row, and every workgroup resident at
 // once (one per CU) -- for ranks sharing a GPU, all of their grids at once.
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                                                           const double* __restrict__ Lf, CgBufs cg, TlBufs tl,
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
                                                           double* wx, unsigned long long* yg, unsigned tag0,
-                                                          unsigned* sync, unsigned epoch0, int oseg, unsigned long long* rung,
+                                                          unsigned* sync, unsigned epoch0, int oseg, double* runs,
                                                           unsigned long long* cgran, double* trace) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
@@ -208,6 +208,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     __shared__ double vec[kCgpRows][8][D];             // the row's r u w z q s p x
     __shared__ int jn[kCgpWaves][NB];                  // neighbour of each register block
     __shared__ int segc[kCgpRows][kCgpSegMax];         // neighbour cluster of each segment
+    __shared__ int clp[DET ? kCgpMaxClusters + 1 : 1];  // DET: the clusters' cluster-ordered position ranges
     __shared__ double prt[kCgpRows][12];               // each row's partials: r.u, w.u, ||L r||^2, Z~_i^T w (9)
     __shared__ int pcl[kCgpRows];                      // each row's cluster (-1: no row)
     __shared__ int bflag;
@@ -239,6 +240,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     const size_t own = (size_t)(has_row ? row : 0) * D + (lane & 7);
     {
         if (lane < nseg && lane < kCgpSegMax) segc[rl][lane] = tl.seg[s0 + lane].x;
+        if constexpr (DET)
+            for (int i = t; i <= nc; i += kCgpThreads) clp[i] = tl.cl_ptr[i];
         if (has_row) {
             Lrow[rl][lane] = Lf[(size_t)row * D * D + lane];
             for (int e = lane; e < BS; e += 64) Zrow[rl][e] = tl.Zt[(size_t)row * BS + e];
@@ -435,13 +438,13 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             double v = prt[rl][lane];
             for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
             if constexpr (DET) {
-                put_y(rung, pos * 12 + lane, tag0, v);
+                st_sc1(runs + (size_t)pos * 12 + lane, v);  // (parity 0: iteration 0's run partials)
             } else {
                 if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)lane * nc + ci, v);
                 else unsafeAtomicAdd(tl.Racc + (size_t)ci * MC + (lane - 3), v);
             }
         }
-        if constexpr (!DET) alive = cgp_barrier(sync, ++epoch, &bflag);
+        alive = cgp_barrier(sync, ++epoch, &bflag);
     }
     if (trace && blockIdx.x == 0 && t == 0) {
         trace[256] = (double)t_start;
@@ -458,49 +461,43 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         // every load of the phase is issued before the first wait: the scalar partials, this wave's gathers (lane
         // (a, b) loads entry b of the w of block 8 g + a), the restriction (all threads, into LDS), the E^-1 row
         const int b0 = it % 3;  // partial sums of this iteration (P2 of it - 1 added them)
-        const unsigned tg = tag0 + (unsigned)it;
         double gl[3][LNC];
         if constexpr (DET) {
-            // cluster owners (wave c for cluster c): the cluster's 12 partials of this iteration summed in a fixed order
-            // (the tagged partials of the cluster's workgroup runs, in run order, kCgpRunBatch loads in flight;
-            // iteration 0's from the setup above), published as tagged granules in the
-            // iteration's parity buffer.  No grid barrier: a workgroup holding every cluster's sums of this iteration
-            // knows every row finished the previous one (each stored its w before its run's partials).
-            unsigned long long* cgi = cgran + (size_t)(it & 1) * 2 * 12 * kCgpMaxClusters;
-            const int l12 = min(lane, 11);
-            bool ok = true;
-            for (int c = gw; ok && c < nc; c += gridDim.x * kCgpWaves) {
-                const int p0 = tl.cl_ptr[c], p1 = tl.cl_ptr[c + 1];
+            // every workgroup sums each cluster's 12 run partials of this iteration itself, in run order (the runs
+            // were stored before the grid barrier that ended the previous iteration, in its parity buffer): the same
+            // doubles in every workgroup, in a fixed order, no atomics
+            const double* rb = runs + (size_t)(it & 1) * gridDim.x * kCgpRows * 12;
+            constexpr int EPT = (12 * kCgpMaxClusters + kCgpThreads - 1) / kCgpThreads;
+            constexpr int RB = 6;  // run heads per cluster loaded at once (clusters with more take a second pass)
+            double x[EPT][RB];
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) {
+                const int e = min(t + q * kCgpThreads, 12 * nc - 1), c = e / 12, k = e - 12 * c;
+                const int p1 = clp[c + 1];
+                int p = clp[c];
+#pragma unroll
+                for (int r = 0; r < RB; ++r) {  // run heads: the cluster's first position, then every multiple of 4
+                    x[q][r] = ld_sc1(rb + (size_t)min(p, p1 - 1) * 12 + k);
+                    if (p < p1) p = (p / kCgpRows + 1) * kCgpRows;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < EPT; ++q) {
+                const int e0 = t + q * kCgpThreads, e = min(e0, 12 * nc - 1), c = e / 12, k = e - 12 * c;
+                const int p1 = clp[c + 1];
+                int p = clp[c];
                 double v = 0.0;
-                {
-                    for (int pb = p0; pb < p1;) {
-                        int hp[kCgpRunBatch], idx[kCgpRunBatch];
-                        double x[kCgpRunBatch];
-                        unsigned skip = 0;
-                        int p = pb;
 #pragma unroll
-                        for (int q = 0; q < kCgpRunBatch; ++q) {  // run heads: p0, then every multiple of kCgpRows
-                            hp[q] = p;
-                            idx[q] = min(p, p1 - 1) * 12 + l12;
-                            x[q] = 0.0;
-                            if (p >= p1) skip |= 1u << q;
-                            else p = (p / kCgpRows + 1) * kCgpRows;
-                        }
-                        if (!poll_wave(rung, idx, x, tg, sync, skip)) { ok = false; break; }
-#pragma unroll
-                        for (int q = 0; q < kCgpRunBatch; ++q)
-                            if (hp[q] < p1) v += x[q];
-                        pb = p;
+                for (int r = 0; r < RB; ++r) {
+                    if (p < p1) {
+                        v += x[q][r];
+                        p = (p / kCgpRows + 1) * kCgpRows;
                     }
                 }
-                if (ok && lane < 12) put_y(cgi, c * 12 + lane, tg, v);
+                for (; p < p1; p = (p / kCgpRows + 1) * kCgpRows) v += ld_sc1(rb + (size_t)p * 12 + k);
+                if (e0 < 12 * nc) rs[e0] = v;
             }
-            if (__syncthreads_or(!ok)) { alive = false; break; }
-            // every workgroup: all clusters' sums into LDS (rs), one poll for the scalars and the restriction
-            if (!poll_tagged<12 * kCgpMaxClusters>(cgi, [](int k) { return k; }, rs, 12 * nc, tg, sync)) {
-                alive = false;
-                break;
-            }
+            __syncthreads();
 #pragma unroll
             for (int q = 0; q < LNC; ++q) {
                 const int c = min(lane + 64 * q, nc - 1);
@@ -743,7 +740,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             double v = prt[rl][lane];
             for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
             if constexpr (DET) {
-                put_y(rung, pos * 12 + lane, tg + 1, v);  // (at the run's head position: read by the owner of ci)
+                // (at the run's head position, parity of iteration it + 1: every workgroup reads it after the barrier)
+                st_sc1(runs + (size_t)((it + 1) & 1) * gridDim.x * kCgpRows * 12 + (size_t)pos * 12 + lane, v);
             } else {
                 const int bsel = (it + 1) % 3;
                 if (lane < 3) unsafeAtomicAdd(tl.Gacc + (size_t)bsel * 3 * nc + (size_t)lane * nc + ci, v);
@@ -752,8 +750,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 2] = (double)wall_clock64();
         if (trace && t == 0 && it == kCgpTraceIt && blockIdx.x < 256) trace[1028 + blockIdx.x] = (double)wall_clock64();
-        if constexpr (!DET)
-            if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
+        if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 3] = (double)wall_clock64();
     }
     if (!alive && blockIdx.x == 0 && t == 0) {

@@ -1565,8 +1565,8 @@ struct insfm_ba {
     // issued behind the CG (k_tl_cgp holds every SIMD of its CUs, so a chain beside it would crawl on the rest)
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
     bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
-    unsigned long long* cgp_runs = nullptr;   // [grid * 4][12] tagged granule pairs: the cluster runs' partials (cgp_det)
-    unsigned long long* cgp_cgran = nullptr;  // [2][kCgpMaxClusters][12] granule pairs of the cluster sums (cgp_det)
+    double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
+    unsigned long long* cgp_cgran = nullptr;  // (unused)
     unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
     int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
@@ -2283,8 +2283,7 @@ int cgp_complete(insfm_ba* h, int* st) {
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
     {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
         if (st[0] == 1 || st[0] == 2) {
-            // (the setup's barrier and one per completed iteration; the DET variant has no grid barrier)
-            if (!h->cgp_det) h->cgp_epochs += (unsigned)st[1] + 1u;
+            h->cgp_epochs += (unsigned)st[1] + 1u;  // (the setup's barrier and one per completed iteration)
         } else {
             HIPCHK(hipStreamSynchronize(h->stream));
             HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
@@ -3809,13 +3808,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                     return fail(INSFM_BA_EHIP, "cgp barrier words");
                 if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, kCgpTraceLen))) return fail(rc, "");
                 if (det) {
-                    const size_t nr = sizeof(unsigned long long) * 2 * 12 * (size_t)grid * kCgpRows;
-                    const size_t ng = sizeof(unsigned long long) * 2 * 2 * 12 * (size_t)kCgpMaxClusters;
-                    if ((rc = hand((void**)&h->cgp_runs, nr)) || (rc = hand((void**)&h->cgp_cgran, ng)))
+                    if ((rc = hand((void**)&h->cgp_runs, sizeof(double) * 2 * 12 * (size_t)grid * kCgpRows)))
                         return fail(rc, "");
-                    if (hipMemsetAsync(h->cgp_runs, 0, nr, h->stream) != hipSuccess ||
-                        hipMemsetAsync(h->cgp_cgran, 0, ng, h->stream) != hipSuccess)
-                        return fail(INSFM_BA_EHIP, "cgp cluster granules");
                 }
                 h->cgp_det = det;
                 h->cgp_nb = nb;
