@@ -487,6 +487,9 @@ def solve_end_to_end(prob, dev):
             "first_update_s": round(first["update_s"], 4),
             "solve_total_s": round(t["total_s"], 4), "pack_s": round(t["pack_s"], 4),
             "create_s": round(t["create_s"], 4), "steps_s": round(t["steps_s"], 4),
+            "ms_per_step": round(1e3 * t["steps_s"] / max(1, t["steps"]), 3),
+            "step_ms": [round(x, 3) for x in t.get("step_ms", [])],
+            "first_solve_step_ms": [round(x, 3) for x in first.get("step_ms", [])],
             "update_s": round(t["update_s"], 4), "steps": t["steps"], "host_frac": round(host / t["total_s"], 4),
             "pack_phases_ms": {k: round(1e3 * v, 2) for k, v in t.get("pack_phases", {}).items()},
             "update_phases_ms": {k: round(1e3 * v, 2) for k, v in t.get("update_phases", {}).items()},

@@ -1711,6 +1711,48 @@ size_t release_cache() {
     return n;
 }
 
+// Process-wide helper streams, one per (HIP device, role): the side stream of the coarse-inverse chain (role 0, low
+// priority) and the camera-linearization stream (role 1).  Every handle of a device shares them, so the number of
+// hardware queues a process uses does not grow with the handles alive at once.  With per-handle streams, a TorchBA.Solve
+// run while another config-3 handle was alive (bench.py's solve_end_to_end beside its main engine) took 1.9-2.0 ms per
+// LM step instead of 1.17: its side chain landed on a queue that the dispatcher served behind k_schur, k_gj_step ran
+// 2-4x longer, and the main stream waited ~330 us per step for the lagged coarse inverse (profiles/r5_v1/).  Handles
+// on one device are driven one at a time (the reference builds a TorchBA per Solve, global_mapper.py:115), and all
+// cross-stream ordering is by the handle's own events, so sharing only serializes what would compete anyway.
+// INSFM_DIAG=own_streams restores per-handle streams (A/B).
+std::mutex& stream_pool_mutex() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+}
+std::map<std::pair<int, int>, hipStream_t>& stream_pool() {
+    static auto* p = new std::map<std::pair<int, int>, hipStream_t>();  // (never destroyed, like the device cache)
+    return *p;
+}
+hipError_t helper_stream(int role, int prio, hipStream_t* out) {
+    if (diag("own_streams")) return hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(stream_pool_mutex());
+    auto& pool = stream_pool();
+    auto it = pool.find(std::make_pair(dev, role));
+    if (it != pool.end()) {
+        *out = it->second;
+        return hipSuccess;
+    }
+    const hipError_t e = hipStreamCreateWithPriority(out, hipStreamNonBlocking, prio);
+    if (e == hipSuccess) pool[std::make_pair(dev, role)] = *out;
+    return e;
+}
+void release_helper_stream(hipStream_t s) {
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> lk(stream_pool_mutex());
+        for (auto& kv : stream_pool())
+            if (kv.second == s) return;  // pooled: stays for the next handle
+    }
+    (void)hipStreamDestroy(s);
+}
+
 // uc: uncached device memory (the CG's cross-workgroup hand-off buffers: their loads, stores and atomics skip the L2s,
 // config 3: 10.4-11.0 -> 9.3-9.7 us per k_tl_cgp iteration; profiles/r4_v7/)
 int dalloc(insfm_ba* h, void** p, size_t bytes, bool uc = false) {
@@ -2945,7 +2987,7 @@ void insfm_ba_destroy(insfm_ba* h) {
         if (e) (void)hipEventDestroy(e);
     if (h->side) {
         (void)hipStreamSynchronize(h->side);
-        (void)hipStreamDestroy(h->side);
+        release_helper_stream(h->side);
     }
     if (h->xstream) {
         (void)hipStreamSynchronize(h->xstream);
@@ -2953,7 +2995,7 @@ void insfm_ba_destroy(insfm_ba* h) {
     }
     if (h->aux) {
         (void)hipStreamSynchronize(h->aux);
-        (void)hipStreamDestroy(h->aux);
+        release_helper_stream(h->aux);
     }
     if (h->ev_lin0) (void)hipEventDestroy(h->ev_lin0);
     if (h->ev_lc) (void)hipEventDestroy(h->ev_lc);
@@ -3448,7 +3490,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     // before the Schur build adds them).
     {
         if (kind == 0 && desc->world_size <= 1 && !desc->allreduce) {
-            hipError_t e = hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking);
+            hipError_t e = helper_stream(1, 0, &h->aux);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lin0, hipEventDisableTiming);
             if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_lc, hipEventDisableTiming);
             if (e != hipSuccess) return fail(INSFM_BA_EHIP, std::string("linearization stream: ") + hipGetErrorString(e));
@@ -3742,7 +3784,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         // normal and high: no measured effect either way, round 1)
         int prio_lo = 0, prio_hi = 0;
         if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-        if (e == hipSuccess) e = hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo);
+        if (e == hipSuccess) e = helper_stream(0, prio_lo, &h->side);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_built, hipEventDisableTiming);
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);

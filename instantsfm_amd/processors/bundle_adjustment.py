@@ -309,6 +309,7 @@ class TorchBA:
         t2 = time.perf_counter()
         window_size = 4                                                                       # :128-150
         loss_history = []
+        step_ms, step_stats = [], []
         it = range(opts['max_num_iterations'])
         bar = None
         if progress:
@@ -319,7 +320,10 @@ class TorchBA:
             except ImportError:
                 pass
         for _ in it:
+            ts = time.perf_counter()
             loss, stats = eng.step(cams_t, pts_t)
+            step_ms.append(1e3 * (time.perf_counter() - ts))
+            step_stats.append(stats)
             self.last_stats = stats
             loss_history.append(loss)
             if len(loss_history) >= 2 * window_size:
@@ -347,4 +351,5 @@ class TorchBA:
         t4 = time.perf_counter()
         self.timings.update(create_s=t2 - t1, steps_s=t3 - t2, update_s=t4 - t3, total_s=t4 - t0,
                             update_phases=dict(cost=t3a - t3, write_back=t3b - t3a, close=t4 - t3b),
-                            steps=len(loss_history), final_rmse=self.final_rmse)
+                            steps=len(loss_history), final_rmse=self.final_rmse, step_ms=step_ms,
+                            step_stats=step_stats)
