@@ -33,7 +33,7 @@ def w_record_doubles(D):
     return 3 * D
 
 
-def algorithmic_bytes(kernel, C, P, N, D, nnzb):
+def algorithmic_bytes(kernel, C, P, N, D, nnzb, extra=None):
     """Compulsory HBM bytes of one launch (every input byte read once, every output byte written once)."""
     if kernel == "k_schur":
         return (N * w_record_doubles(D) * 8  # W_o records
@@ -57,6 +57,15 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb):
                 + 8 * C * D * 8        # z, q, s, p, x, r, u, w written
                 + C * D * D * 8        # L_i (true-residual norm)
                 + 3 * C * 8 + C * (D + 1) * 8)  # row partials and restriction partials written
+    if kernel == "k_tl_cgp":
+        # one launch = one whole two-level PCG solve (csrc/ba_cgp.h): S~'s unique off-diagonal blocks once (the kernel
+        # holds each row's blocks of both triangles in registers, i.e. reads 2x this), Z~ and L_i once, the row vectors
+        # in and out once; per iteration the coarse rows of E^-1 once (y = E^-1 R), the exchanged w written and
+        # gathered once, and the per-cluster partials / tagged y granules (written and read once)
+        off = nnzb - C
+        m, nc, iters = extra["m"], extra["nc"], extra["iters"]
+        return (off * D * D * 8 + C * D * (D + 1) * 8 + C * D * D * 8 + 16 * C * D * 8
+                + iters * (m * m * 8 + 2 * C * D * 8 + 2 * 16 * m + 2 * 8 * (3 * nc + m)))
     if kernel == "k_lin_points":
         return (N * 2 * 8              # observed uv
                 + N * 4 * 2            # cam, ptl
@@ -742,13 +751,6 @@ def main():
             rmse_conv = eng.cost(ci, pi)[1]
     eng.set_timing(False)
     tl = args.precond == 1
-    us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
-    us_schur = eng.debug_time_kernel(1, 5)
-    us_tl_iter = eng.debug_time_kernel(2, 50) if tl else None
-    us_tl_setup = eng.debug_time_kernel(4, 10) if tl else None
-    us_lin = eng.debug_time_kernel(5, 20)
-    us_gj = eng.debug_time_kernel(6, 10) if tl else None     # the coarse inverse (k_gj_pinv0 + nB k_gj_step)
-    us_erow = eng.debug_time_kernel(7, 10) if tl else None   # the E build (k_tl_erow + k_tl_ereduce)
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))
@@ -756,45 +758,66 @@ def main():
     ph = np.sum([s["time_ms"] for s in istats], axis=0)
     trials = sum(s["trials"] for s in stats)
     cg_launches = sum(s["cg_launches"] for s in stats)
-    kern = {
-        ("k_tl_pspmv" if tl else "k_cg_iter"): (us_cg * cg_launches, cg_launches, us_cg,
-                                               algorithmic_bytes("k_tl_pspmv" if tl else "k_cg_iter", C, Pl, Nl, D, nnzb)),
-        "k_schur": (us_schur * trials, trials, us_schur, algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb)),
-    }
+    # which CG the default path runs: the persistent k_tl_cgp (one launch per solve) when this handle is eligible
+    cgp = eng.debug_time_cgp(10) if tl else None
+    us_schur = eng.debug_time_kernel(1, 5)
+    us_lin = eng.debug_time_kernel(5, 20)
+    us_gj = eng.debug_time_kernel(6, 10) if tl else None     # the coarse inverse (k_gj_pinv0 + nB k_gj_step)
+    us_erow = eng.debug_time_kernel(7, 10) if tl else None   # the E build (k_tl_erow + k_tl_ereduce)
+    kern = {}  # name -> (device us per step, launches per step, us per launch, algorithmic bytes per launch, extra)
+    steps_k = float(args.steps)
+    if cgp is not None:
+        us_cgp, us_pc0, it_cgp = cgp
+        m = eng.coarse_dim()
+        ext = {"m": m, "nc": m // (D + 1), "iters": it_cgp}
+        kern["k_tl_cgp"] = (us_cgp * cg_launches / steps_k, cg_launches / steps_k, us_cgp,
+                            algorithmic_bytes("k_tl_cgp", C, Pl, Nl, D, nnzb, ext), ext)
+    else:
+        kcg = "k_tl_pspmv" if tl else "k_cg_iter"
+        us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
+        kern[kcg] = (us_cg * cg_launches / steps_k, cg_launches / steps_k, us_cg,
+                     algorithmic_bytes(kcg, C, Pl, Nl, D, nnzb), None)
+    kern["k_schur"] = (us_schur * trials / steps_k, trials / steps_k, us_schur,
+                       algorithmic_bytes("k_schur", C, Pl, Nl, D, nnzb), None)
+    kern["k_lin_points"] = (us_lin, 1.0, us_lin, algorithmic_bytes("k_lin_points", C, Pl, Nl, D, nnzb), None)
+    # the dominant kernel: the most device time per LM step on the default path (launches per step x hipEvent-timed
+    # average launch)
     name = max(kern, key=lambda k: kern[k][0])
-    _, launches, avg_us, nbytes = kern[name]
-    achieved = nbytes / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0
-    traffic = None
+    traffic_tab = {}
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             tr = json.load(f)
-        if tr.get("config") == args.config and name in tr.get("kernels", {}):
-            traffic = tr["kernels"][name]["hbm_bytes_per_launch"]
+        if tr.get("config") == args.config:
+            traffic_tab = {k: v["hbm_bytes_per_launch"] for k, v in tr.get("kernels", {}).items()}
     except (OSError, ValueError):
         pass
-    roof = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(nbytes), "launches_per_run": int(launches),
-            "timing": "hipEvents on the library stream around 100 back-to-back launches (insfm_ba_debug_time_kernel)"}
 
-    # the next kernels by time per step, on the same footing (algorithmic bytes / hipEvent-timed launch)
-    others = []
-    for kname, us, nb in ((("k_tl_pspmv" if tl else "k_cg_iter"), us_cg,
-                           algorithmic_bytes("k_tl_pspmv" if tl else "k_cg_iter", C, Pl, Nl, D, nnzb)),
-                          ("k_lin_points", us_lin, algorithmic_bytes("k_lin_points", C, Pl, Nl, D, nnzb))):
-        if kname == name or not us:
-            continue
-        ach = nb / (us * 1e-6) / 1e9
-        others.append({"kernel": kname, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(ach / HBM_PEAK_GBS, 4), "avg_launch_us": round(us, 3),
-                       "algorithmic_bytes_per_launch": int(nb),
-                       "timing": "back-to-back launches (hipEvents): for k_lin_points that is the sustained rate of its "
-                                 "384-MB W write; in the step its trace time is shorter (profiles/r2_v6/kernel_stats.csv)"
-                                 if kname == "k_lin_points" else "back-to-back launches (hipEvents)"})
+    def roof_entry(kname):
+        per_step, lps, avg_us, nbytes, ext = kern[kname]
+        ach = nbytes / (avg_us * 1e-6) / 1e9 if avg_us > 0 else 0.0
+        e = {"kernel": kname, "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic_tab.get(kname),
+             "avg_launch_us": round(avg_us, 3), "algorithmic_bytes_per_launch": int(nbytes),
+             "launches_per_step": round(lps, 3), "device_us_per_step": round(per_step, 2),
+             "timing": "hipEvents on the library stream (insfm_ba_debug_time_kernel / insfm_ba_debug_time_cgp)"}
+        if kname == "k_tl_cgp":
+            e.update(iterations_per_solve=round(ext["iters"], 2),
+                     us_per_iteration_incl_setup_share=round(avg_us / max(ext["iters"], 1.0), 3),
+                     bytes_formula="8*[(nnzb-C)*D^2 + C*D*(D+1) + C*D^2 + 16*C*D + iters*(m^2 + 2*C*D + 4*m + 2*(3*nc+m))]",
+                     timing="hipEvents around the k_tl_cgp launch of a solve re-run from its rhs "
+                            "(insfm_ba_debug_time_cgp; the coarse solve of r0 runs inside it since round 5)")
+        if kname == "k_lin_points":
+            e["timing"] = ("back-to-back launches (hipEvents): the sustained rate of its 384-MB record write; in the step "
+                           "it overlaps the previous solve's coarse-inverse chain")
+        return e
+    roof = roof_entry(name)
+    roof["timing"] = roof["timing"] + "; dominant = most device time per LM step on the default path"
+    others = [roof_entry(k) for k in sorted(kern, key=lambda k: -kern[k][0]) if k != name]
 
-    # the side chain of the two-level preconditioner (runs on the side stream, overlapping the CG): the Gauss-Jordan
-    # inversion of E against the FP64 matrix peak (2 m^3 flops; its tile products are v_mfma_f64_16x16x4f64), the E
-    # build against HBM (it streams the full-row S~ copy once plus Z~)
+    # the side chain of the two-level preconditioner (runs on the side stream, overlapping the next linearization /
+    # Schur build): the Gauss-Jordan inversion of E against the FP64 matrix peak (2 m^3 flops; its tile products are
+    # v_mfma_f64_16x16x4f64), the E build against HBM
+    chain_situ_ms = float(ph[6]) / args.steps if len(ph) > 6 else None
     if tl:
         m = eng.coarse_dim()
         nb_gj = (m + 31) // 32
@@ -804,14 +827,18 @@ def main():
                        "achieved": round(tfs, 3), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": round(tfs / FP64_PEAK_TFS, 4), "avg_launch_us": round(us_gj / (nb_gj + 1), 3),
                        "chain_us": round(us_gj, 2), "algorithmic_flops_per_chain": int(flops),
-                       "timing": "back-to-back chains (hipEvents), main stream alone; in the step it overlaps the CG"})
+                       "chain_in_situ_us_per_step": None if chain_situ_ms is None else round(1e3 * chain_situ_ms, 2),
+                       "timing": "chain_us: back-to-back chains (hipEvents), main stream alone; chain_in_situ_us_per_step: "
+                                 "the side stream's E build + inversion per LM step in the instrumented replay (events "
+                                 "on the side stream around each chain), overlapping the next linearization / Schur"})
         nbe = 2 * (nnzb - C) * D * (D + (D & 1)) * 8 + C * D * (D + 1) * 8
         ach = nbe / (us_erow * 1e-6) / 1e9 if us_erow else 0.0
-        others.append({"kernel": "k_tl_erow + k_tl_ereduce (E build)", "bound": "hbm", "achieved": round(ach, 2),
+        others.append({"kernel": "k_tl_erow + k_tl_ereduce (E build; behind k_tl_cgp only k_tl_ereduce runs)",
+                       "bound": "hbm", "achieved": round(ach, 2),
                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                        "avg_launch_us": round(us_erow, 3), "algorithmic_bytes_per_launch": int(nbe),
-                       "timing": "back-to-back builds with the full grid on the main stream (hipEvents); in the step it "
-                                 "runs on the side stream with at most 256 workgroups"})
+                       "timing": "back-to-back builds with the full grid on the main stream (hipEvents); on the default "
+                                 "path k_tl_cgp writes the segments and only k_tl_ereduce runs"})
 
     out = {
         "metric": "LM-BA iterations/sec (+ final reprojection RMSE)",
@@ -838,17 +865,31 @@ def main():
         "trials": trials,
         "phase_ms_per_step": {k: round(float(v) / args.steps, 3) for k, v in
                               zip(["linearize", "k_schur", "linear_solve", "backsub_update", "trial_cost",
-                                   "cg_iterations"], ph)},
-        "kernel_us": {("k_tl_pspmv" if tl else "k_cg_iter"): round(us_cg, 3), "k_schur": round(us_schur, 2),
-                      "two_level_iteration": us_tl_iter and round(us_tl_iter, 3),
-                      "two_level_setup": us_tl_setup and round(us_tl_setup, 2), "k_lin_points": round(us_lin, 2)},
+                                   "cg_iterations", "coarse_chain_side_stream"], ph)},
+        "kernel_us": dict({k: round(v[2], 3) for k, v in kern.items()},
+                          **({"k_tl_cgp_iterations": round(cgp[2], 2)}
+                             if cgp is not None else {})),
         "preconditioner": "two-level (block-Jacobi + camera-cluster similarity coarse space)" if tl else "block-Jacobi",
         "roofline": roof,
         "roofline_next_kernels": others,
     }
+    if world > 1 or eng.exchange_calls[0]:
+        from instantsfm_amd.engine import CG_PATHS
+        xspan = float(ph[7]) / args.steps if len(ph) > 7 else 0.0
+        out["dist"] = {"backend": dist.get_backend() if dist is not None else None, "world_size": world,
+                       "rank0_shard_points": Pl, "rank0_shard_obs": Nl,
+                       "cg_path": CG_PATHS.get(eng.cg_path, str(eng.cg_path)), "cg_path_code": eng.cg_path,
+                       "ranks_per_device": getattr(eng, "ranks_per_device", 1),
+                       "exchange_calls": eng.exchange_calls[0],
+                       "exchange_callback_host_ms_per_step": round(1e3 * eng.exchange_calls[1] / (2 * args.steps), 4),
+                       "exchange_span_ms_per_step": round(xspan, 4),
+                       "note": "exchange_span: the chunked [S | b] all-reduce's span on the exchange stream per LM step "
+                               "in the instrumented replay (first chunk issued -> b reduced; overlaps the Schur build); "
+                               "callback host ms: time inside the synchronous callbacks ([U | g_c], trial scalars) over "
+                               "the timed + replayed steps"}
     if rank == 0 and world == 1 and not args.no_solve:
         out["solve_end_to_end"] = solve_end_to_end(prob, dev)
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cb = cpu_baseline(prob, args.cpu_max_steps, cluster_size=args.cluster_size)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["cpu_final_rmse_px"] = cb["final_rmse_px"]

@@ -140,6 +140,16 @@ int insfm_ba_set_exchange(insfm_ba* h, double* dev_buf, int64_t count);
  * until a grid barrier times out); otherwise every rank takes the launch-per-iteration CG, so that all ranks round
  * alike.  Default 1 (one GPU per rank). */
 int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks);
+/* Which CG this handle runs: out[0] = 0 the launch-per-iteration two-level / block-Jacobi CG, 1 the persistent
+ * k_tl_cgp with atomic cluster sums (single rank), 2 the persistent k_tl_cgp in its fixed-order form (deterministic
+ * mode, replicated multi-rank CG), 3 the row-partitioned multi-rank CG; out[1] the k_tl_cgp grid (workgroups), out[2]
+ * the workgroups of it the device holds at once, out[3] its register blocks per row (0: not eligible). */
+int insfm_ba_cg_info(const insfm_ba* h, int32_t* out);
+/* on = 0: this handle leaves the persistent k_tl_cgp for the launch-per-iteration CG (ranks of a replicated
+ * multi-rank CG must all take the same path: the engine all-gathers insfm_ba_cg_info and turns it off everywhere
+ * unless every rank runs the fixed-order k_tl_cgp and every GPU holds all grids placed on it).  on = 1: EINVAL unless
+ * the handle already runs it. */
+int insfm_ba_set_persistent_cg(insfm_ba* h, int32_t on);
 
 /* Row-partitioned two-level CG across ranks (multi-rank handles with precond 1): each rank applies
  * the reduced camera matrix to its own rows (whole camera clusters) and writes those rows' CG partials straight into
@@ -184,6 +194,12 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host_out);
  * (BA with stored W records only), 6 the coarse inverse alone (k_gj_pinv0 + one k_gj_step per 32-wide block of E),
  * 7 the E build alone (k_tl_erow + k_tl_ereduce).  Overwrites CG scratch state. */
 int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double* us_per_launch);
+/* The persistent two-level CG (k_tl_cgp, the default D = 8 solve) of the last solve, re-run `reps` times from its
+ * right-hand side: out[0] device microseconds per k_tl_cgp launch (a whole solve: the coarse solve of r0, the in-kernel
+ * setup and every iteration), out[1] 0 (reserved: the setup launch that preceded it until round 4), out[2] PCG
+ * iterations per solve.  EINVAL when the handle does not
+ * run k_tl_cgp.  Overwrites CG scratch state.  (Measurement of PCG(tol=1e-5), bundle_adjustment.py:117.) */
+int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out);
 /* Camera cluster labels [C] of the two-level preconditioner's coarse space (HOST out); returns the cluster count. */
 int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);
 /* Number of upper-triangular camera blocks of the reduced system (incl. the diagonal). */

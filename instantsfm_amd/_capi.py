@@ -51,7 +51,7 @@ class Stats(ctypes.Structure):
     def as_dict(self):
         return dict(loss=self.loss, loss_before=self.loss_before, damping=self.damping, trials=self.trials,
                     rejects=self.rejects, pcg_iters=self.pcg_iters_last, pcg_total=self.pcg_iters_total,
-                    failed=self.solver_failed, cg_launches=self.cg_launches, time_ms=list(self.time_ms)[:6],
+                    failed=self.solver_failed, cg_launches=self.cg_launches, time_ms=list(self.time_ms),
                     coarse_used=self.coarse_used)
 
 
@@ -60,8 +60,8 @@ SYMBOLS = ("insfm_build_info", "insfm_ba_default_desc", "insfm_ba_create", "insf
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
            "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters", "insfm_ba_debug_spd_inverse",
-           "insfm_ba_release_cache", "insfm_ba_set_ranks_per_device", "insfm_ba_cg_window", "insfm_ba_cg_attach", "insfm_ba_cg_partition",
-           "insfm_ba_debug_time_xchg",
+           "insfm_ba_release_cache", "insfm_ba_set_ranks_per_device", "insfm_ba_cg_info", "insfm_ba_set_persistent_cg", "insfm_ba_cg_window", "insfm_ba_cg_attach", "insfm_ba_cg_partition",
+           "insfm_ba_debug_time_xchg", "insfm_ba_debug_time_cgp",
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
            "insfm_gp_debug_get_ds",
            "insfm_undistort", "insfm_filter_reproj_normalized", "insfm_filter_angle", "insfm_filter_tri_angle",
@@ -140,6 +140,8 @@ def load(path=None):
     L.insfm_ba_set_exchange.restype = ctypes.c_int
     L.insfm_ba_debug_time_kernel.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, dp]
     L.insfm_ba_debug_time_kernel.restype = ctypes.c_int
+    L.insfm_ba_debug_time_cgp.argtypes = [vp, ctypes.c_int32, dp]
+    L.insfm_ba_debug_time_cgp.restype = ctypes.c_int
     L.insfm_ba_set_timing.argtypes = [vp, ctypes.c_int32]
     L.insfm_ba_set_timing.restype = ctypes.c_int
     L.insfm_ba_debug_clusters.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
@@ -150,6 +152,10 @@ def load(path=None):
     L.insfm_ba_release_cache.restype = ctypes.c_int64
     L.insfm_ba_set_ranks_per_device.argtypes = [vp, ctypes.c_int32]
     L.insfm_ba_set_ranks_per_device.restype = ctypes.c_int
+    L.insfm_ba_cg_info.argtypes = [vp, ctypes.POINTER(ctypes.c_int32)]
+    L.insfm_ba_cg_info.restype = ctypes.c_int
+    L.insfm_ba_set_persistent_cg.argtypes = [vp, ctypes.c_int32]
+    L.insfm_ba_set_persistent_cg.restype = ctypes.c_int
     L.insfm_ba_cg_window.argtypes = [vp, ctypes.c_char_p]
     L.insfm_ba_cg_window.restype = ctypes.c_int
     L.insfm_ba_cg_attach.argtypes = [vp, ctypes.c_char_p]

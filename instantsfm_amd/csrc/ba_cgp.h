@@ -31,6 +31,8 @@
 // cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row, and every workgroup resident at
 // once (one per CU) -- for ranks sharing a GPU, all of their grids at once.
 #pragma once
+#include <climits>
+
 #include "ba_common.h"
 #include "ba_twolevel.h"
 
@@ -186,14 +188,17 @@ __device__ __forceinline__ double uni(double v) {
 // trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
 // of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
 // barriers (workgroup 0).
+constexpr int kCgpPadSlot = INT_MIN;  // ssrc of a pad slot (a zero block)
+
 template <int NB, bool DET>
 __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __restrict__ nbr_ptr,
-                                                          const int* __restrict__ nbr_j, const double* __restrict__ Sn,
+                                                          const int* __restrict__ nbr_j, const double* __restrict__ S,
+                                                          const int* __restrict__ ssrc, const double* __restrict__ Li,
                                                           const double* __restrict__ Lf, CgBufs cg, TlBufs tl,
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
                                                           double* wx, unsigned long long* yg, unsigned tag0,
                                                           unsigned* sync, unsigned epoch0, int oseg, double* runs,
-                                                          unsigned long long* cgran, double* trace) {
+                                                          double* trace) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
     constexpr int NG = NB / 8;                          // gather loads per wave and iteration
@@ -204,6 +209,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     __shared__ double rs[DET ? 12 * kCgpMaxClusters : kCoarseMax];
     __shared__ double ys[kCoarseMax];                  // y of the iteration
     __shared__ double Lrow[kCgpRows][D * D];           // L_i (row a, column k)
+    __shared__ double Lirow[kCgpRows][D * D];          // L_i^-1 (row a, column k)
+    __shared__ int sq[kCgpWaves][NB];                  // S block of each register slot (ssrc: upper / ~lower / pad)
     __shared__ double Zrow[kCgpRows][BS];              // Z~_i (row a, column k)
     __shared__ double vec[kCgpRows][8][D];             // the row's r u w z q s p x
     __shared__ int jn[kCgpWaves][NB];                  // neighbour of each register block
@@ -230,12 +237,54 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     const long long t_start = wall_clock64();
     double* V = &vec[rl][0][0];
     enum { VR = 0, VU = 8, VW = 16, VZ = 24, VQ = 32, VS = 40, VP = 48, VX = 56 };
+    // L_i^-1 applied to the row sums of an unscaled product: lane (a, b) holds after the butterfly over b the sum of
+    // row a in acc; lane la = lane & 7 gets (L_i^-1 sum)[la] = sum_{k <= la} L_i^-1[la][k] sum_k (k ascending)
+    auto lscale = [&](double acc) {
+        double sm[D], li[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) { sm[k] = __shfl(acc, 8 * k, 64); li[k] = Lirow[rl][(lane & 7) * D + k]; }
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (k <= (lane & 7)) v += li[k] * sm[k];
+        return v;
+    };
+    // v = L_i^-T x for the row's vector x (its 8 entries x8, in every lane): lane la gets sum_{k >= la} L_i^-1[k][la] x_k
+    auto ltscale = [&](const double (&x8)[D]) {
+        double li[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) li[k] = Lirow[rl][k * D + (lane & 7)];
+        double v = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+            if (k >= (lane & 7)) v += li[k] * x8[k];
+        return v;
+    };
     // ---- setup ----
-    // the row's blocks (slots past the row: zero, neighbour = the row itself, so the products need no guard)
+    // The operator is held UNSCALED (round 5): slot k of the row keeps S_ij (j = its neighbour) from the upper block
+    // pattern of S -- block ssrc >= 0 as stored, or block ~ssrc transposed for a lower neighbour -- and the block-Jacobi
+    // scaling S~_ij = L_i^-1 S_ij L_j^-T is applied to the vectors instead: every row publishes v_j = L_j^-T w_j and
+    // forms S~ w = L_i^-1 (sum_j S_ij v_j).  So no k_cg_scale launch and no 61-MB Sn copy in front of the CG (the
+    // first solve of an LM run, whose own coarse matrix k_tl_erow builds from Sn, still has them).
+    // The row's blocks (slots past the row: zero, neighbour = the row itself, so the products need no guard).
+    for (int k = lane; k < NB; k += 64) {
+        jn[wv][k] = k < nk ? nbr_j[n0 + k] : (has_row ? row : 0);
+        sq[wv][k] = k < nk ? ssrc[n0 + k] : kCgpPadSlot;
+    }
+    const int lt = b8 * D + a8;  // this lane's entry of a transposed block
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto slot_val = [&](int k) {  // entry (a8, b8) of S_ij for register slot k (branch-free: one load per slot)
+        const int q = sq[wv][k];
+        const bool pad = q == kCgpPadSlot;
+        const int e = pad ? 0 : (q >= 0 ? q : ~q);
+        const double v = S[(size_t)e * (D * D) + (q >= 0 ? lane : lt)];
+        return pad ? 0.0 : v;
+    };
     double sreg[NB];
 #pragma unroll
-    for (int k = 0; k < NB; ++k) sreg[k] = k < nk ? Sn[(size_t)(n0 + k) * (D * D) + lane] : 0.0;
-    for (int k = lane; k < NB; k += 64) jn[wv][k] = k < nk ? nbr_j[n0 + k] : (has_row ? row : 0);
+    for (int k = 0; k < NB; ++k) sreg[k] = slot_val(k);
     for (int e = t; e < kCgpRows * kCgpSegMax * BS; e += kCgpThreads) (&Aseg[0][0][0])[e] = 0.0;
     const size_t own = (size_t)(has_row ? row : 0) * D + (lane & 7);
     {
@@ -244,6 +293,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             for (int i = t; i <= nc; i += kCgpThreads) clp[i] = tl.cl_ptr[i];
         if (has_row) {
             Lrow[rl][lane] = Lf[(size_t)row * D * D + lane];
+            Lirow[rl][lane] = Li[(size_t)row * D * D + lane];
             for (int e = lane; e < BS; e += 64) Zrow[rl][e] = tl.Zt[(size_t)row * BS + e];
             const double* src = lane < 8 ? cg.r[0] : lane < 16 ? tl.u : lane < 24 ? cg.w[0] : lane < 32 ? cg.w[1]
                               : lane < 40 ? cg.r[1] : lane < 48 ? cg.s[0] : lane < 56 ? cg.p : cg.x;
@@ -252,10 +302,12 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     }
     __syncthreads();
     if (trace && blockIdx.x == 0 && t == 0) trace[578] = (double)wall_clock64();  // (blocks issued, LDS tables in)
-    // A_ic: lane (a, b) sums S~_ij[a][b] Z~_j[b][q] over the segment's blocks (segment boundaries are wave-uniform); at
-    // the segment's end the eight b lanes are summed by a fixed butterfly and lane (a, 0) writes row a of A_ic (one wave
-    // per row: each segment is written once, in a fixed order).  The Z~_j rows of ZC blocks at a time are staged in the
-    // wave's gather buffer by coalesced loads (all in flight together), then read back per lane.
+    // A_ic = S~_i,c Z~_c = L_i^-1 B_ic with B_ic = sum_{j in c} S_ij G_j (Z~_j = L_j^T G_j, G_j the unscaled basis):
+    // lane (a, b) sums S_ij[a][b] G_j[b][q] over the segment's blocks (segment boundaries are wave-uniform); at the
+    // segment's end the eight b lanes are summed by a fixed butterfly and lane (a, 0) writes row a of B_ic (one wave
+    // per row: each segment is written once, in a fixed order); then every segment is multiplied by L_i^-1 in place.
+    // The G_j rows of ZC blocks at a time are staged in the wave's gather buffer by coalesced loads (all in flight
+    // together), then read back per lane.
     if (nk > 0) {
         constexpr int ZC = NB * D / BS;            // blocks per staging chunk (14 for NB = 128)
         constexpr int ZU = (ZC * BS + 63) / 64;    // coalesced loads per lane and chunk
@@ -288,10 +340,10 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
             for (int u = 0; u < ZU; ++u) {
                 const int e = min(lane + 64 * u, ZC * BS - 1), c = e / BS;
-                zl[u] = tl.Zt[(size_t)jn[wv][min(k0 + c, NB - 1)] * BS + (e - c * BS)];
+                zl[u] = tl.Gb[(size_t)jn[wv][min(k0 + c, NB - 1)] * BS + (e - c * BS)];
             }
 #pragma unroll
-            for (int c = 0; c < ZC; ++c) sv[c] = Sn[(size_t)(n0 + min(k0 + c, nk - 1)) * (D * D) + lane];
+            for (int c = 0; c < ZC; ++c) sv[c] = slot_val(min(k0 + c, nk - 1));
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -326,6 +378,32 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         flush();
+        // A_ic = L_i^-1 B_ic for every segment (lane pair entries (a, q); the wave reads its B entries first)
+        const int ns = min(nseg, kCgpSegMax);
+        for (int sg = 0; sg < ns; ++sg) {
+            double* A = &Aseg[rl][sg][0];
+            double bo[2];
+            int eo[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int e = min(lane + 64 * h, BS - 1), a = e / MC, q = e - a * MC;
+                double v = 0.0;
+#pragma unroll
+                for (int k = 0; k < D; ++k)
+                    if (k <= a) v += Lirow[rl][a * D + k] * A[k * MC + q];
+                bo[h] = v;
+                eo[h] = lane + 64 * h;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (eo[h] < BS) A[eo[h]] = bo[h];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
     }
     const int ci = has_row ? tl.clab[row] : 0;
     if (lane == 0) pcl[rl] = has_row ? ci : -1;
@@ -356,10 +434,73 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             }
         }
     }
-    // ---- iteration 0's operator product (k_tl_pspmv's setup, folded in): w0 = u0 + S~ u0 with u0 = M~^-1 r0 from
-    // k_tl_pc's setup launch, z0 = q0 = 0; w0 into the exchange buffer of parity 0 and the partials of iteration 0
-    // (r0.u0, w0.u0, ||L r0||^2, Z~^T w0) published like P2's (atomic buffer 0 / runs tagged with iteration 0)
+    // ---- u0 = M~^-1 r0 (round 5: k_tl_pc's setup launch folded in; config 3 saved its 10-us launch and the gap
+    // in front of it).  The restriction R(r0): every workgroup sums k_tl_basis's row partials of each cluster itself,
+    // rows in cluster order (k_tl_pc's order, so the same doubles); the wave's own cluster's rows of y0 = E^-1 R
+    // (k_tl_pc's products and butterfly); u0_i = r0_i + Z~_i y0_ci.  u0 goes to the neighbours through the w exchange
+    // buffer of parity 1 (next written by P2 of iteration 0, two grid barriers later) behind one grid barrier, in
+    // front of which the per-cluster atomic buffers 0 and 1 are cleared (the setup's partials go to buffer 0, P2 of
+    // iteration 0 adds into buffer 1) and workgroup 0 reports whether the coarse correction is on.
     {
+        if (!DET) {
+            for (int q = blockIdx.x * kCgpThreads + t; q < 2 * (m + 3 * nc); q += gridDim.x * kCgpThreads)
+                st_sc1(q < 2 * m ? tl.Racc + q : tl.Gacc + (q - 2 * m), 0.0);
+        }
+        if (blockIdx.x == 0 && t == 0) {
+            cg.status[2] = use ? 1 : 0;  // reported as insfm_ba_stats.coarse_used
+            if (cg.prog) __hip_atomic_store(cg.prog + 3, use ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (use) {
+            for (int e = t; e < m; e += kCgpThreads) {
+                const int c2 = e / MC, k = e - c2 * MC;
+                const int r0 = tl.cl_ptr[c2], r1 = tl.cl_ptr[c2 + 1];
+                double v = 0.0;
+#pragma unroll 8
+                for (int mi = r0; mi < r1; ++mi) v += tl.rowR[(size_t)mi * MC + k];
+                rs[e] = v;
+            }
+        }
+        __syncthreads();
+        if (has_row) {
+            const int la = lane & 7;
+            double v = V[VR + la];
+            if (use) {
+                double yv[MC];
+#pragma unroll
+                for (int k = 0; k < MC; ++k) {
+                    const double* er = Einv + (size_t)(ci * MC + k) * m;
+                    double sy = 0.0;
+#pragma unroll
+                    for (int q = 0; q < LPL; ++q) {
+                        const int l = lane + 64 * q;
+                        if (l < m) sy += er[l] * rs[l];
+                    }
+                    yv[k] = wave_sum(sy);
+                }
+                double sz = 0.0;
+#pragma unroll
+                for (int k = 0; k < MC; ++k) sz += Zrow[rl][la * MC + k] * yv[k];
+                v += sz;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < D) V[VU + la] = v;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            double u8[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) u8[k] = V[VU + k];
+            const double v0 = ltscale(u8);  // the neighbours read L_i^-T u0
+            if (lane < D) st_sc1(wx + (size_t)C * D + (size_t)row * D + lane, v0);
+        }
+        alive = cgp_barrier(sync, ++epoch, &bflag);
+    }
+    // ---- iteration 0's operator product (k_tl_pspmv's setup, folded in): w0 = u0 + S~ u0, z0 = q0 = 0; w0 into the
+    // exchange buffer of parity 0 and the partials of iteration 0 (r0.u0, w0.u0, ||L r0||^2, Z~^T w0) published like
+    // P2's (atomic buffer 0 / runs tagged with iteration 0)
+    if (alive) {
         double uv8[NG];
         {
             int jr[NG];
@@ -367,7 +508,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             for (int g = 0; g < NG; ++g) jr[g] = jn[wv][8 * g + a8];
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int g = 0; g < NG; ++g) uv8[g] = tl.u[(size_t)jr[g] * D + b8];
+            for (int g = 0; g < NG; ++g) uv8[g] = ld_sc1(wx + (size_t)C * D + (size_t)jr[g] * D + b8);
         }
 #pragma unroll
         for (int g = 0; g < NG; ++g) wg[wv][8 * g + a8][b8] = uv8[g];
@@ -388,17 +529,14 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             acc += __shfl_xor(acc, 1, 64);
             acc += __shfl_xor(acc, 2, 64);
             acc += __shfl_xor(acc, 4, 64);
-            const double su = __shfl(acc, 8 * (lane & 7), 64);
+            const double su = lscale(acc);  // (S~ u0)_i = L_i^-1 sum_j S_ij v0_j
             const int la = lane & 7;
             const double u_ = V[VU + la], r_ = V[VR + la];
             const double w0 = u_ + su;  // (the diagonal block of S~ is I)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < D) {
-                V[VW + la] = w0; V[VZ + la] = 0.0; V[VQ + la] = 0.0;
-                st_sc1(wx + (size_t)row * D + lane, w0);
-            }
+            if (lane < D) { V[VW + la] = w0; V[VZ + la] = 0.0; V[VQ + la] = 0.0; }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -427,6 +565,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
+                const double v0 = ltscale(w8);  // the neighbours read L_i^-T w0
+                if (lane < D) st_sc1(wx + (size_t)row * D + lane, v0);
             }
             wave_sum3(g0, g1, g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
@@ -477,7 +617,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 int p = clp[c];
 #pragma unroll
                 for (int r = 0; r < RB; ++r) {  // run heads: the cluster's first position, then every multiple of 4
-                    x[q][r] = ld_sc1(rb + (size_t)min(p, p1 - 1) * 12 + k);
+                    x[q][r] = ld_sc1(rb + (size_t)max(min(p, p1 - 1), 0) * 12 + k);  // (an empty first cluster: 0)
                     if (p < p1) p = (p / kCgpRows + 1) * kCgpRows;
                 }
             }
@@ -634,7 +774,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             acc += __shfl_xor(acc, 1, 64);
             acc += __shfl_xor(acc, 2, 64);
             acc += __shfl_xor(acc, 4, 64);
-            sw = __shfl(acc, 8 * (lane & 7), 64);
+            sw = lscale(acc);  // (S~ w)_i = L_i^-1 sum_j S_ij v_j
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 0] = (double)wall_clock64();
         // ======== P2 ========
@@ -694,8 +834,6 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (lane < D) {
                 V[VZ + la] = zn; V[VQ + la] = qn; V[VS + la] = sn; V[VP + la] = pn;
                 V[VX + la] = xn; V[VR + la] = rn; V[VU + la] = un; V[VW + la] = wn;
-                // the row's new w for the neighbours (first: its write-back overlaps the partials below)
-                st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, wn);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -726,6 +864,9 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
+                // the row's new v = L_i^-T w for the neighbours (its write-back overlaps the partials' reductions)
+                const double vn = ltscale(w8);
+                if (lane < D) st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, vn);
             }
             wave_sum3(g0, g1, g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }

@@ -1330,7 +1330,7 @@ constexpr int kFinalThreads = 1024;
 __global__ __launch_bounds__(kFinalThreads) void k_final(const double* __restrict__ cost_part, int ncost,
                                                     const double* __restrict__ gp_part, int ngp,
                                                     const double* __restrict__ gc_part, int ngc, int* __restrict__ flags,
-                                                    double* __restrict__ result) {
+                                                    double* __restrict__ result, const int* __restrict__ cgst) {
     // the three partial arrays in one pass (every load of a round in flight together), each array still summed by
     // each thread in index order and then by the same butterfly and wave order: bitwise the sums of three separate
     // sum_partials passes, with one latency chain instead of three
@@ -1349,6 +1349,9 @@ __global__ __launch_bounds__(kFinalThreads) void k_final(const double* __restric
     if (threadIdx.x == 0) {
         result[0] = c2[0]; result[1] = c2[1]; result[2] = a[0]; result[3] = b[0];
         result[4] = (double)flags[0];
+        // a k_tl_cgp solve whose status the host reads after the cost: 1 when it aborted at a grid barrier (status 4).
+        // All-reduced with the other scalars, so every rank of a replicated CG sees whether any rank aborted.
+        result[5] = (cgst != nullptr && cgst[0] == 4) ? 1.0 : 0.0;
         flags[0] = 0;  // consumed: the next solve's point preparation starts from a clear flag
     }
 }
@@ -1459,10 +1462,13 @@ __global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__
                                                       long long npts) {
     const double loss = result[0];
     // cgst (a k_tl_cgp solve whose status the host reads afterwards): only a converged CG's trial can be accepted
-    const bool acc = result[4] == 0.0 && !(last < loss && can_reject) && (cgst == nullptr || cgst[0] == 1);
+    // (result[5]: a k_tl_cgp abort on any rank -- every rank then repeats the trial on the launch path)
+    const bool acc = result[4] == 0.0 && !(last < loss && can_reject) && (cgst == nullptr || cgst[0] == 1) &&
+                     result[5] == 0.0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         for (int k = 0; k < 5; ++k) pub[k] = result[k];
         pub[5] = acc ? 1.0 : 0.0;
+        pub[6] = result[5];
         __threadfence_system();
         __hip_atomic_store(reinterpret_cast<unsigned*>(pub + 8), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -1548,7 +1554,9 @@ struct insfm_ba {
     double damping = 0.0, down = 0.0, loss = 0.0;
     bool have_loss = false;
     int last_cg_iters = 16;
-    hipEvent_t ev[12]{};
+    hipEvent_t ev[18]{};  // 0-9 phase markers, 10-11 debug timing, 12-15 the side chain's start / end by slot,
+                          // 16-17 the chunked exchange's span on the exchange stream
+    bool chain_timed[2]{};  // set_timing: the side chain of that slot has timing events not yet harvested
     bool timing = false;
     // device time of the current step, accumulated per phase (ms): see insfm_ba_stats.time_ms
     double tms[8]{};
@@ -1566,7 +1574,8 @@ struct insfm_ba {
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
     bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
     double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
-    unsigned long long* cgp_cgran = nullptr;  // (unused)
+    int* cgp_src = nullptr;     // [n_nbr] S block of each CG slot: e (upper), ~e (lower, transposed), INT_MIN (pad)
+    bool sn_valid = false;      // Sn holds the scaled S~ of the current solve (k_cg_scale ran for it)
     unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
     int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
@@ -1641,6 +1650,8 @@ namespace {
 //                 persistent register-resident k_tl_cgp is eligible (A/B and parity of the two paths)
 //   cgp_trace     k_tl_cgp records gamma, delta, rho and its stop flag per iteration; printed after each solve
 //   cgp128        k_tl_cgp with 128 register blocks per row even for shorter rows (tests the wide variant)
+//   own_streams   per-handle side / linearization streams instead of the process-wide ones (A/B)
+//   chain_hold    timing only: the lagged coarse-inverse chain is never issued (later solves keep an older E^-1)
 bool diag(const char* name) {
     static const std::string v = [] { const char* e = std::getenv("INSFM_DIAG"); return std::string(e ? e : ""); }();
     const size_t n = std::strlen(name);
@@ -2141,15 +2152,33 @@ constexpr int kCgAhead = CG_AHEAD;
 // solve's setup, while the GPU is still in k_lin_points / k_schur: the host is then ~0.6 ms ahead of the GPU, the
 // launches cost the GPU nothing, and the chain overlaps the CG.  (Round 2 issued it piecemeal from the CG poll loop,
 // and a chain deferred past the CG was measured too: both slower)
+// set_timing: the device time of finished side chains (start after the wait on ev_E, end after the last Gauss-Jordan
+// unit) into phase slot 6 of the current step.  A chain issued behind the CG usually finishes during the next step, so
+// it is counted there; summed over the steps of a run every chain is counted once (but the last one).
+void harvest_chain_time(insfm_ba* h) {
+    for (int sl = 0; sl < 2; ++sl) {
+        if (!h->chain_timed[sl] || hipEventQuery(h->ev[14 + sl]) != hipSuccess) continue;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, h->ev[12 + sl], h->ev[14 + sl]) == hipSuccess) h->tms[6] += ms;
+        h->chain_timed[sl] = false;
+    }
+}
+
 int issue_side_chain(insfm_ba* h, int slot, bool have_oseg = false) {
     hipStream_t fs = h->side;
     HIPCHK(hipStreamWaitEvent(fs, h->ev_E, 0));
+    const bool tm = h->timing && !h->chain_timed[slot];
+    if (tm) HIPCHK(hipEventRecord(h->ev[12 + slot], fs));
     if (int rc = run_tl_build(h, slot, fs, have_oseg)) return rc;
     HIPCHK(hipEventRecord(h->ev_built, fs));
     h->built_pending = true;
     for (int u = 0; u <= gj_steps(h->tl.m); ++u)
         if (int rc = run_tl_gj_unit(h, slot, u, fs)) return rc;
     HIPCHK(hipEventRecord(h->ev_fact[slot], fs));
+    if (tm) {
+        HIPCHK(hipEventRecord(h->ev[14 + slot], fs));
+        h->chain_timed[slot] = true;
+    }
     return 0;
 }
 
@@ -2163,6 +2192,7 @@ int side_flush(insfm_ba* h) {
 // E^-1 under the lag rule, else its own (the main stream waits for the factorization).
 int run_tl_setup(insfm_ba* h, const double* cams) {
     const int slot = (int)(h->tl_solves & 1);
+    if (h->timing) harvest_chain_time(h);
     int rc = run_tl_basis(h, cams, h->stream);
     if (rc) return rc;
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
@@ -2257,14 +2287,9 @@ void launch_tl_iter_x(insfm_ba* h, int it, int maxit, double tol2) {
     pspmv(it);
 }
 
-// The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): k_tl_pc's setup launch (u0),
-// then one launch for the operator product of the setup and every iteration.
+// The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): one launch for the coarse
+// solve of r0 (u0 = M~^-1 r0, formerly k_tl_pc's setup launch), the setup's operator product and every iteration.
 int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
-    constexpr int D = 8;
-    // u0 = M~^-1 r0 (k_tl_pc's setup, which also clears the atomic partial buffers 0 and 1); k_tl_cgp forms
-    // w0 = S~ u0 and iteration 0's partials itself (the launch path's k_tl_pspmv setup launch streamed S~ once more)
-    k_tl_pc<D><<<h->tl.nc, kPcThreads, h->pc_lds, h->stream>>>(-1, h->C, maxit, tol2, h->pc_rows, h->cg, h->tl,
-                                                               h->tl.Einv);
     if (h->cgp_epochs > (1u << 24)) {  // (counter headroom: zero them now and then; an abort zeroes them too)
         HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
         h->cgp_epochs = 0;
@@ -2273,9 +2298,10 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     static std::atomic<int> faults{diag("cgp_fault") ? 1 : 0};
     const bool fault = faults.load() > 0 && faults.fetch_sub(1) > 0;
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->Sn,
-                           h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg, h->cgp_tag, h->cgp_sync,
-                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_cgran, h->cgp_trace);
+        hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->S,
+                           h->cgp_src, h->Li, h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
+                           h->cgp_tag, h->cgp_sync,
+                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace);
     };
     if (h->cgp_det) {
         if (h->cgp_nb == 64) go(k_tl_cgp<64, true>);
@@ -2325,7 +2351,7 @@ int cgp_complete(insfm_ba* h, int* st) {
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
     {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
         if (st[0] == 1 || st[0] == 2) {
-            h->cgp_epochs += (unsigned)st[1] + 1u;  // (the setup's barrier and one per completed iteration)
+            h->cgp_epochs += (unsigned)st[1] + 2u;  // (the setup's two barriers and one per completed iteration)
         } else {
             HIPCHK(hipStreamSynchronize(h->stream));
             HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
@@ -2423,8 +2449,13 @@ int run_tl_cg(insfm_ba* h, int* st) {
     if (int rc = enqueue(0, enq)) return rc;
     if (h->cgp_nb) h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
     if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup)
-        HIPCHK(hipEventRecord(h->ev_E, h->stream));
-        if (int rc = issue_side_chain(h, h->cgp_slot, true)) return rc;
+        // (INSFM_DIAG=chain_hold, timing only: no lagged chain at all -- later solves keep an older coarse inverse --
+        // to measure what the chain's overlap costs the kernels it runs beside)
+        static const bool hold = diag("chain_hold");
+        if (!hold) {
+            HIPCHK(hipEventRecord(h->ev_E, h->stream));
+            if (int rc = issue_side_chain(h, h->cgp_slot, true)) return rc;
+        }
         h->cgp_defer = false;
     }
     if (h->cgp_nb && h->cg_async) {
@@ -2578,6 +2609,20 @@ int cg_tail(insfm_ba* h, int* st) {
 
 int solve_tail(insfm_ba* h, double f, const double* cams, const double* pts_local, const double* dcp);
 
+// The scaled copy Sn of the current solve's S~ (k_cg_scale), for consumers that read it when the solve skipped it
+// (k_tl_cgp's lagged solves): the launch-path CG after an abort, the debug timing of launch-path kernels.
+int ensure_sn(insfm_ba* h) {
+    if (h->sn_valid || h->kind != 0 || !h->d.optimize_poses) return 0;
+    const int rc = with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
+            h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
+        return launch_err(h, "k_cg_scale");
+    });
+    if (!rc) h->sn_valid = true;
+    return rc;
+}
+
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
     // the point preparation of the linearization covers this solve when it runs at the prepared damping factor
@@ -2624,10 +2669,13 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 const int64_t b0 = h->rptr_host[h->xr[c]], b1 = h->rptr_host[h->xr[c + 1]];
                 HIPCHK(hipEventRecord(h->ev_x, h->stream));
                 HIPCHK(hipStreamWaitEvent(h->xstream, h->ev_x, 0));
+                // set_timing: the exchange's span on its stream, from the first chunk's start to b's end (phase 7)
+                if (h->timing && c == 0) HIPCHK(hipEventRecord(h->ev[16], h->xstream));
                 if (b1 > b0 && (rc = allreduce_async(h, h->S + b0 * D * D, (b1 - b0) * D * D))) return rc;
             }
             if ((rc = allreduce_async(h, h->b, (int64_t)h->C * D))) return rc;
             HIPCHK(hipEventRecord(h->ev_xdone, h->xstream));
+            if (h->timing) HIPCHK(hipEventRecord(h->ev[17], h->xstream));
             HIPCHK(hipStreamWaitEvent(h->stream, h->ev_xdone, 0));
             rec(h, 7);
         } else {
@@ -2644,15 +2692,21 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         }
         if ((rc = lin_join(h))) return rc;
         const bool ul = h->u_late && !gpk;
+        // k_tl_cgp holds S unscaled and scales the vectors (ba_cgp.h): a lagged solve on it (whose E build behind
+        // the CG takes the coarse segments k_tl_cgp writes) needs no scaled copy Sn; the first solve after a
+        // linearization that factorizes its own E (k_tl_erow reads Sn), the launch-path CG and the debug getters do
+        const bool scale = !(h->tlon && h->cgp_nb && h->tl_solves > 0 && h->tl_fresh && !h->keep_S);
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
                 h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
                 h->d.clamp_min, h->d.clamp_max);
-            k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(h->nnzb, h->blk_row, h->col, h->row_ptr,
-                                                                            h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
+            if (scale)
+                k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
+                    h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
             return launch_err(h, "k_cg_factor/scale");
         });
+        h->sn_valid = scale;
         if (rc) return rc;
         hmark(h, "factor/scale");
         if (h->tlon && (rc = run_tl_setup(h, cams))) return rc;
@@ -2663,7 +2717,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (h->cgp_lost) {  // k_tl_cgp aborted (it left r0 alone): the CG again from the basis, launch path
             h->cgp_lost = false;
             HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
-            if ((rc = run_tl_basis(h, cams, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
+            if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, cams, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
         }
         const int ci = cg_tail(h, st);
         if (ci < 0) return ci;
@@ -2712,6 +2766,29 @@ void cgp_drop_pending(insfm_ba* h) {
     h->cgp_epochs = 0;
 }
 
+// Multi-rank: every rank leaves k_tl_cgp after an abort on any rank (own status `st0`).  A rank whose k_tl_cgp
+// converged left its final CG vectors in place of r0, so r0 = L^-1 b is formed again from the completed S / b
+// (k_cg_factor without U / g_c: the same L, L^-1 and r0) before the basis / restriction and the launch-path CG.
+int cgp_collective_fallback(insfm_ba* h, int st0) {
+    std::fprintf(stderr, "[insfm] rank %d: a k_tl_cgp grid barrier timed out on %s rank; every rank continues on the "
+                         "launch-per-iteration CG\n", h->d.rank, st0 == 4 ? "this" : "another");
+    h->cgp_nb = 0;
+    h->cgp_lost = false;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
+    h->cgp_epochs = 0;
+    HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+    const int rc = with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg,
+                                                                       nullptr, nullptr, 1.0, 0.0, 0.0);
+        return launch_err(h, "k_cg_factor");
+    });
+    if (rc) return rc;
+    if (int r2 = ensure_sn(h)) return r2;
+    return run_tl_basis(h, h->cams_cur, h->stream);
+}
+
 // lm_step's accept rule for the trial being costed (k_publish copies an accepted trial into the caller's buffers)
 struct TrialAccept {
     double last;     // the loss before the step
@@ -2724,7 +2801,7 @@ struct TrialAccept {
 int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     h->trial_copied = false;
     if (!h->pub_host) {
-        HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 5, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(hipMemcpyAsync(h->host_res, h->result, sizeof(double) * 6, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(hipStreamSynchronize(h->stream));
         return 0;
     }
@@ -2767,6 +2844,7 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     hmark(h, "published");
     const volatile double* pv = h->pub_host;
     for (int k = 0; k < 5; ++k) h->host_res[k] = pv[k];
+    h->host_res[5] = pv[6];  // k_tl_cgp aborts (summed over the ranks)
     h->trial_copied = copy;
     return 0;
 }
@@ -2779,11 +2857,11 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
             k_gp_cost<<<h->n_cost, kThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->trans, h->fcam, cams, pts_local, scl,
                                                              h->d.huber_delta, h->part_cost);
         k_final<<<1, kFinalThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
-                                               h->n_gp, nullptr, 0, h->flags, h->result);
+                                               h->n_gp, nullptr, 0, h->flags, h->result, nullptr);
         int rc = launch_err(h, "k_gp_cost/k_final");
         if (rc) return rc;
         h->flags_dirty = false;
-        rc = allreduce(h, h->result, 5);
+        rc = allreduce(h, h->result, 6);
         if (rc) return rc;
         return finish_cost(h, nullptr);
     }
@@ -2793,12 +2871,13 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
             k_cost<M><<<h->n_cost, kCostThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
                                                              h->d.huber_delta, h->part_cost);
         k_final<<<1, kFinalThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
-                                               h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result);
+                                               h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result,
+                                               h->cgp_pending ? h->cg.status : nullptr);
         return launch_err(h, "k_cost/k_final");
     });
     if (rc) return rc;
     h->flags_dirty = false;
-    rc = allreduce(h, h->result, 5);
+    rc = allreduce(h, h->result, 6);
     if (rc) return rc;
     return finish_cost(h, ta);
 }
@@ -2843,13 +2922,28 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
             if ((rc = cgp_complete(h, cst))) return rc;
             if (h->timing) acc_time(h, 8, 9, 5);
             if (h->host_res[4] != 0.0) { failed = 1; h->loss = last; break; }  // a damped point block was not SPD
-            if (cst[0] == 4 && h->cgp_lost) {
+            const bool multi = h->d.world_size > 1 || h->d.allreduce;
+            if (multi && h->host_res[5] != 0.0) {
+                // a replicated multi-rank CG: some rank's k_tl_cgp timed out at a grid barrier (the all-reduced flag,
+                // the same on every rank, and k_publish accepted nowhere).  Every rank leaves the persistent CG for
+                // good and repeats this trial's solve on the launch path from r0 -- the same fixed-order arithmetic
+                // everywhere, so the ranks' dc stay bitwise equal -- then its back-substitution and cost.
+                if ((rc = cgp_collective_fallback(h, cst[0]))) return rc;
+                int* st = reinterpret_cast<int*>(h->host_res + 8);
+                if ((rc = run_tl_cg(h, st))) return rc;
+                it = cg_tail(h, st);
+                if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
+                if (it < 0) return it;
+                if ((rc = solve_tail(h, f, h->cams_cur, h->pts_cur, h->dc))) return rc;
+                if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new, &ta))) return rc;
+            } else if (cst[0] == 4 && h->cgp_lost) {
                 // single rank: a grid barrier timed out (cgp_complete switched the handle to the launch path); this
                 // trial's CG again from the basis, then its back-substitution and cost (k_publish rejected the first)
                 h->cgp_lost = false;
                 HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
                 int* st = reinterpret_cast<int*>(h->host_res + 8);
-                if ((rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
+                if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = run_tl_cg(h, st)))
+                    return rc;
                 it = cg_tail(h, st);
                 if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
                 if (it < 0) return it;
@@ -2873,6 +2967,7 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
             if (h->d.optimize_poses) {
                 acc_time(h, 6, 7, 1);
                 acc_time(h, 1, 3, 2);
+                if (h->xstream) acc_time(h, 16, 17, 7);
             }
             acc_time(h, 3, 4, 3);
             acc_time(h, 4, 5, 4);
@@ -2919,6 +3014,7 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         h->loss = loss_new;
         break;
     }
+    if (h->timing) harvest_chain_time(h);
     if (st) {
         st->loss = h->loss;
         st->loss_before = last;
@@ -3853,6 +3949,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                     if ((rc = hand((void**)&h->cgp_runs, sizeof(double) * 2 * 12 * (size_t)grid * kCgpRows)))
                         return fail(rc, "");
                 }
+                // k_tl_cgp holds S unscaled: the S block (and orientation) of every slot, and the unscaled basis
+                {
+                    std::vector<int> src((size_t)std::max<int64_t>(h->n_nbr, 1), kCgpPadSlot);
+                    for (int e = 0; e < h->nnzb; ++e) {
+                        if (e == rptr[brow[e]]) continue;  // diagonal block: no slot
+                        src[pup[e]] = e;
+                        src[plo[e]] = ~e;
+                    }
+                    if ((rc = upload(h, &h->cgp_src, src.data(), src.size()))) return fail(rc, "");
+                    if ((rc = dd(&tl.Gb, cd * MC))) return fail(rc, "");
+                }
                 h->cgp_det = det;
                 h->cgp_nb = nb;
                 h->cgp_grid = grid;
@@ -3908,6 +4015,23 @@ int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks) {
                          "launch path\n", ranks, (long long)ranks * h->cgp_grid, h->cgp_slots);
         h->cgp_nb = 0;
     }
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_cg_info(const insfm_ba* h, int32_t* out) {
+    if (!h || !out) return INSFM_BA_EINVAL;
+    out[0] = h->xpart ? 3 : h->cgp_nb ? (h->cgp_det ? 2 : 1) : 0;
+    out[1] = h->cgp_grid;
+    out[2] = h->cgp_slots;
+    out[3] = h->cgp_nb;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_set_persistent_cg(insfm_ba* h, int32_t on) {
+    if (!h) return INSFM_BA_EINVAL;
+    if (on) return h->cgp_nb ? INSFM_BA_OK : INSFM_BA_EINVAL;  // (cannot turn on what create found ineligible)
+    cgp_drop_pending(h);
+    h->cgp_nb = 0;
     return INSFM_BA_OK;
 }
 
@@ -4023,6 +4147,7 @@ int insfm_ba_reset(insfm_ba* h) {
     h->tl_solves = 0;
     h->tl_fresh = false;
     h->last_cg_iters = 16;
+    h->chain_timed[0] = h->chain_timed[1] = false;
     return INSFM_BA_OK;
 }
 
@@ -4139,6 +4264,8 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     if (which < 0 || which > 7) return INSFM_BA_EINVAL;
     if (int rc0 = side_flush(h)) return rc0;  // its pending E build / factorization must not interleave
     if (int rc0 = lin_join(h)) return rc0;
+    if (which != 1 && which != 5 && which != 6)
+        if (int rc0 = ensure_sn(h)) return rc0;  // (kernels that read the scaled copy Sn)
     if (which == 2 && h->tl.Racc) {
         // atomic cluster sums: iteration 1's k_tl_pc reads buffer 1 every repetition (its k_tl_pspmv adds into buffer
         // 0, which the next repetition clears), so fill buffer 1 once from a k_tl_pspmv of iteration 0
@@ -4197,6 +4324,57 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, h->ev[10], h->ev[11]));
     *us_per_launch = 1e3 * ms / reps;
+    return INSFM_BA_OK;
+}
+
+int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out) {
+    // the persistent CG of the last solve again, `reps` times: k_cg_factor on the completed S / b (no U / g_c added:
+    // the same L, L^-1 and r0 = L^-1 b), k_tl_basis (Z~ and the restriction of r0), then the timed part -- k_tl_pc's
+    // k_tl_cgp launch, bracketed by events -- with the coarse segments written as in a lagged solve.  out[0] us per
+    // k_tl_cgp launch, out[1] 0 (the setup launch k_tl_pc that preceded it until round 4 is folded in), out[2]
+    // iterations (mean).
+    if (!h || reps <= 0 || !out || !h->cgp_nb || h->kind != 0 || !h->prog_host) return INSFM_BA_EINVAL;
+    cgp_drop_pending(h);
+    if (int rc0 = side_flush(h)) return rc0;
+    if (int rc0 = lin_join(h)) return rc0;
+    const int maxit = h->d.pcg_max_iter;
+    const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
+    double t_cg = 0.0, t_pc = 0.0, iters = 0.0;
+    for (int r = 0; r < reps; ++r) {
+        HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+        const int rc = with_D(h->D, [&](auto dc_) -> int {
+            constexpr int DV = decltype(dc_)::value;
+            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li,
+                                                                           h->cg, nullptr, nullptr, 1.0, 0.0, 0.0);
+            return launch_err(h, "k_cg_factor");
+        });
+        if (rc) return rc;
+        if (int rc2 = run_tl_basis(h, h->cams_new, h->stream)) return rc2;  // (the last trial's cameras)
+        volatile int* pg = h->prog_host;
+        pg[0] = pg[1] = pg[2] = pg[3] = 0;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
+        h->cgp_defer = true;  // (oseg: the segments are written, as in the lagged solves that are most of a run)
+        HIPCHK(hipEventRecord(h->ev[10], h->stream));
+        if (int rc2 = launch_tl_cgp(h, maxit, tol2)) { h->cgp_defer = false; return rc2; }
+        h->cgp_defer = false;
+        h->cgp_tag += (unsigned)maxit + 2u;
+        HIPCHK(hipEventRecord(h->ev[11], h->stream));
+        HIPCHK(hipEventSynchronize(h->ev[11]));
+        int st[3];
+        if (int rc2 = cgp_complete(h, st)) return rc2;
+        if (st[0] != 1) {
+            h->err = "debug_time_cgp: the CG ended with status " + std::to_string(st[0]);
+            return st[0] == 2 ? INSFM_BA_ESOLVER : INSFM_BA_EHIP;
+        }
+        float ms = 0.f;
+        HIPCHK(hipEventElapsedTime(&ms, h->ev[10], h->ev[11]));
+        t_cg += ms;
+        iters += st[1];
+    }
+    // (round 5: the coarse solve of r0 runs inside k_tl_cgp; no setup launch in front of it)
+    out[1] = t_pc;
+    out[0] = 1e3 * t_cg / reps;
+    out[2] = iters / reps;
     return INSFM_BA_OK;
 }
 

@@ -35,6 +35,7 @@ struct TlBufs {
     double* u;           // [C*D]  preconditioned residual
     double* Zt;          // [C][D][MC]
     double* Ztc;         // [C][D][MC] the same rows in cluster-member order (cpos)
+    double* Gb;          // [C][D][MC] the unscaled basis G_i (Z~_i = L_i^T G_i; k_tl_cgp's A_ic); nullptr: not kept
     double* vc;          // [C][D] the vector k_tl_pc reads (r0 at setup, w after), rows in cluster-member order
     double* Rc;          // [m]   (debug) restriction
     double* gd;          // [3][C] row partials r_i.u_i | w_i.u_i | ||L_i r_i||^2 (k_tl_pspmv), rows in cluster-member order
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
 #pragma unroll
         for (int l = a; l < D; ++l) s += L[l * D + a] * col[l];
         tl.Zt[((size_t)i * D + a) * MC + k] = s;
+        if (tl.Gb) tl.Gb[((size_t)i * D + a) * MC + k] = col[a];
         tl.Ztc[((size_t)tl.cpos[i] * D + a) * MC + k] = s;
         rr += s * r[a];
     }

@@ -6,6 +6,7 @@ All arithmetic runs in the HIP library (libinsfm_ba.so) through the C ABI of inc
 only hold device memory and provide the stream / torch.distributed plumbing.  There is no CPU path.
 """
 import ctypes
+import time
 
 import numpy as np
 import torch
@@ -18,17 +19,53 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
                    pcg_max_iter=500, precond=1, cluster_size=14, exchange_chunks=4)
 
 
-def ranks_per_device(device, group=None):
-    """The most ranks of ``group`` that run on one GPU (host name + PCI address of each rank's device, all-gathered):
-    insfm_ba_set_ranks_per_device keeps the persistent CG only when that many of its grids fit on a GPU at once."""
-    import socket
+CG_PATHS = {0: "launch-per-iteration two-level CG", 1: "k_tl_cgp (persistent, atomic cluster sums)",
+            2: "k_tl_cgp (persistent, fixed-order)", 3: "row-partitioned CG"}
 
-    import torch.distributed as dist
+
+def device_key(device):
+    """(host name, PCI domain / bus / device) of ``device``: ranks with equal keys share one GPU."""
+    import socket
     p = torch.cuda.get_device_properties(device)
-    me = (socket.gethostname(), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+    return (socket.gethostname(), int(p.pci_domain_id), int(p.pci_bus_id), int(p.pci_device_id))
+
+
+def ranks_per_device(device, group=None):
+    """The most ranks of ``group`` that run on one GPU (host name + PCI address of each rank's device, all-gathered)."""
+    import torch.distributed as dist
     ids = [None] * dist.get_world_size(group)
-    dist.all_gather_object(ids, me, group=group)
+    dist.all_gather_object(ids, device_key(device), group=group)
     return max(ids.count(x) for x in ids)
+
+
+def cg_path_decision(allv):
+    """The pure part of agree_cg_path on the all-gathered (device key, path, grid, slots) of every rank: (ranks on the
+    most shared GPU, keep k_tl_cgp).  The same list on every rank gives the same answer on every rank."""
+    keys = [a[0] for a in allv]
+    rpd = max(keys.count(k) for k in keys)
+    keep = all(a[1] == 2 for a in allv) and all(keys.count(a[0]) * a[2] <= a[3] for a in allv)
+    return rpd, keep
+
+
+def agree_cg_path(handle, device, group=None):
+    """Collective: the CG every rank of a replicated multi-rank handle runs.  The ranks must all take the same path
+    (the persistent k_tl_cgp and the launch path sum S~ m in different orders, so mixed paths would give dc that differ
+    in rounding and replicated cameras that drift apart silently).  Every rank all-gathers its device key and
+    insfm_ba_cg_info (its own eligibility: grid, slots, INSFM_DIAG, the host-mapped progress word ...); k_tl_cgp stays
+    only if every rank runs its fixed-order form and every GPU holds the grids of all ranks placed on it at once.
+    Returns (ranks on the most shared GPU, the agreed path code)."""
+    import torch.distributed as dist
+    L = _capi.load()
+    info = (ctypes.c_int32 * 4)()
+    _capi.check(handle, L.insfm_ba_cg_info(handle, info))
+    me = (device_key(device), int(info[0]), int(info[1]), int(info[2]))
+    allv = [None] * dist.get_world_size(group)
+    dist.all_gather_object(allv, me, group=group)
+    rpd, keep = cg_path_decision(allv)
+    if not keep and int(info[0]) in (1, 2):
+        _capi.check(handle, L.insfm_ba_set_persistent_cg(handle, 0))
+    _capi.check(handle, L.insfm_ba_cg_info(handle, info))
+    return rpd, int(info[0])
 
 
 def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
@@ -41,6 +78,7 @@ def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
     import torch.distributed as dist
 
     def _allreduce(ctx, ptr, count):
+        t0 = time.perf_counter()
         try:
             if counter is not None:
                 counter[0] += 1
@@ -61,6 +99,9 @@ def make_allreduce_callback(get_buffer, group=None, errors=None, counter=None):
             if errors is not None:
                 errors.append(e)
             return -1
+        finally:
+            if counter is not None and len(counter) > 1:
+                counter[1] += time.perf_counter() - t0  # host seconds inside the callback (gloo: the whole reduce)
     return _allreduce
 
 
@@ -158,7 +199,7 @@ class BundleAdjuster:
         self._xbuf = None
         self._cb = None
         self._errors = []
-        self.exchange_calls = [0]
+        self.exchange_calls = [0, 0.0]  # exchange callbacks made, host seconds spent in the synchronous one
         exchange = world_size > 1 or force_exchange
         if exchange:
             self._cb = _capi.ALLREDUCE_FN(make_allreduce_callback(lambda: self._xbuf, process_group, self._errors,
@@ -189,9 +230,9 @@ class BundleAdjuster:
             n = L.insfm_ba_exchange_count(h)
             self._xbuf = torch.zeros(int(n), dtype=torch.float64, device=self.device)
             _capi.check(h, L.insfm_ba_set_exchange(h, ctypes.c_void_p(self._xbuf.data_ptr()), n))
+        self.cg_path = self.cg_info()[0]
         if world_size > 1:
-            self.ranks_per_device = ranks_per_device(self.device, process_group)
-            _capi.check(h, L.insfm_ba_set_ranks_per_device(h, self.ranks_per_device))
+            self.ranks_per_device, self.cg_path = agree_cg_path(h, self.device, process_group)
 
     # ------------------------------------------------------------------------------------------------------------
     def close(self):
@@ -288,6 +329,24 @@ class BundleAdjuster:
         us = ctypes.c_double()
         _capi.check(self._h, _capi.load().insfm_ba_debug_time_kernel(self._h, int(which), int(reps), ctypes.byref(us)))
         return us.value
+
+    def cg_info(self):
+        """(path code, k_tl_cgp grid, workgroup slots, register blocks per row) -- insfm_ba_cg_info; CG_PATHS names
+        the codes."""
+        info = (ctypes.c_int32 * 4)()
+        _capi.check(self._h, _capi.load().insfm_ba_cg_info(self._h, info))
+        return tuple(int(x) for x in info)
+
+    def debug_time_cgp(self, reps=10):
+        """The persistent CG (k_tl_cgp) of the last solve re-run `reps` times: (us per k_tl_cgp launch, us per k_tl_pc
+        setup launch, PCG iterations per solve); None when this handle does not run k_tl_cgp
+        (insfm_ba_debug_time_cgp)."""
+        out = (ctypes.c_double * 3)()
+        rc = _capi.load().insfm_ba_debug_time_cgp(self._h, int(reps), out)
+        if rc == _capi.INSFM_BA_EINVAL:
+            return None
+        _capi.check(self._h, rc)
+        return float(out[0]), float(out[1]), float(out[2])
 
     def nnzb(self):
         return int(_capi.load().insfm_ba_nnzb(self._h))

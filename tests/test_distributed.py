@@ -113,3 +113,58 @@ def test_ranks_per_device(buses, expect):
     engine passes to insfm_ba_set_ranks_per_device (the persistent CG stays on only if that many grids fit on a GPU;
     every rank gets the same count, so every rank takes the same CG path)."""
     _run(_rpd_worker, len(buses), buses, expect)
+
+
+@pytest.mark.parametrize("infos,expect", [
+    # (bus, path, grid, slots) per rank -> (ranks per device, keep k_tl_cgp)
+    ([(1, 2, 250, 256), (2, 2, 250, 256)], (1, True)),       # one rank per GPU, fixed-order everywhere
+    ([(1, 2, 50, 256), (1, 2, 50, 256)], (2, True)),         # two config-2 grids fit one GPU
+    ([(1, 2, 250, 256), (1, 2, 250, 256)], (2, False)),      # two config-3 grids do not
+    ([(1, 2, 250, 256), (2, 0, 250, 256)], (1, False)),      # one rank ineligible (e.g. INSFM_DIAG=no_cgp there)
+    ([(1, 2, 250, 256), (2, 2, 250, 240)], (1, False)),      # one GPU with fewer CUs (a partition mode)
+    ([(1, 1, 250, 256), (2, 2, 250, 256)], (1, False)),      # a rank on the atomic (non-deterministic) form
+])
+def test_cg_path_decision(infos, expect):
+    """engine.cg_path_decision: the replicated multi-rank CG keeps k_tl_cgp only when every rank runs its
+    fixed-order form and every GPU holds all the grids placed on it; otherwise every rank takes the launch path."""
+    from instantsfm_amd import engine
+    allv = [(("h", 0, bus, 0), path, grid, slots) for bus, path, grid, slots in infos]
+    assert engine.cg_path_decision(allv) == expect
+
+
+class _FakeLib:
+    def __init__(self, info):
+        self.info, self.off = list(info), False
+
+    def insfm_ba_cg_info(self, h, out):
+        for k, v in enumerate(self.info):
+            out[k] = v
+        return 0
+
+    def insfm_ba_set_persistent_cg(self, h, on):
+        if not on:
+            self.off = True
+            self.info[0] = 0
+        return 0
+
+
+def _agree_worker(rank, world, port, infos, expect_path):
+    _init(rank, world, port)
+    from instantsfm_amd import _capi, engine
+    bus, path, grid, slots = infos[rank]
+    fake = _FakeLib([path, grid, slots, 64])
+    _capi.load = lambda: fake
+    _capi.check = lambda h, rc: rc
+    torch.cuda.get_device_properties = lambda device: _Props(bus)
+    rpd, got = engine.agree_cg_path(None, None)
+    assert got == expect_path, (rank, got, expect_path)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("infos,expect_path", [
+    ([(1, 2, 50, 256), (1, 2, 50, 256), (2, 2, 50, 256), (2, 2, 50, 256)], 2),
+    ([(1, 2, 50, 256), (1, 2, 50, 256), (2, 0, 50, 256), (2, 2, 50, 256)], 0),   # rank 2 ineligible: all launch path
+])
+def test_agree_cg_path_world4(infos, expect_path):
+    """agree_cg_path over 4 gloo ranks: one rank that cannot run k_tl_cgp turns it off on every rank."""
+    _run(_agree_worker, len(infos), infos, expect_path)

@@ -46,9 +46,10 @@ def test_cgp_matches_launch_path():
 
 
 def test_cgp_deterministic_variant():
-    """deterministic=True runs the fixed-order k_tl_cgp (cluster owners sum the workgroups' partials in a fixed order
-    and publish them as tagged granules; no atomics): two runs of each scene are bitwise equal, one launch per solve,
-    and the launch path's deterministic CG agrees to rounding (losses 1e-8, PCG iterations within one per step)."""
+    """deterministic=True runs the fixed-order k_tl_cgp (no atomics: every workgroup run stores its partials in a
+    parity buffer before the grid barrier, and after it every workgroup sums each cluster's runs itself in run order):
+    two runs of each scene are bitwise equal, one launch per solve, and the launch path's deterministic CG agrees to
+    rounding (losses 1e-8, PCG iterations within one per step)."""
     a = run("", "--det", "--repeat", "2", scenes="small,config2")
     b = run("no_cgp", "--det", scenes="small,config2")
     for name in ("small", "config2"):

@@ -290,13 +290,16 @@ def test_repeated_solves_lagged_coarse_inverse(model, det):
 
     The bound of each solve is derived in the test, not fitted: the oracle is re-run with the Schur row sums taken in
     other orders (order_seed 1..3: each camera row's observations in a seeded permutation; order_mode 2: the PCG's dot
-    products in reverse order) -- the same arithmetic, only the summation order moved, which is what the GPU's
-    LDS-atomic row accumulation (and, in deterministic mode, its own fixed order) does.  The GPU must stay within 10x
-    the largest spread of those re-runs from the oracle, or within the fixed tolerances below where that spread is
-    smaller (resid 1e-9, energy 1e-6, max-abs 1e-8 for own-E solves and 1e-6 for lagged ones).  For FULL_OPENCV
-    (D = 16) at k = 0 the distortion columns k1..k3 and k4..k6 are exactly dependent, held apart only by the damping
-    (cond(S) ~ 5e13): there the order re-runs alone move a lagged solve by ~3e-9 in residual space and ~7e-5 in
-    max-abs, which is the bound's scale."""
+    products in reverse order).  That is a yardstick of the rounding scale of these solves, not a model of the GPU's
+    arithmetic: the oracle builds S = U - W V^-1 W^T from W records, while the GPU sums symmetric records
+    Y_o = W_o R_p^-T (R_p the Cholesky factor of the first trial's damped point block) and, on retried trials, applies
+    M_p = R_p^T V'^-1 R_p -- the same S in exact arithmetic, with other roundings and another summation order.  The GPU
+    must stay within 10x the largest spread of those re-runs from the oracle, or within the fixed tolerances below
+    where that spread is smaller (resid 1e-9, energy 1e-6, max-abs 1e-8 for own-E solves and 1e-6 for lagged ones),
+    and always under the explicit caps resid 1e-7, energy 1e-4, max-abs 1e-3 (the derived bound alone can
+    reach ~7e-4 in max-abs for D = 16).  For FULL_OPENCV (D = 16) at k = 0 the distortion columns k1..k3 and k4..k6
+    are exactly dependent, held apart only by the damping (cond(S) ~ 5e13): there the order re-runs alone move a lagged
+    solve by ~3e-9 in residual space and ~7e-5 in max-abs, which is the bound's scale."""
     prob = make_problem(30, 800, seed=5, model=model)
     cams, pts = prob.cams_init.copy(), prob.points_init.copy()
     args = (prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points)
@@ -335,8 +338,10 @@ def test_repeated_solves_lagged_coarse_inverse(model, det):
             bound = {"resid": max(1e-9, 10 * spread[k]["resid"]), "energy": max(1e-6, 10 * spread[k]["energy"]),
                      "max": max(1e-6 if lagged else 1e-8, 10 * spread[k]["max"])}
             print(f"model {model} det {det} rep {rep} solve {k}: {d}; order spread {spread[k]}")
+            cap = {"resid": 1e-7, "energy": 1e-4, "max": 1e-3}
             for q in ("resid", "energy", "max"):
                 assert d[q] < bound[q], (rep, k, q, d, spread[k])
+                assert d[q] < cap[q], (rep, k, q, d)
         eng.close()
 
 

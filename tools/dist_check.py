@@ -87,8 +87,12 @@ def main():
                     help="row-partitioned CG (each rank applies S~ to its own rows, partials exchanged over IPC windows)")
     ap.add_argument("--exchange-chunks", type=int, default=4,
                     help="row chunks of the [S | b] exchange behind the Schur build (1: one all-reduce after it)")
+    ap.add_argument("--diag-rank", type=int, default=-1, help="set INSFM_DIAG=--diag on this rank only")
+    ap.add_argument("--diag", default="")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if rank == args.diag_rank:  # (read by the library once, at its first diagnostic query)
+        os.environ["INSFM_DIAG"] = args.diag
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", 0 if args.same_device else local)
     torch.cuda.set_device(dev)
@@ -106,6 +110,7 @@ def main():
                          world_size=world, rank=rank, shard=shards[rank], deterministic=True,
                          force_exchange=args.force_exchange, exchange_chunks=args.exchange_chunks)
     rows = eng.partition_cg() if args.cg_partition else None
+    path0 = eng.cg_info()[0]  # the CG every rank agreed on at create (engine.agree_cg_path)
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
     pts = torch.from_numpy(prob.points_init.copy()).to(dev)
     losses, iters, launches, trials = [], [], [], []
@@ -136,7 +141,10 @@ def main():
         cams_all = [torch.zeros_like(cams) for _ in range(world)]
         dist.all_gather(cams_all, cams)
         cams_all = [c.cpu() for c in cams_all]
+    paths = [None] * world  # (agreed at create, after the steps) per rank
+    dist.all_gather_object(paths, (path0, eng.cg_info()[0]))
     if rank == 0:
+        os.environ.pop("INSFM_DIAG", None)
         ref = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
                              device=dev, deterministic=True)
         rc = torch.from_numpy(prob.cams_init.copy()).to(dev)
@@ -150,7 +158,7 @@ def main():
                    rmse=rmse, ref_rmse=ref_rmse, exchange_calls=eng.exchange_calls[0], n_obs=int(prob.n_obs),
                    cg_partition=bool(args.cg_partition), rows=rows, pcg_iters=iters, xchg_us=xchg_us,
                    ranks_per_device=getattr(eng, "ranks_per_device", 1), cg_launches=launches, trials=trials,
-                   losses_hex=[float(x).hex() for x in losses],
+                   losses_hex=[float(x).hex() for x in losses], cg_paths=paths,
                    params_sha=hashlib.sha256(cams.cpu().numpy().tobytes() + full.numpy().tobytes()).hexdigest(),
                    cams_equal_across_ranks=all(bool(torch.equal(c, cams_all[0])) for c in cams_all) if cams_all else None)
         print(json.dumps(out), flush=True)
