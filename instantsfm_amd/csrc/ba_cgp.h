@@ -198,20 +198,24 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
                                                           double* wx, unsigned long long* yg, unsigned tag0,
                                                           unsigned* sync, unsigned epoch0, int oseg, double* runs,
-                                                          double* trace) {
+                                                          double* trace, long long* stp) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
+    const StampScope stamp_(stp);
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
     constexpr int NG = NB / 8;                          // gather loads per wave and iteration
     constexpr int RPT = (kCoarseMax + kCgpThreads - 1) / kCgpThreads;  // coarse entries per thread (LDS fills)
-    __shared__ double Aseg[kCgpRows][kCgpSegMax][BS];  // A_ic of the row's segments, a-major
+    // B_ic = sum_{j in c} S_ij G_j of the row's segments, a-major (A_ic = S~_i,c Z~_c = L_i^-1 B_ic)
+    // (segment stride BS + 1: P2's lanes (a, j) read row a of segments j, j + 8, ... -- an odd stride keeps the 8
+    // segments of a row on distinct banks)
+    __shared__ double Aseg[kCgpRows][kCgpSegMax][BS + 1];
     __shared__ double wg[kCgpWaves][NB][D];            // the neighbours' w of the wave's blocks (gathered per iteration)
     // the restriction R of the iteration; DET: the 12 cluster sums (gamma, delta, rho partials, R) of every cluster
     __shared__ double rs[DET ? 12 * kCgpMaxClusters : kCoarseMax];
     __shared__ double ys[kCoarseMax];                  // y of the iteration
     __shared__ double Lrow[kCgpRows][D * D];           // L_i (row a, column k)
     __shared__ double Lirow[kCgpRows][D * D];          // L_i^-1 (row a, column k)
-    __shared__ int sq[kCgpWaves][NB];                  // S block of each register slot (ssrc: upper / ~lower / pad)
     __shared__ double Zrow[kCgpRows][BS];              // Z~_i (row a, column k)
+    __shared__ double Grow[kCgpRows][BS];              // G_i, the unscaled basis (row a, column k)
     __shared__ double vec[kCgpRows][8][D];             // the row's r u w z q s p x
     __shared__ int jn[kCgpWaves][NB];                  // neighbour of each register block
     __shared__ int segc[kCgpRows][kCgpSegMax];         // neighbour cluster of each segment
@@ -237,29 +241,21 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     const long long t_start = wall_clock64();
     double* V = &vec[rl][0][0];
     enum { VR = 0, VU = 8, VW = 16, VZ = 24, VQ = 32, VS = 40, VP = 48, VX = 56 };
-    // L_i^-1 applied to the row sums of an unscaled product: lane (a, b) holds after the butterfly over b the sum of
-    // row a in acc; lane la = lane & 7 gets (L_i^-1 sum)[la] = sum_{k <= la} L_i^-1[la][k] sum_k (k ascending)
-    auto lscale = [&](double acc) {
-        double sm[D], li[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) { sm[k] = __shfl(acc, 8 * k, 64); li[k] = Lirow[rl][(lane & 7) * D + k]; }
-        double v = 0.0;
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (k <= (lane & 7)) v += li[k] * sm[k];
+    // The block-Jacobi scaling on the vector side, lane (a, b) = (a8, b8) holding one entry of the 8 x 8 factor
+    // L_i^-1 (li_ba = L_i^-1[b][a], li_ab = L_i^-1[a][b], set once per solve below):
+    //   lscale: acc = sum of row a of an unscaled product (the value lane (a, *) holds after the butterfly over b) ->
+    //           (L_i^-1 sum)[b] = sum_{a <= b} L_i^-1[b][a] sum_a, by a butterfly over a (lane stride 8, 16, 32);
+    //   ltscale: x = the row's vector entry of lane a8 -> (L_i^-T x)[b] = sum_{a >= b} L_i^-1[a][b] x_a, the same way.
+    // Either way every lane ends with the entry of index b8 = lane & 7 (the lanes < 8 store it).
+    double li_ba = 0.0, li_ab = 0.0;
+    auto bfly8 = [&](double v) {
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
         return v;
     };
-    // v = L_i^-T x for the row's vector x (its 8 entries x8, in every lane): lane la gets sum_{k >= la} L_i^-1[k][la] x_k
-    auto ltscale = [&](const double (&x8)[D]) {
-        double li[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) li[k] = Lirow[rl][k * D + (lane & 7)];
-        double v = 0.0;
-#pragma unroll
-        for (int k = 0; k < D; ++k)
-            if (k >= (lane & 7)) v += li[k] * x8[k];
-        return v;
-    };
+    auto lscale = [&](double acc) { return bfly8(a8 <= b8 ? li_ba * acc : 0.0); };
+    auto ltscale = [&](double xa) { return bfly8(a8 >= b8 ? li_ab * xa : 0.0); };
     // ---- setup ----
     // The operator is held UNSCALED (round 5): slot k of the row keeps S_ij (j = its neighbour) from the upper block
     // pattern of S -- block ssrc >= 0 as stored, or block ~ssrc transposed for a lower neighbour -- and the block-Jacobi
@@ -267,16 +263,14 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     // forms S~ w = L_i^-1 (sum_j S_ij v_j).  So no k_cg_scale launch and no 61-MB Sn copy in front of the CG (the
     // first solve of an LM run, whose own coarse matrix k_tl_erow builds from Sn, still has them).
     // The row's blocks (slots past the row: zero, neighbour = the row itself, so the products need no guard).
-    for (int k = lane; k < NB; k += 64) {
-        jn[wv][k] = k < nk ? nbr_j[n0 + k] : (has_row ? row : 0);
-        sq[wv][k] = k < nk ? ssrc[n0 + k] : kCgpPadSlot;
-    }
+    for (int k = lane; k < NB; k += 64) jn[wv][k] = k < nk ? nbr_j[n0 + k] : (has_row ? row : 0);
+    // the slots' S blocks, slot k in lane k & 63 of sqa (k < 64) / sqb; read back per slot by readlane (no memory
+    // round trip between a slot's index and its block load)
+    const int sqa = lane < nk ? ssrc[n0 + lane] : kCgpPadSlot;
+    const int sqb = (NB > 64 && lane + 64 < nk) ? ssrc[n0 + 64 + lane] : kCgpPadSlot;
     const int lt = b8 * D + a8;  // this lane's entry of a transposed block
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     auto slot_val = [&](int k) {  // entry (a8, b8) of S_ij for register slot k (branch-free: one load per slot)
-        const int q = sq[wv][k];
+        const int q = __builtin_amdgcn_readlane(k < 64 ? sqa : sqb, k & 63);
         const bool pad = q == kCgpPadSlot;
         const int e = pad ? 0 : (q >= 0 ? q : ~q);
         const double v = S[(size_t)e * (D * D) + (q >= 0 ? lane : lt)];
@@ -285,7 +279,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     double sreg[NB];
 #pragma unroll
     for (int k = 0; k < NB; ++k) sreg[k] = slot_val(k);
-    for (int e = t; e < kCgpRows * kCgpSegMax * BS; e += kCgpThreads) (&Aseg[0][0][0])[e] = 0.0;
+    for (int e = t; e < kCgpRows * kCgpSegMax * (BS + 1); e += kCgpThreads) (&Aseg[0][0][0])[e] = 0.0;
     const size_t own = (size_t)(has_row ? row : 0) * D + (lane & 7);
     {
         if (lane < nseg && lane < kCgpSegMax) segc[rl][lane] = tl.seg[s0 + lane].x;
@@ -294,7 +288,12 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         if (has_row) {
             Lrow[rl][lane] = Lf[(size_t)row * D * D + lane];
             Lirow[rl][lane] = Li[(size_t)row * D * D + lane];
-            for (int e = lane; e < BS; e += 64) Zrow[rl][e] = tl.Zt[(size_t)row * BS + e];
+            li_ab = Li[(size_t)row * D * D + lane];   // L_i^-1[a8][b8]
+            li_ba = Li[(size_t)row * D * D + lt];     // L_i^-1[b8][a8]
+            for (int e = lane; e < BS; e += 64) {
+                Zrow[rl][e] = tl.Zt[(size_t)row * BS + e];
+                Grow[rl][e] = tl.Gb[(size_t)row * BS + e];
+            }
             const double* src = lane < 8 ? cg.r[0] : lane < 16 ? tl.u : lane < 24 ? cg.w[0] : lane < 32 ? cg.w[1]
                               : lane < 40 ? cg.r[1] : lane < 48 ? cg.s[0] : lane < 56 ? cg.p : cg.x;
             V[lane] = src[own];
@@ -302,12 +301,12 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     }
     __syncthreads();
     if (trace && blockIdx.x == 0 && t == 0) trace[578] = (double)wall_clock64();  // (blocks issued, LDS tables in)
-    // A_ic = S~_i,c Z~_c = L_i^-1 B_ic with B_ic = sum_{j in c} S_ij G_j (Z~_j = L_j^T G_j, G_j the unscaled basis):
+    // B_ic = sum_{j in c} S_ij G_j (A_ic = S~_i,c Z~_c = L_i^-1 B_ic, since Z~_j = L_j^T G_j, G_j the unscaled basis):
     // lane (a, b) sums S_ij[a][b] G_j[b][q] over the segment's blocks (segment boundaries are wave-uniform); at the
     // segment's end the eight b lanes are summed by a fixed butterfly and lane (a, 0) writes row a of B_ic (one wave
-    // per row: each segment is written once, in a fixed order); then every segment is multiplied by L_i^-1 in place.
-    // The G_j rows of ZC blocks at a time are staged in the wave's gather buffer by coalesced loads (all in flight
-    // together), then read back per lane.
+    // per row: each segment is written once, in a fixed order).  L_i^-1 is applied per iteration together with the
+    // row's S~ w (P2), and Z~_i^T A_ic = G_i^T B_ic for the coarse segments.  The G_j rows of ZC blocks at a time are
+    // staged in the wave's gather buffer by coalesced loads (all in flight together), then read back per lane.
     if (nk > 0) {
         constexpr int ZC = NB * D / BS;            // blocks per staging chunk (14 for NB = 128)
         constexpr int ZU = (ZC * BS + 63) / 64;    // coalesced loads per lane and chunk
@@ -378,32 +377,6 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         flush();
-        // A_ic = L_i^-1 B_ic for every segment (lane pair entries (a, q); the wave reads its B entries first)
-        const int ns = min(nseg, kCgpSegMax);
-        for (int sg = 0; sg < ns; ++sg) {
-            double* A = &Aseg[rl][sg][0];
-            double bo[2];
-            int eo[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int e = min(lane + 64 * h, BS - 1), a = e / MC, q = e - a * MC;
-                double v = 0.0;
-#pragma unroll
-                for (int k = 0; k < D; ++k)
-                    if (k <= a) v += Lirow[rl][a * D + k] * A[k * MC + q];
-                bo[h] = v;
-                eo[h] = lane + 64 * h;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                if (eo[h] < BS) A[eo[h]] = bo[h];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
     }
     const int ci = has_row ? tl.clab[row] : 0;
     if (lane == 0) pcl[rl] = has_row ? ci : -1;
@@ -429,7 +402,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                     for (int a = 0; a < D; ++a) v += Zrow[rl][a * MC + k] * Zrow[rl][a * MC + l];
                 }
 #pragma unroll
-                for (int a = 0; a < D; ++a) v += Zrow[rl][a * MC + k] * Aseg[rl][sg][a * MC + l];
+                for (int a = 0; a < D; ++a) v += Grow[rl][a * MC + k] * Aseg[rl][sg][a * MC + l];  // Z~_i^T A = G_i^T B
                 tl.Oseg[(size_t)(s0 + sg) * MC * MC + o] = v;
             }
         }
@@ -450,36 +423,55 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             cg.status[2] = use ? 1 : 0;  // reported as insfm_ba_stats.coarse_used
             if (cg.prog) __hip_atomic_store(cg.prog + 3, use ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        // R(r0) = k_tl_basis's cluster sums (tl.Rc, k_tl_pc's order); wave gw forms coarse row gw of y0 = E^-1 R
+        // (k_tl_pc's products and butterfly) and publishes it as tagged granules like an iteration's y, under the
+        // setup's own tag (tag0 + maxit + 1: never an iteration's); every workgroup polls all of y0
+        const unsigned tag_s = tag0 + (unsigned)maxit + 1u;
         if (use) {
-            for (int e = t; e < m; e += kCgpThreads) {
-                const int c2 = e / MC, k = e - c2 * MC;
-                const int r0 = tl.cl_ptr[c2], r1 = tl.cl_ptr[c2 + 1];
-                double v = 0.0;
-#pragma unroll 8
-                for (int mi = r0; mi < r1; ++mi) v += tl.rowR[(size_t)mi * MC + k];
-                rs[e] = v;
+            double rv[RPT];
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) rv[q] = tl.Rc[min(t + q * kCgpThreads, m - 1)];
+            double ev[LPL];
+            if (gw < m) {
+#pragma unroll
+                for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
             }
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+            __syncthreads();
+            if (gw < m) {
+                double rq[LPL];
+#pragma unroll
+                for (int q = 0; q < LPL; ++q) rq[q] = rs[min(lane + 64 * q, m - 1)];
+                __builtin_amdgcn_sched_barrier(0);
+                double sy = 0.0;
+#pragma unroll
+                for (int q = 0; q < LPL; ++q)
+                    if (lane + 64 * q < m) sy += ev[q] * rq[q];
+                const double y = wave_sum(sy);
+                if (lane == 0) put_y(yg, gw, tag_s, y);
+            }
+            for (int g = gw + gridDim.x * kCgpWaves; g < m; g += gridDim.x * kCgpWaves) {
+                const double* er = Einv + (size_t)g * m;
+                double sy = 0.0;
+                for (int l = lane; l < m; l += 64) sy += er[l] * rs[l];
+                const double y = wave_sum(sy);
+                if (lane == 0) put_y(yg, g, tag_s, y);
+            }
+            if (!get_y(yg, ys, m, tag_s, sync)) alive = false;
         }
-        __syncthreads();
-        if (has_row) {
+        if (alive && has_row) {
             const int la = lane & 7;
             double v = V[VR + la];
             if (use) {
-                double yv[MC];
+                double z9[MC], y9[MC];
 #pragma unroll
-                for (int k = 0; k < MC; ++k) {
-                    const double* er = Einv + (size_t)(ci * MC + k) * m;
-                    double sy = 0.0;
-#pragma unroll
-                    for (int q = 0; q < LPL; ++q) {
-                        const int l = lane + 64 * q;
-                        if (l < m) sy += er[l] * rs[l];
-                    }
-                    yv[k] = wave_sum(sy);
-                }
+                for (int k = 0; k < MC; ++k) { z9[k] = Zrow[rl][la * MC + k]; y9[k] = ys[ci * MC + k]; }
+                __builtin_amdgcn_sched_barrier(0);
                 double sz = 0.0;
 #pragma unroll
-                for (int k = 0; k < MC; ++k) sz += Zrow[rl][la * MC + k] * yv[k];
+                for (int k = 0; k < MC; ++k) sz += z9[k] * y9[k];
                 v += sz;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -489,13 +481,10 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            double u8[D];
-#pragma unroll
-            for (int k = 0; k < D; ++k) u8[k] = V[VU + k];
-            const double v0 = ltscale(u8);  // the neighbours read L_i^-T u0
+            const double v0 = ltscale(V[VU + a8]);  // the neighbours read L_i^-T u0
             if (lane < D) st_sc1(wx + (size_t)C * D + (size_t)row * D + lane, v0);
         }
-        alive = cgp_barrier(sync, ++epoch, &bflag);
+        if (alive) alive = cgp_barrier(sync, ++epoch, &bflag);
     }
     // ---- iteration 0's operator product (k_tl_pspmv's setup, folded in): w0 = u0 + S~ u0, z0 = q0 = 0; w0 into the
     // exchange buffer of parity 0 and the partials of iteration 0 (r0.u0, w0.u0, ||L r0||^2, Z~^T w0) published like
@@ -565,7 +554,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
-                const double v0 = ltscale(w8);  // the neighbours read L_i^-T w0
+                const double v0 = ltscale(V[VW + a8]);  // the neighbours read L_i^-T w0
                 if (lane < D) st_sc1(wx + (size_t)row * D + lane, v0);
             }
             wave_sum3(g0, g1, g2);
@@ -774,7 +763,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             acc += __shfl_xor(acc, 1, 64);
             acc += __shfl_xor(acc, 2, 64);
             acc += __shfl_xor(acc, 4, 64);
-            sw = lscale(acc);  // (S~ w)_i = L_i^-1 sum_j S_ij v_j
+            sw = acc;  // row a8's sum_j S_ij v_j, unscaled (L_i^-1 is applied with the coarse part in P2)
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 0] = (double)wall_clock64();
         // ======== P2 ========
@@ -800,11 +789,12 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                 for (int k = 0; k < MC; ++k) sz += z9[k] * y9[k];
                 mi += sz;
-                // lane (j, a) = (lane >> 3, lane & 7): row a of the segments j, j + 8, ..., then summed over j
+                // lane (a, j) = (a8, b8): row a of B_ic y_c over the segments j, j + 8, ..., then summed over j -- the
+                // layout of sw's row sums, so that L_i^-1 is applied once to both
                 const int ns = min(nseg, kCgpSegMax);
-                for (int sg = lane >> 3; sg < ns; sg += 8) {
+                for (int sg = b8; sg < ns; sg += 8) {
                     const double* yc = ys + segc[rl][sg] * MC;
-                    const double* A = &Aseg[rl][sg][la * MC];
+                    const double* A = &Aseg[rl][sg][a8 * MC];
                     double a9[MC], c9[MC];
 #pragma unroll
                     for (int k = 0; k < MC; ++k) { a9[k] = A[k]; c9[k] = yc[k]; }
@@ -812,14 +802,16 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                     for (int k = 0; k < MC; ++k) ay += a9[k] * c9[k];
                 }
-                ay += __shfl_xor(ay, 8, 64);
-                ay += __shfl_xor(ay, 16, 64);
-                ay += __shfl_xor(ay, 32, 64);
+                ay += __shfl_xor(ay, 1, 64);
+                ay += __shfl_xor(ay, 2, 64);
+                ay += __shfl_xor(ay, 4, 64);
             }
+            // (S~ m)_i - m_i = L_i^-1 (sum_j S_ij v_j + sum_c B_ic y_c), entry la
+            const double soff = lscale(sw + ay);
             const double vz = V[VZ + la], vq = V[VQ + la], vs = V[VS + la], vu = V[VU + la], vp = V[VP + la];
             const double vx = V[VX + la], vr = V[VR + la];
             __builtin_amdgcn_sched_barrier(0);
-            const double prod = mi + (sw + ay);  // (the diagonal block of S~ is I)
+            const double prod = mi + soff;  // (the diagonal block of S~ is I)
             const double zn = prod + be * vz;
             const double qn = mi + be * vq;
             const double sn = w_ + be * vs;
@@ -828,6 +820,10 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             const double rn = vr - alpha * sn;
             const double un = vu - alpha * qn;
             const double wn = w_ - alpha * zn;
+            // the row's new v = L_i^-T w for the neighbours first (w entry a8 from lane a8 by one permute, not
+            // through LDS): its store overlaps the partials below
+            const double vn = ltscale(__shfl(wn, a8, 64));
+            if (lane < D) st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, vn);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -864,9 +860,6 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
-                // the row's new v = L_i^-T w for the neighbours (its write-back overlaps the partials' reductions)
-                const double vn = ltscale(w8);
-                if (lane < D) st_sc1(wx + (size_t)((it + 1) & 1) * C * D + (size_t)row * D + lane, vn);
             }
             wave_sum3(g0, g1, g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }

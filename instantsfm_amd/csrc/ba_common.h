@@ -54,5 +54,19 @@ struct CgGeom {
     static constexpr int BPR = BPW * kCgWaves;                    // blocks per round per workgroup
 };
 
+// INSFM_DIAG=stamps: tracer-free timestamps of selected main-queue kernels (wall_clock64, 100 MHz, one clock for the
+// whole device).  p[0] = the entry of workgroup 0, p[1] = the latest end of any workgroup's thread 0 (no-return
+// atomic max); p null: off (the default, no code path change).
+struct StampScope {
+    unsigned long long* p;
+    __device__ explicit StampScope(long long* q) : p(reinterpret_cast<unsigned long long*>(q)) {
+        if (p && blockIdx.x == 0 && threadIdx.x == 0) p[0] = (unsigned long long)wall_clock64();
+    }
+    __device__ ~StampScope() {
+        if (p && threadIdx.x == 0) atomicMax(p + 1, (unsigned long long)wall_clock64());
+    }
+};
+constexpr int kStampSteps = 1024;  // ring of LM steps
+enum StampKind { kStLinPoints = 0, kStSchur = 1, kStCgp = 2, kStCgFinish = 3, kStPublish = 4, kStKinds = 5 };
 
 }  // namespace insfm

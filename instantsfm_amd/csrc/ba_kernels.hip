@@ -242,7 +242,7 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
                                                          const double* __restrict__ uv, const double* __restrict__ pp,
                                                          const double* __restrict__ cams, const double* __restrict__ pts,
                                                          double delta, double* __restrict__ Y, double* __restrict__ V,
-                                                         double* __restrict__ gp, PointPrep pp1) {
+                                                         double* __restrict__ gp, PointPrep pp1, long long* stp) {
     // One workgroup per run of whole tracks (blk, built at create: at most kLinThreads observations unless a single track
     // is longer), one thread per observation: coalesced uv / cam / point loads.  Each observation's V / g terms go to
     // LDS and one thread per track adds them in observation order -- the same sequence of additions as a thread walking
@@ -253,6 +253,7 @@ __global__ __launch_bounds__(kLinThreads) void k_lin_points(const int* __restric
     // R_p^-1 table and the record staging (6 workgroups per CU).  Y null (points-only solves): no records.
     constexpr int D = kD<M>, WR = 3 * D, WRP = WR | 1;  // odd LDS row stride
     static_assert(WRP >= 9, "the V / g terms reuse a record staging row");
+    const StampScope stamp_(stp);
     __shared__ double wst[kLinThreads * WRP];
     const int t = threadIdx.x;
     const int tb = blk[blockIdx.x], te = blk[blockIdx.x + 1];
@@ -616,7 +617,8 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                                                       const double* __restrict__ Vinv, const double* __restrict__ y,
                                                       const double* __restrict__ U, const double* __restrict__ gc, double f,
                                                       double cmin, double cmax, int add_diag, double* __restrict__ S,
-                                                      double* __restrict__ b) {
+                                                      double* __restrict__ b, long long* stp) {
+    const StampScope stamp_(stp);
     constexpr int DD = D * D;
     constexpr int BS = schur_bs(D);  // LDS stride of an accumulated block (padded off the 64-bank period)
     constexpr int WS = schur_ws(D);  // LDS stride of a group's W^ staging
@@ -1160,7 +1162,8 @@ __global__ __launch_bounds__(kCgThreads) void k_cg_iter(int it, int C, int maxit
 // dc = L^-T x~
 template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_finish(int C, const double* __restrict__ Li, const double* __restrict__ xt,
-                                                        double* __restrict__ dc) {
+                                                        double* __restrict__ dc, long long* stp) {
+    const StampScope stamp_(stp);
     const int k = blockIdx.x * kThreads + threadIdx.x;
     if (k >= C * D) return;
     const int i = k / D, a = k % D;
@@ -1459,7 +1462,8 @@ __global__ __launch_bounds__(kThreads) void k_publish(const double* __restrict__
                                                       int can_reject, const double* __restrict__ cams_new,
                                                       double* __restrict__ cams_cur, long long ncam,
                                                       const double* __restrict__ pts_new, double* __restrict__ pts_cur,
-                                                      long long npts) {
+                                                      long long npts, long long* stp) {
+    const StampScope stamp_(stp);
     const double loss = result[0];
     // cgst (a k_tl_cgp solve whose status the host reads afterwards): only a converged CG's trial can be accepted
     // (result[5]: a k_tl_cgp abort on any rank -- every rank then repeats the trial on the launch path)
@@ -1517,7 +1521,9 @@ struct insfm_ba {
     int64_t n_nbr = 0;
     int nbr_stride = 0;  // > 0: every CG row has exactly nbr_stride neighbour slots (padded), row r starts at r * stride
     bool flags_dirty = false;  // a solve's point preparation ran and no k_final has consumed (cleared) its flag yet
-    int keep_S = 0;      // write the scaled S~ back into S (only the debug getters read it; set by the debug entry points)
+    int keep_S = 0;      // debug entry points: every solve forms the scaled copy Sn (insfm_ba_debug_get(5) reads S~ from it;
+                         // S itself stays unscaled -- k_tl_cgp reads it)
+    std::vector<int> pos_up_host;  // [nnzb] Sn slot of each upper block (debug_get(5))
     int4* work = nullptr;
     int nwork = 0, nnzb = 0, max_chunk = 0;
     size_t schur_lds = 0;
@@ -1576,6 +1582,8 @@ struct insfm_ba {
     double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
     int* cgp_src = nullptr;     // [n_nbr] S block of each CG slot: e (upper), ~e (lower, transposed), INT_MIN (pad)
     bool sn_valid = false;      // Sn holds the scaled S~ of the current solve (k_cg_scale ran for it)
+    long long* stamps = nullptr;  // INSFM_DIAG=stamps: [kStampSteps][kStKinds][2] kernel entry / exit (wall_clock64)
+    long long stamp_step = 0;     // LM steps stamped so far
     unsigned cgp_epochs = 0;  // grid barriers the counters in cgp_sync have counted (reset with them)
     bool cgp_defer = false;
     int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
@@ -1903,6 +1911,11 @@ int allreduce_async(insfm_ba* h, double* buf, int64_t n) {
     return 0;
 }
 
+long long* stamp_ptr(const insfm_ba* h, int kind) {
+    if (!h->stamps) return nullptr;
+    return h->stamps + ((size_t)(h->stamp_step % kStampSteps) * kStKinds + kind) * 2;
+}
+
 void rec(insfm_ba* h, int k) {
     if (h->timing) (void)hipEventRecord(h->ev[k], h->stream);
 }
@@ -2023,7 +2036,7 @@ template <int M>
 void launch_lin_points_w(insfm_ba* h, const double* cams, const double* pts_local, const PointPrep& pp1) {
     k_lin_points<M><<<h->n_lin, kLinThreads, 0, h->stream>>>(h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams,
                                                          pts_local, h->d.huber_delta, pp1.R ? h->W : nullptr, h->V, h->gp,
-                                                         pp1);
+                                                         pp1, stamp_ptr(h, kStLinPoints));
 }
 
 int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
@@ -2095,13 +2108,14 @@ int run_linearize(insfm_ba* h, const double* cams, const double* pts_local) {
 int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
     const int C = h->C;
     if (h->kind == 1) {
-        k_tl_basis<kGP><<<cdiv(C * 4, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
+        k_tl_basis<kGP><<<h->tl.nc, kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
         return launch_err(h, "k_tl_basis");
     }
     return with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int MC = kD<M> + 1;
-        k_tl_basis<M><<<cdiv(C * MC, kThreads), kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
+        k_tl_basis<M><<<h->tl.nc, kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
+        (void)MC;
         return launch_err(h, "k_tl_basis");
     });
 }
@@ -2301,7 +2315,8 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
         hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->S,
                            h->cgp_src, h->Li, h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
                            h->cgp_tag, h->cgp_sync,
-                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace);
+                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace,
+                           stamp_ptr(h, kStCgp));
     };
     if (h->cgp_det) {
         if (h->cgp_nb == 64) go(k_tl_cgp<64, true>);
@@ -2323,7 +2338,7 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
         if (det)
             k_schur<3, 1, true><<<h->nwork, nt, h->schur_lds, h->stream>>>(
                 h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
-                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+                h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, nullptr);
         else
             k_schur_gp<kSchurWaves, kGPSG><<<h->nwork, nt, h->schur_lds, h->stream>>>(
                 h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->sdesc, h->cam, h->W, h->VY, Uin, gcin, h->S, h->b);
@@ -2335,7 +2350,7 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3(w1 - w0), dim3(nt), h->schur_lds, h->stream,
                 h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
-                h->W, h->Mp, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b);
+                h->W, h->Mp, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, stamp_ptr(h, kStSchur));
         };
         if (det) retry ? go(k_schur<DV, 1, false, true>) : go(k_schur<DV, 1>);
         else retry ? go(k_schur<DV, kSchurWaves, false, true>) : go(k_schur<DV, kSchurWaves>);
@@ -2599,7 +2614,7 @@ int cg_tail(insfm_ba* h, int* st) {
     rc = with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
-                                                                                        h->dc);
+                                                                                        h->dc, stamp_ptr(h, kStCgFinish));
         return launch_err(h, "k_cg_finish");
     });
     if (rc) return rc;
@@ -2616,7 +2631,7 @@ int ensure_sn(insfm_ba* h) {
     const int rc = with_D(h->D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
-            h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
+            h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, 0);
         return launch_err(h, "k_cg_scale");
     });
     if (!rc) h->sn_valid = true;
@@ -2703,7 +2718,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
                 h->d.clamp_min, h->d.clamp_max);
             if (scale)
                 k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
-                    h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, h->keep_S);
+                    h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, 0);
             return launch_err(h, "k_cg_factor/scale");
         });
         h->sn_valid = scale;
@@ -2812,7 +2827,8 @@ int finish_cost(insfm_ba* h, const TrialAccept* ta) {
     const int grid = copy ? std::max(1, std::min(1024, cdiv(std::max(ncam, npts / 2 + 1), kThreads))) : 1;
     k_publish<<<grid, kThreads, 0, h->stream>>>(h->result, h->cgp_pending ? h->cg.status : nullptr, h->pub_dev, seq,
                                                ta ? ta->last : 0.0, ta ? ta->can_reject : 0,
-                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts);
+                                               h->cams_new, copy ? h->cams_cur : nullptr, ncam, h->pts_new, h->pts_cur, npts,
+                                               stamp_ptr(h, kStPublish));
     if (int rc = launch_err(h, "k_publish")) return rc;
     hmark(h, "publish");
     const unsigned* w = reinterpret_cast<const unsigned*>(h->pub_host + 8);
@@ -3029,6 +3045,7 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
         st->coarse_used = h->coarse_used;
     }
     h->timing = false;
+    if (h->stamps) ++h->stamp_step;
     if (host_trace2() && !h->hmarks.empty()) {
         hmark(h, "step end");
         std::string line = "[insfm host2]";
@@ -3609,6 +3626,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if ((rc = upload(h, &h->nbr_ptr, nptr.data(), nptr.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->nbr_j, nj.data(), nj.size()))) return fail(rc, "");
     if ((rc = upload(h, &h->pos_up, pup.data(), pup.size()))) return fail(rc, "");
+    h->pos_up_host = pup;
     if ((rc = upload(h, &h->pos_lo, plo.data(), plo.size()))) return fail(rc, "");
     {
         const int DPd = D + (D & 1);
@@ -3971,6 +3989,11 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
     }
     tick("two-level setup (end)");
+    if (kind == 0 && diag("stamps")) {
+        const size_t n = (size_t)kStampSteps * kStKinds * 2;
+        if ((rc = dalloc(h, (void**)&h->stamps, sizeof(long long) * n))) return fail(rc, "");
+        if (hipMemsetAsync(h->stamps, 0, sizeof(long long) * n, h->stream) != hipSuccess) return fail(INSFM_BA_EHIP, "stamps");
+    }
     h->damping = 1.0 / desc->tr_radius;
     h->down = desc->tr_down;
     *out = h;
@@ -4025,6 +4048,21 @@ int insfm_ba_cg_info(const insfm_ba* h, int32_t* out) {
     out[2] = h->cgp_slots;
     out[3] = h->cgp_nb;
     return INSFM_BA_OK;
+}
+
+int32_t insfm_ba_debug_stamps(insfm_ba* h, int64_t* host_out, int32_t max_steps) {
+    if (!h || !host_out || max_steps < 0) return INSFM_BA_EINVAL;
+    if (!h->stamps) return 0;
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const long long n = std::min<long long>(std::min<long long>(h->stamp_step, kStampSteps), max_steps);
+    std::vector<long long> ring((size_t)kStampSteps * kStKinds * 2);
+    HIPCHK(hipMemcpy(ring.data(), h->stamps, sizeof(long long) * ring.size(), hipMemcpyDeviceToHost));
+    const long long first = h->stamp_step - n;  // the oldest of the last n steps
+    for (long long q = 0; q < n; ++q) {
+        const size_t src = (size_t)((first + q) % kStampSteps) * kStKinds * 2;
+        std::memcpy(host_out + (size_t)q * kStKinds * 2, ring.data() + src, sizeof(long long) * kStKinds * 2);
+    }
+    return (int32_t)n;
 }
 
 int insfm_ba_set_persistent_cg(insfm_ba* h, int32_t on) {
@@ -4396,7 +4434,25 @@ int64_t insfm_ba_debug_get(insfm_ba* h, int32_t which, double* host) {
         case 2: src = h->gp; n = Pl * 3; break;
         case 3: src = h->U; n = C * D * D; break;
         case 4: src = h->gc; n = C * D; break;
-        case 5: src = h->S; n = (size_t)h->nnzb * D * D; break;
+        case 5: {  // the scaled upper blocks S~ (diagonal: I), assembled from the row-contiguous copy Sn
+            if (h->kind != 0 && h->kind != 1) return INSFM_BA_EINVAL;
+            if (int rc0 = side_flush(h)) return rc0;
+            if (int rc0 = ensure_sn(h)) return rc0;
+            const size_t DP = D + (D & 1), nb = (size_t)h->nnzb;
+            std::vector<double> sn((size_t)std::max<int64_t>(h->n_nbr, 1) * D * DP);
+            if (h->n_nbr) HIPCHK(hipMemcpyAsync(sn.data(), h->Sn, sizeof(double) * h->n_nbr * D * DP, hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(hipStreamSynchronize(h->stream));
+            std::vector<int> rp(C + 1);
+            HIPCHK(hipMemcpy(rp.data(), h->row_ptr, sizeof(int) * (C + 1), hipMemcpyDeviceToHost));
+            std::vector<char> diag_blk(nb, 0);
+            for (size_t i = 0; i < C; ++i) diag_blk[rp[i]] = 1;
+            for (size_t e = 0; e < nb; ++e)
+                for (size_t a = 0; a < D; ++a)
+                    for (size_t c = 0; c < D; ++c)
+                        host[(e * D + a) * D + c] = diag_blk[e] ? (a == c ? 1.0 : 0.0)
+                                                                : sn[((size_t)h->pos_up_host[e] * D + a) * DP + c];
+            return (int64_t)(nb * D * D);
+        }
         case 6: src = h->b; n = C * D; break;
         case 7: src = h->dc; n = C * D; break;
         case 8: src = h->dp; n = Pl * 3; break;

@@ -18,6 +18,7 @@
 //   k_tl_pspmv   : n = S~ m (row-contiguous Sn stream), the row's vector updates, its partials for the next iteration
 #pragma once
 #include <algorithm>
+#include <utility>
 
 #include "ba_common.h"
 
@@ -72,14 +73,35 @@ __device__ __forceinline__ void st_sc1(double* p, double v) { __hip_atomic_store
 __device__ __forceinline__ double ld_sc1(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // ---- setup ---------------------------------------------------------------------------------------------------
-// One thread per (camera i, coarse column k): column k of G_i at the linearization point and Z~_i[:,k] = L_i^T G_i[:,k].
+// One workgroup per camera cluster c, one thread per (member camera i, coarse column k): column k of G_i at the
+// linearization point and Z~_i[:,k] = L_i^T G_i[:,k], the row partial Z~_i[:,k]^T r0_i of the restriction of the CG's
+// starting residual; then the cluster's restriction R_c[k] = sum of its members' partials in cluster order (k_tl_pc's
+// order of additions) into tl.Rc (k_tl_cgp's coarse solve of r0 reads it; k_tl_pc sums the partials itself).
+template <int M>
+__device__ __forceinline__ void tl_basis_entry(int i, int k, const double* __restrict__ cams, const double* __restrict__ Lf,
+                                               const TlBufs& tl, const double* __restrict__ r0);
+
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __restrict__ cams, const double* __restrict__ Lf,
                                                        TlBufs tl, const double* __restrict__ r0) {
+    constexpr int D = kD<M>, MC = D + 1;
+    const int c = blockIdx.x, e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
+    for (int g = threadIdx.x; g < ne * MC; g += kThreads) tl_basis_entry<M>(tl.cl_cams[e0 + g / MC], g % MC, cams, Lf, tl, r0);
+    __syncthreads();  // (the block's rowR stores are visible to the block behind the barrier)
+    if (threadIdx.x < MC) {
+        const int k = threadIdx.x;
+        double v = 0.0;
+        for (int e = 0; e < ne; ++e) v += tl.rowR[(size_t)(e0 + e) * MC + k];
+        tl.Rc[(size_t)c * MC + k] = v;
+    }
+    (void)D;
+    (void)C;
+}
+
+template <int M>
+__device__ __forceinline__ void tl_basis_entry(int i, int k, const double* __restrict__ cams, const double* __restrict__ Lf,
+                                               const TlBufs& tl, const double* __restrict__ r0) {
     constexpr int D = kD<M>, MC = D + 1, ST = kStride<M>;
-    const int g = blockIdx.x * kThreads + threadIdx.x;
-    if (g >= C * MC) return;
-    const int i = g / MC, k = g % MC;
     double col[D];
 #pragma unroll
     for (int a = 0; a < D; ++a) col[a] = 0.0;
@@ -328,6 +350,10 @@ __device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __res
 
 // In-place scalar Gauss-Jordan inversion of the SPD block in M (LDS) by wave 0 (lane r & 31 = row r), result back into
 // M; every thread of the workgroup must call it.  Returns (in wave 0) whether a pivot was not positive.
+// GJ_PINV 6 (default since round 5): lane l holds the 4 x 4 sub-block (rows 4 (l & 7) .., columns 4 (l >> 3) ..), the
+// pivot column / row entries it needs come by ds_bpermute -- about half the instructions per pivot of variant 4: the
+// inversion of E (m = 639) 310 -> 242 us standalone, bitwise equal (tools/bench_dense.hip, profiles/r5_v2/);
+// 5: variant 4's layout with the pivot row broadcast by ds_swizzle (294 us);
 // GJ_PINV 0: the pivot row is broadcast by readlane (2 x 32 v_readlane per pivot); 1: lane p stores its row in LDS and
 // every lane reads it back (one 16-B read per column pair, all lanes the same address); 2: timing only (no inversion,
 // results wrong); 3: all 256 threads, four entries each, the matrix ping-ponged through LDS; 4: one wave, 16 entries
@@ -335,8 +361,91 @@ __device__ __forceinline__ void gj_stage(double (*dst)[kGS], const double* __res
 // the same order.  (Round 4: a variant exchanging the pivot row and column by lane permutes instead of LDS was bitwise
 // equal and 8-10 % slower at m = 567-747, profiles/r4_v2/gj_pinv4_vs_pinv5.log, and was removed.)
 #ifndef GJ_PINV
-#define GJ_PINV 4
+#define GJ_PINV 6
 #endif
+// variant 5: lane P of each 32-lane half, broadcast to its half by ds_swizzle (BitMode: and 0, or P, xor 0) -- the LDS
+// crossbar without an LDS store, a fence or a read-back
+template <int P>
+__device__ __forceinline__ double swz_bcast(double v) {
+    constexpr int pat = P << 5;
+    const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+    const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+    return __hiloint2double(hi, lo);
+}
+// one pivot round of variant 5 (variant 4's arithmetic: the same products and fused multiply-adds in the same order)
+template <int P>
+__device__ __forceinline__ void gj_p5_round(double (&a)[16], int r, int h, bool& bad) {
+    constexpr int hp = P >> 4, jp = P & 15;
+    double pr[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) pr[j] = swz_bcast<P>(a[j]);  // row P, this half's columns
+    const double mine = a[jp];
+    const double other = __shfl_xor(mine, 32, 64);               // row r, column P from the other half
+    double piv = readlane_d(mine, P + 32 * hp);
+    const double aip = (h == hp) ? mine : other;
+    if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+    const double inv = 1.0 / piv;
+    const int cb = 16 * h;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        if (cb + j == P) {
+            a[j] = (r == P) ? inv : -aip * inv;
+        } else {
+            const double rpc = pr[j] * inv;
+            a[j] = (r == P) ? rpc : __builtin_fma(-aip, rpc, a[j]);
+        }
+    }
+}
+template <int... P>
+__device__ __forceinline__ void gj_p5_all(double (&a)[16], int r, int h, bool& bad, std::integer_sequence<int, P...>) {
+    (gj_p5_round<P>(a, r, h, bad), ...);
+}
+
+// variant 6: lane l holds the 4 x 4 sub-block (rows 4 (l & 7) .., columns 4 (l >> 3) ..); per pivot P the lane fetches
+// the 4 pivot-column entries of its rows and the 4 pivot-row entries of its columns by ds_bpermute from the two lanes
+// that hold them (16 dword permutes), forms 4 scaled row entries and does 16 fused multiply-adds -- variant 4's values
+// for every entry (rpc = row * (1 / piv), fma(-aip, rpc, a), the pivot row / column cases), in half the instructions
+__device__ __forceinline__ double bperm_d(int src_lane, double v) {
+    const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, __double2loint(v));
+    const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, __double2hiint(v));
+    return __hiloint2double(hi, lo);
+}
+template <int P>
+__device__ __forceinline__ void gj_p6_round(double (&a)[4][4], int rb, int cb, bool& bad) {
+    constexpr int PB = P >> 2, PI = P & 3;
+    double colv[4], rowv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) colv[i] = bperm_d(PB * 8 + rb, a[i][PI]);  // row 4 rb + i, column P
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rowv[c] = bperm_d(cb * 8 + PB, a[PI][c]);  // row P, column 4 cb + c
+    double piv = readlane_d(a[PI][PI], PB * 8 + PB);
+    if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+    const double inv = 1.0 / piv;
+    double rpc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rpc[c] = rowv[c] * inv;
+    const bool prow = rb == PB, pcol = cb == PB;  // this lane holds part of row P / of column P
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double up = __builtin_fma(-colv[i], rpc[c], a[i][c]);
+            if (c == PI && i == PI) {
+                a[i][c] = pcol ? (prow ? inv : -colv[i] * inv) : (prow ? rpc[c] : up);
+            } else if (c == PI) {
+                a[i][c] = pcol ? -colv[i] * inv : up;
+            } else if (i == PI) {
+                a[i][c] = prow ? rpc[c] : up;
+            } else {
+                a[i][c] = up;
+            }
+        }
+}
+template <int... P>
+__device__ __forceinline__ void gj_p6_all(double (&a)[4][4], int rb, int cb, bool& bad, std::integer_sequence<int, P...>) {
+    (gj_p6_round<P>(a, rb, cb, bad), ...);
+}
+
 __device__ bool gj_invert_block(double (*M)[kGS]) {
 #if GJ_PINV == 2
     __syncthreads();
@@ -429,6 +538,43 @@ __device__ bool gj_invert_block(double (*M)[kGS]) {
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) M[r][cb + j] = a[j];
+    }
+    __syncthreads();
+    return bad;
+#elif GJ_PINV == 5
+    // one wave, variant 4's layout (lane l: row l & 31, columns 16 (l >> 5) .. +15) and arithmetic; per pivot the
+    // pivot row goes to each half by ds_swizzle, the pivot by readlane, the other half's pivot-column entry by one
+    // permute: no LDS traffic and no fence in the pivot loop
+    static_assert(kGB == 32, "64 lanes = 32 rows x 2 column halves");
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, r = l & 31, h = l >> 5, cb = 16 * h;
+        double a[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) a[j] = M[r][cb + j];
+        gj_p5_all(a, r, h, bad, std::make_integer_sequence<int, kGB>{});
+#pragma unroll
+        for (int j = 0; j < 16; ++j) M[r][cb + j] = a[j];
+    }
+    __syncthreads();
+    return bad;
+#elif GJ_PINV == 6
+    static_assert(kGB == 32, "64 lanes = 8 x 8 sub-blocks of 4 x 4");
+    __syncthreads();
+    bool bad = false;
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x, rb = l & 7, cb = l >> 3;
+        double a[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[i][c] = M[4 * rb + i][4 * cb + c];
+        gj_p6_all(a, rb, cb, bad, std::make_integer_sequence<int, kGB>{});
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) M[4 * rb + i][4 * cb + c] = a[i][c];
     }
     __syncthreads();
     return bad;

@@ -330,6 +330,14 @@ class BundleAdjuster:
         _capi.check(self._h, _capi.load().insfm_ba_debug_time_kernel(self._h, int(which), int(reps), ctypes.byref(us)))
         return us.value
 
+    def debug_stamps(self, max_steps=1024):
+        """INSFM_DIAG=stamps: int64 [steps, 5, 2] device-clock (100 MHz) entry / exit of k_lin_points, k_schur,
+        k_tl_cgp, k_cg_finish, k_publish per LM step (insfm_ba_debug_stamps); an empty array when off."""
+        out = np.zeros((max_steps, 5, 2), dtype=np.int64)
+        n = _capi.load().insfm_ba_debug_stamps(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), max_steps)
+        _capi.check(self._h, n)
+        return out[:n]
+
     def cg_info(self):
         """(path code, k_tl_cgp grid, workgroup slots, register blocks per row) -- insfm_ba_cg_info; CG_PATHS names
         the codes."""

@@ -59,7 +59,7 @@ def test_config2_replicated_persistent_cg(nproc):
     launch per trial on every rank, bitwise-equal cameras across ranks, loss 1e-9 / parameters 1e-7 against one GPU."""
     out = _run(nproc, "gloo", ["--config", "2", "--steps", "3"])
     assert out["ranks_per_device"] == nproc, out
-    assert all(p == (2, 2) for p in out["cg_paths"]), out  # fixed-order k_tl_cgp agreed, kept through the steps
+    assert all(list(p) == [2, 2] for p in out["cg_paths"]), out  # fixed-order k_tl_cgp agreed, kept through the steps
     assert out["cg_launches"] == out["trials"], out
     assert out["cams_equal_across_ranks"], out
     assert out["loss_rel"] < 1e-9, out
@@ -71,7 +71,7 @@ def test_one_rank_ineligible_takes_every_rank_to_launch_path():
     """ADVICE r4: k_tl_cgp eligibility is decided collectively.  Rank 1 alone runs with INSFM_DIAG=no_cgp (ineligible);
     engine.agree_cg_path then turns the persistent CG off on every rank, and the run still matches one GPU."""
     out = _run(2, "gloo", ["--config", "2", "--steps", "3", "--diag-rank", "1", "--diag", "no_cgp"])
-    assert all(p == (0, 0) for p in out["cg_paths"]), out
+    assert all(list(p) == [0, 0] for p in out["cg_paths"]), out
     assert all(l > t for l, t in zip(out["cg_launches"], out["trials"])), out
     assert out["cams_equal_across_ranks"], out
     assert out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7, out
@@ -84,7 +84,7 @@ def test_cgp_abort_on_one_rank_is_collective():
     the persistent CG and repeats the solve on the launch path from r0.  The run completes, the ranks stay bitwise
     equal, and it matches one GPU."""
     out = _run(2, "gloo", ["--config", "2", "--steps", "3", "--diag-rank", "1", "--diag", "cgp_fault"])
-    assert all(p == (2, 0) for p in out["cg_paths"]), out  # k_tl_cgp agreed at create, launch path after the abort
+    assert all(list(p) == [2, 0] for p in out["cg_paths"]), out  # k_tl_cgp agreed at create, launch path after the abort
     assert out["cams_equal_across_ranks"], out
     assert out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
 

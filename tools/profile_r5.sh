@@ -16,6 +16,12 @@ S[trace]="trace|240|cd /tmp && rocprofv3 --kernel-trace --stats --output-format 
 S[trace_hold]="trace_hold|240|cd /tmp && INSFM_DIAG=chain_hold rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_hold -o run -- python3 $R/bench.py --no-cpu --no-solve"
 S[pmc_fetch]="pmc_fetch|150|cd /tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu --no-solve"
 S[pmc_write]="pmc_write|150|cd /tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --steps 2 --warmup 0 --no-cpu --no-solve"
+S[stamps]="stamps|200|INSFM_DIAG=stamps python -u tools/stamp_probe.py > $R/gpurun_out/stamps.log"
+S[ab_old]="ab_old|600|tools/ab_trees.sh 3 abtree/old"
+S[cgtrace]="cgtrace|300|INSFM_DIAG=cgp_trace python -u bench.py --no-cpu --no-solve --steps 6 > $R/gpurun_out/cgtrace_new.json 2> $R/gpurun_out/cgtrace_new.err; INSFM_DIAG=cgp_trace python -u abtree/old/bench.py --no-cpu --no-solve --steps 6 > $R/gpurun_out/cgtrace_old.json 2> $R/gpurun_out/cgtrace_old.err"
+S[gj]="gj|200|for m in 567 639 747; do tools/bench_dense_p5 \$m 30; tools/bench_dense_p6 \$m 30; done"
+S[ab_k]="ab_k|600|tools/ab_args.sh 2 --cluster-size=14 --cluster-size=12 --cluster-size=10 --cluster-size=16"
+S[sp]="sp|300|python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_default.log 2>&1; INSFM_DIAG=no_cgp python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_nocgp.log 2>&1; INSFM_DIAG=cgp_trace python -u -m pytest tests/test_gpu_parity.py -q -k \"test_solve_parity and 1-32-True-2\" -s --timeout 120 --timeout-method thread > $R/gpurun_out/sp_trace.log 2>&1; true"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done
