@@ -1660,6 +1660,7 @@ namespace {
 //   cgp128        k_tl_cgp with 128 register blocks per row even for shorter rows (tests the wide variant)
 //   own_streams   per-handle side / linearization streams instead of the process-wide ones (A/B)
 //   chain_hold    timing only: the lagged coarse-inverse chain is never issued (later solves keep an older E^-1)
+//   side_hi / side_normal   the coarse-inverse side stream at the high / normal stream priority (default: lowest)
 bool diag(const char* name) {
     static const std::string v = [] { const char* e = std::getenv("INSFM_DIAG"); return std::string(e ? e : ""); }();
     const size_t n = std::strlen(name);
@@ -3898,7 +3899,9 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         // normal and high: no measured effect either way, round 1)
         int prio_lo = 0, prio_hi = 0;
         if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-        if (e == hipSuccess) e = helper_stream(0, prio_lo, &h->side);
+        // (INSFM_DIAG=side_hi / side_normal: the side stream at the high / normal priority instead, for A/B runs)
+        const int side_prio = diag("side_hi") ? prio_hi : diag("side_normal") ? 0 : prio_lo;
+        if (e == hipSuccess) e = helper_stream(0, side_prio, &h->side);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_E, hipEventDisableTiming);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&h->ev_built, hipEventDisableTiming);
         for (int sl = 0; sl < 2 && e == hipSuccess; ++sl) e = hipEventCreateWithFlags(&h->ev_fact[sl], hipEventDisableTiming);

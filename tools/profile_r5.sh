@@ -22,6 +22,7 @@ S[cgtrace]="cgtrace|300|INSFM_DIAG=cgp_trace python -u bench.py --no-cpu --no-so
 S[gj]="gj|200|for m in 567 639 747; do tools/bench_dense_p5 \$m 30; tools/bench_dense_p6 \$m 30; done"
 S[ab_k]="ab_k|600|tools/ab_args.sh 2 --cluster-size=14 --cluster-size=12 --cluster-size=10 --cluster-size=16"
 S[sp]="sp|300|python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_default.log 2>&1; INSFM_DIAG=no_cgp python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_nocgp.log 2>&1; INSFM_DIAG=cgp_trace python -u -m pytest tests/test_gpu_parity.py -q -k \"test_solve_parity and 1-32-True-2\" -s --timeout 120 --timeout-method thread > $R/gpurun_out/sp_trace.log 2>&1; true"
+S[ab_prio]="ab_prio|400|tools/ab_env.sh 3 side_hi; tools/ab_env.sh 2 side_normal"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done
