@@ -783,12 +783,13 @@ def main():
     # the dominant kernel: the most device time per LM step on the default path (launches per step x hipEvent-timed
     # average launch)
     name = max(kern, key=lambda k: kern[k][0])
-    traffic_tab = {}
+    traffic_tab, traffic_it = {}, {}
     try:
         with open(os.path.join(REPO, "profiles", "pmc_traffic.json")) as f:
             tr = json.load(f)
         if tr.get("config") == args.config:
             traffic_tab = {k: v["hbm_bytes_per_launch"] for k, v in tr.get("kernels", {}).items()}
+            traffic_it = {k: v.get("iterations") for k, v in tr.get("kernels", {}).items()}
     except (OSError, ValueError):
         pass
 
@@ -801,7 +802,7 @@ def main():
              "launches_per_step": round(lps, 3), "device_us_per_step": round(per_step, 2),
              "timing": "hipEvents on the library stream (insfm_ba_debug_time_kernel / insfm_ba_debug_time_cgp)"}
         if kname == "k_tl_cgp":
-            e.update(iterations_per_solve=round(ext["iters"], 2),
+            e.update(iterations_per_solve=round(ext["iters"], 2), traffic_iterations=traffic_it.get(kname),
                      us_per_iteration_incl_setup_share=round(avg_us / max(ext["iters"], 1.0), 3),
                      bytes_formula="8*[(nnzb-C)*D^2 + C*D*(D+1) + C*D^2 + 16*C*D + iters*(m^2 + 2*C*D + 4*m + 2*(3*nc+m))]",
                      timing="hipEvents around the k_tl_cgp launch of a solve re-run from its rhs "

@@ -201,9 +201,10 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
  * run k_tl_cgp.  Overwrites CG scratch state.  (Measurement of PCG(tol=1e-5), bundle_adjustment.py:117.) */
 int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out);
 /* INSFM_DIAG=stamps only (else returns 0): the device-clock timestamps (wall_clock64, 100 MHz) of the last
- * min(steps taken, 1024, max_steps) LM steps, oldest first, [steps][5 kernels][entry, exit] as int64 into HOST memory:
- * kernels k_lin_points, k_schur, k_tl_cgp, k_cg_finish, k_publish (the last launch of each in the step; exit = the
- * latest workgroup end).  Tracer-free step-boundary and post-CG gaps.  Returns the number of steps copied. */
+ * min(steps taken, 1024, max_steps) LM steps, oldest first, [steps][10 kernels][entry, exit] as int64 into HOST
+ * memory: kernels k_lin_points, k_schur, k_tl_cgp, k_cg_finish, k_publish, k_cg_factor, k_tl_basis, k_backsub_rc,
+ * k_cost, k_final (the trial's: the last launch of each in the step; entry = workgroup 0's, exit = the latest
+ * workgroup end; 0 = not launched).  Tracer-free main-queue busy time and gaps.  Returns the number of steps copied. */
 int32_t insfm_ba_debug_stamps(insfm_ba* h, int64_t* host_out, int32_t max_steps);
 /* Camera cluster labels [C] of the two-level preconditioner's coarse space (HOST out); returns the cluster count. */
 int32_t insfm_ba_debug_clusters(const insfm_ba* h, int32_t* labels);

@@ -55,18 +55,25 @@ struct CgGeom {
 };
 
 // INSFM_DIAG=stamps: tracer-free timestamps of selected main-queue kernels (wall_clock64, 100 MHz, one clock for the
-// whole device).  p[0] = the entry of workgroup 0, p[1] = the latest end of any workgroup's thread 0 (no-return
-// atomic max); p null: off (the default, no code path change).
+// whole device).  p[0] = the entry of workgroup 0, p[1] = the latest end of the last kStampTail workgroups' thread 0
+// (no-return atomic max; workgroups are dispatched in index order, so the last to finish is among the last
+// dispatched; an atomic from every workgroup of a 16k-workgroup grid tripled its duration); p null: off (the default,
+// no code path change).
+constexpr unsigned kStampTail = 1024;
 struct StampScope {
     unsigned long long* p;
     __device__ explicit StampScope(long long* q) : p(reinterpret_cast<unsigned long long*>(q)) {
         if (p && blockIdx.x == 0 && threadIdx.x == 0) p[0] = (unsigned long long)wall_clock64();
     }
     __device__ ~StampScope() {
-        if (p && threadIdx.x == 0) atomicMax(p + 1, (unsigned long long)wall_clock64());
+        if (p && threadIdx.x == 0 && blockIdx.x + kStampTail >= gridDim.x)
+            atomicMax(p + 1, (unsigned long long)wall_clock64());
     }
 };
 constexpr int kStampSteps = 1024;  // ring of LM steps
-enum StampKind { kStLinPoints = 0, kStSchur = 1, kStCgp = 2, kStCgFinish = 3, kStPublish = 4, kStKinds = 5 };
+enum StampKind {
+    kStLinPoints = 0, kStSchur = 1, kStCgp = 2, kStCgFinish = 3, kStPublish = 4,  // (round 5, first set)
+    kStFactor = 5, kStBasis = 6, kStBacksub = 7, kStCost = 8, kStFinal = 9, kStKinds = 10
+};
 
 }  // namespace insfm

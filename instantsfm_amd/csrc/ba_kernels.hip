@@ -771,7 +771,9 @@ template <int D>
 __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, double* __restrict__ S,
                                                         double* __restrict__ b, double* __restrict__ Lf,
                                                         double* __restrict__ Li, CgBufs cg, const double* __restrict__ Ul,
-                                                        const double* __restrict__ gcl, double f, double cmin, double cmax) {
+                                                        const double* __restrict__ gcl, double f, double cmin, double cmax,
+                                                        long long* stp = nullptr) {
+    const StampScope stamp_(stp);
     constexpr int DD = D * D;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int i = blockIdx.x * kWaves + wv;
@@ -1232,7 +1234,9 @@ __global__ __launch_bounds__(kLinThreads) void k_backsub_rc(const int* __restric
                                                             double* __restrict__ pts_new, double* __restrict__ part,
                                                             int nrun, int C, const double* __restrict__ U,
                                                             const double* __restrict__ gc, int with_gain,
-                                                            double* __restrict__ cams_new, double* __restrict__ part_gc) {
+                                                            double* __restrict__ cams_new, double* __restrict__ part_gc,
+                                                            long long* stp = nullptr) {
+    const StampScope stamp_(stp);
     constexpr int D = kD<M>, ST = kStride<M>;
     __shared__ double red[kLinThreads];
     __shared__ double q[kLinThreads][3];
@@ -1303,7 +1307,9 @@ template <int M>
 __global__ __launch_bounds__(kCostThreads) void k_cost(int Nl, const int* __restrict__ cam, const int* __restrict__ ptl,
                                                        const double* __restrict__ uv, const double* __restrict__ pp,
                                                        const double* __restrict__ cams, const double* __restrict__ pts,
-                                                       double delta, double* __restrict__ part) {
+                                                       double delta, double* __restrict__ part,
+                                                       long long* stp = nullptr) {
+    const StampScope stamp_(stp);
     constexpr int ST = kStride<M>;
     __shared__ double red[2 * (kCostThreads / 64)];
     const int o = blockIdx.x * kCostThreads + threadIdx.x;
@@ -1333,7 +1339,9 @@ constexpr int kFinalThreads = 1024;
 __global__ __launch_bounds__(kFinalThreads) void k_final(const double* __restrict__ cost_part, int ncost,
                                                     const double* __restrict__ gp_part, int ngp,
                                                     const double* __restrict__ gc_part, int ngc, int* __restrict__ flags,
-                                                    double* __restrict__ result, const int* __restrict__ cgst) {
+                                                    double* __restrict__ result, const int* __restrict__ cgst,
+                                                    long long* stp = nullptr) {
+    const StampScope stamp_(stp);
     // the three partial arrays in one pass (every load of a round in flight together), each array still summed by
     // each thread in index order and then by the same butterfly and wave order: bitwise the sums of three separate
     // sum_partials passes, with one latency chain instead of three
@@ -1605,6 +1613,7 @@ struct insfm_ba {
     unsigned long long* cgp_yg = nullptr;  // [kCoarseMax][2] tagged granules of y
     unsigned cgp_tag = 1;               // tag of the next launch's first iteration
     unsigned* cgp_sync = nullptr;
+    bool chain_oseg = false;  // the side chain of slot cgp_slot builds E from k_tl_cgp's segments (reissue_chain)
     // the coarse factorization of solve n runs on `side` while the CG of solve n uses slot (n-1)&1
     double *Ebuf[2]{}, *Einvbuf[2]{};
     double* gjW = nullptr;  // Gauss-Jordan ping-pong buffer [ldE][ldE]
@@ -2115,7 +2124,7 @@ int run_tl_basis(insfm_ba* h, const double* cams, hipStream_t stream) {
     return with_model(h->model, [&](auto mc) -> int {
         constexpr int M = decltype(mc)::value;
         constexpr int MC = kD<M> + 1;
-        k_tl_basis<M><<<h->tl.nc, kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0]);
+        k_tl_basis<M><<<h->tl.nc, kThreads, 0, stream>>>(C, cams, h->Lf, h->tl, h->cg.r[0], stamp_ptr(h, kStBasis));
         (void)MC;
         return launch_err(h, "k_tl_basis");
     });
@@ -2185,6 +2194,7 @@ int issue_side_chain(insfm_ba* h, int slot, bool have_oseg = false) {
     const bool tm = h->timing && !h->chain_timed[slot];
     if (tm) HIPCHK(hipEventRecord(h->ev[12 + slot], fs));
     if (int rc = run_tl_build(h, slot, fs, have_oseg)) return rc;
+    h->chain_oseg = have_oseg;
     HIPCHK(hipEventRecord(h->ev_built, fs));
     h->built_pending = true;
     for (int u = 0; u <= gj_steps(h->tl.m); ++u)
@@ -2464,13 +2474,15 @@ int run_tl_cg(insfm_ba* h, int* st) {
     if (h->cgp_nb) enq = maxit + 2;  // k_tl_cgp: one launch runs every iteration
     if (int rc = enqueue(0, enq)) return rc;
     if (h->cgp_nb) h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
-    if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup)
+    if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup), from k_tl_cgp's segments
         // (INSFM_DIAG=chain_hold, timing only: no lagged chain at all -- later solves keep an older coarse inverse --
         // to measure what the chain's overlap costs the kernels it runs beside)
         static const bool hold = diag("chain_hold");
         if (!hold) {
             HIPCHK(hipEventRecord(h->ev_E, h->stream));
             if (int rc = issue_side_chain(h, h->cgp_slot, true)) return rc;
+        } else {
+            h->chain_oseg = false;
         }
         h->cgp_defer = false;
     }
@@ -2639,6 +2651,16 @@ int ensure_sn(insfm_ba* h) {
     return rc;
 }
 
+// After a k_tl_cgp abort: the basis was formed again on the main stream; a side chain issued from the launch's coarse
+// segments (incomplete when a workgroup never got past the A build) is issued once more from S~ / Z~ (k_tl_erow),
+// behind the first on the side stream, so the next solve's coarse inverse is this solve's.
+int reissue_chain(insfm_ba* h) {
+    if (!h->chain_oseg) return 0;
+    h->chain_oseg = false;
+    HIPCHK(hipEventRecord(h->ev_E, h->stream));
+    return issue_side_chain(h, h->cgp_slot);
+}
+
 int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local) {
     const int D = h->D;
     // the point preparation of the linearization covers this solve when it runs at the prepared damping factor
@@ -2716,7 +2738,7 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
             constexpr int DV = decltype(dc_)::value;
             k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
                 h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
-                h->d.clamp_min, h->d.clamp_max);
+                h->d.clamp_min, h->d.clamp_max, stamp_ptr(h, kStFactor));
             if (scale)
                 k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
                     h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, 0);
@@ -2733,7 +2755,9 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         if (h->cgp_lost) {  // k_tl_cgp aborted (it left r0 alone): the CG again from the basis, launch path
             h->cgp_lost = false;
             HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
-            if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, cams, h->stream)) || (rc = run_tl_cg(h, st))) return rc;
+            if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, cams, h->stream)) || (rc = reissue_chain(h)) ||
+                (rc = run_tl_cg(h, st)))
+                return rc;
         }
         const int ci = cg_tail(h, st);
         if (ci < 0) return ci;
@@ -2764,7 +2788,8 @@ int solve_tail(insfm_ba* h, double f, const double* cams, const double* pts_loca
         const int nrun = h->Pl > 0 ? h->n_lin : 0;  // point runs, then the camera-update blocks
         k_backsub_rc<M><<<nrun + h->n_gc, kLinThreads, 0, h->stream>>>(
             h->lin_blk, h->pt_ptr, h->cam, h->ptl, h->uv, h->pp, cams, h->d.huber_delta, dcp, h->V, h->Vinv, h->gp,
-            pts_local, h->dp, h->pts_new, h->part_gp, nrun, h->C, h->U, h->gc, h->d.rank == 0, h->cams_new, h->part_gc);
+            pts_local, h->dp, h->pts_new, h->part_gp, nrun, h->C, h->U, h->gc, h->d.rank == 0, h->cams_new, h->part_gc,
+            stamp_ptr(h, kStBacksub));
         return launch_err(h, "k_backsub_rc");
     });
     if (rc) return rc;
@@ -2802,7 +2827,8 @@ int cgp_collective_fallback(insfm_ba* h, int st0) {
     });
     if (rc) return rc;
     if (int r2 = ensure_sn(h)) return r2;
-    return run_tl_basis(h, h->cams_cur, h->stream);
+    if (int r3 = run_tl_basis(h, h->cams_cur, h->stream)) return r3;
+    return reissue_chain(h);
 }
 
 // lm_step's accept rule for the trial being costed (k_publish copies an accepted trial into the caller's buffers)
@@ -2886,10 +2912,12 @@ int run_cost(insfm_ba* h, const double* cams, const double* pts_local, bool gain
         constexpr int M = decltype(mc)::value;
         if (h->Nl > 0)
             k_cost<M><<<h->n_cost, kCostThreads, 0, h->stream>>>(h->Nl, h->cam, h->ptl, h->uv, h->pp, cams, pts_local,
-                                                             h->d.huber_delta, h->part_cost);
+                                                             h->d.huber_delta, h->part_cost,
+                                                             gains ? stamp_ptr(h, kStCost) : nullptr);
         k_final<<<1, kFinalThreads, 0, h->stream>>>(h->part_cost, h->Nl > 0 ? h->n_cost : 0, gains && h->Pl > 0 ? h->part_gp : nullptr,
                                                h->n_gp, gains ? h->part_gc : nullptr, h->n_gc, h->flags, h->result,
-                                               h->cgp_pending ? h->cg.status : nullptr);
+                                               h->cgp_pending ? h->cg.status : nullptr,
+                                               gains ? stamp_ptr(h, kStFinal) : nullptr);
         return launch_err(h, "k_cost/k_final");
     });
     if (rc) return rc;
@@ -2959,7 +2987,8 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
                 h->cgp_lost = false;
                 HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
                 int* st = reinterpret_cast<int*>(h->host_res + 8);
-                if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = run_tl_cg(h, st)))
+                if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = reissue_chain(h)) ||
+                    (rc = run_tl_cg(h, st)))
                     return rc;
                 it = cg_tail(h, st);
                 if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }

@@ -83,7 +83,9 @@ __device__ __forceinline__ void tl_basis_entry(int i, int k, const double* __res
 
 template <int M>
 __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __restrict__ cams, const double* __restrict__ Lf,
-                                                       TlBufs tl, const double* __restrict__ r0) {
+                                                       TlBufs tl, const double* __restrict__ r0,
+                                                       long long* stp = nullptr) {
+    const StampScope stamp_(stp);
     constexpr int D = kD<M>, MC = D + 1;
     const int c = blockIdx.x, e0 = tl.cl_ptr[c], ne = tl.cl_ptr[c + 1] - e0;
     for (int g = threadIdx.x; g < ne * MC; g += kThreads) tl_basis_entry<M>(tl.cl_cams[e0 + g / MC], g % MC, cams, Lf, tl, r0);

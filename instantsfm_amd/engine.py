@@ -19,6 +19,9 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
                    pcg_max_iter=500, precond=1, cluster_size=14, exchange_chunks=4)
 
 
+# insfm_ba_debug_stamps' kernel order (ba_common.h StampKind)
+STAMP_KERNELS = ("k_lin_points", "k_schur", "k_tl_cgp", "k_cg_finish", "k_publish", "k_cg_factor", "k_tl_basis",
+                 "k_backsub_rc", "k_cost", "k_final")
 CG_PATHS = {0: "launch-per-iteration two-level CG", 1: "k_tl_cgp (persistent, atomic cluster sums)",
             2: "k_tl_cgp (persistent, fixed-order)", 3: "row-partitioned CG"}
 
@@ -331,9 +334,10 @@ class BundleAdjuster:
         return us.value
 
     def debug_stamps(self, max_steps=1024):
-        """INSFM_DIAG=stamps: int64 [steps, 5, 2] device-clock (100 MHz) entry / exit of k_lin_points, k_schur,
-        k_tl_cgp, k_cg_finish, k_publish per LM step (insfm_ba_debug_stamps); an empty array when off."""
-        out = np.zeros((max_steps, 5, 2), dtype=np.int64)
+        """INSFM_DIAG=stamps: int64 [steps, 10, 2] device-clock (100 MHz) entry / exit of k_lin_points, k_schur,
+        k_tl_cgp, k_cg_finish, k_publish, k_cg_factor, k_tl_basis, k_backsub_rc, k_cost, k_final per LM step
+        (insfm_ba_debug_stamps; STAMP_KERNELS names them); an empty array when off."""
+        out = np.zeros((max_steps, len(STAMP_KERNELS), 2), dtype=np.int64)
         n = _capi.load().insfm_ba_debug_stamps(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), max_steps)
         _capi.check(self._h, n)
         return out[:n]

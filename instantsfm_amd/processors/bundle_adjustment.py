@@ -248,14 +248,17 @@ def pack(cameras, images, tracks, options, native=True, phases=None):
                          remaining, pp_indices, track_vals)
 
 
-def update(cameras, images, tracks, packed, camera_params, points_3d):
-    """bundle_adjustment.py:18-36: write the optimized parameters back into the scene objects."""
+def update(cameras, images, tracks, packed, camera_params, points_3d, phases=None):
+    """bundle_adjustment.py:18-36: write the optimized parameters back into the scene objects.  ``phases`` (a dict)
+    gets the wall-time split: d2h (the device-to-host copies), xyz (every track's ``xyz`` set to its row), poses (the
+    pose matrices, ``world2cam`` per image, ``set_params`` per camera)."""
+    t0 = time.perf_counter()
     cp = camera_params.detach().cpu().numpy() if torch.is_tensor(camera_params) else np.asarray(camera_params)
     pts = points_3d.detach().cpu().numpy() if torch.is_tensor(points_3d) else np.asarray(points_3d)
+    t1 = time.perf_counter()
     full = np.zeros((cp.shape[0], cp.shape[1] + 2))
     full[:, packed.remaining_indices] = cp
     full[:, packed.pp_indices] = packed.camera_pps
-    mats = _pose_matrices(full[:, :7])
     keys = packed.track_keys
     if packx() is not None and pts.dtype == np.float64 and pts.flags.c_contiguous and pts.ndim == 2:
         packx().assign_xyz(list(tracks.values()) if packed.track_vals is None else packed.track_vals,
@@ -263,6 +266,8 @@ def update(cameras, images, tracks, packed, camera_params, points_3d):
     else:
         for orig, xyz in zip(packed.unique_points.tolist(), pts):
             tracks[keys[orig]].xyz = xyz
+    t2 = time.perf_counter()
+    mats = _pose_matrices(full[:, :7])
     last = {}
     for i, image_id in enumerate(packed.unique_cameras.tolist()):
         image = images[image_id]
@@ -270,6 +275,8 @@ def update(cameras, images, tracks, packed, camera_params, points_3d):
         last[image.cam_id] = i            # :33-36 set_params per image: the last image of a camera wins
     for cam_id, i in last.items():
         cameras[cam_id].set_params(full[i, 7:])
+    if phases is not None:
+        phases.update(d2h=t1 - t0, xyz=t2 - t1, poses=time.perf_counter() - t2)
 
 
 class TorchBA:
@@ -345,11 +352,13 @@ class TorchBA:
         t3 = time.perf_counter()
         self.final_loss, self.final_rmse = eng.cost(cams_t, pts_t)
         t3a = time.perf_counter()
-        update(cameras, images, tracks, packed, cams_t, pts_t)
+        wb = {}
+        update(cameras, images, tracks, packed, cams_t, pts_t, phases=wb)
         t3b = time.perf_counter()
         eng.close()
         t4 = time.perf_counter()
         self.timings.update(create_s=t2 - t1, steps_s=t3 - t2, update_s=t4 - t3, total_s=t4 - t0,
-                            update_phases=dict(cost=t3a - t3, write_back=t3b - t3a, close=t4 - t3b),
+                            update_phases=dict(cost=t3a - t3, write_back=t3b - t3a, close=t4 - t3b,
+                                               **{"write_back_" + k: v for k, v in wb.items()}),
                             steps=len(loss_history), final_rmse=self.final_rmse, step_ms=step_ms,
                             step_stats=step_stats)

@@ -23,6 +23,12 @@ S[gj]="gj|200|for m in 567 639 747; do tools/bench_dense_p5 \$m 30; tools/bench_
 S[ab_k]="ab_k|600|tools/ab_args.sh 2 --cluster-size=14 --cluster-size=12 --cluster-size=10 --cluster-size=16"
 S[sp]="sp|300|python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_default.log 2>&1; INSFM_DIAG=no_cgp python -u -m pytest tests/test_gpu_parity.py -q -k test_solve_parity --timeout 120 --timeout-method thread > $R/gpurun_out/sp_nocgp.log 2>&1; INSFM_DIAG=cgp_trace python -u -m pytest tests/test_gpu_parity.py -q -k \"test_solve_parity and 1-32-True-2\" -s --timeout 120 --timeout-method thread > $R/gpurun_out/sp_trace.log 2>&1; true"
 S[ab_prio]="ab_prio|400|tools/ab_env.sh 3 side_hi; tools/ab_env.sh 2 side_normal"
+S[ab_late]="ab_late|500|tools/ab_env.sh 3 late_chain"
+S[trace_late]="trace_late|240|cd /tmp && INSFM_DIAG=late_chain rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_late -o run -- python3 $R/bench.py --no-cpu --no-solve"
+S[tl]="tl|400|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k \"lagged or two_level or coarse or config3 or solve_parity\""
+S[gloo2]="gloo2|400|INSFM_DIST_BACKEND=gloo python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 > $R/gpurun_out/gloo2.json"
+S[pmc_cgp_f]="pmc_cgp_f|150|cd /tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_cgp_fetch -o run -- python3 $R/tools/cgp_pmc_probe.py > $R/gpurun_out/cgp_probe_fetch.json"
+S[pmc_cgp_w]="pmc_cgp_w|150|cd /tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_cgp_write -o run -- python3 $R/tools/cgp_pmc_probe.py > $R/gpurun_out/cgp_probe_write.json"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done

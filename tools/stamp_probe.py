@@ -1,16 +1,12 @@
 #!/usr/bin/env python3
-"""Tracer-free main-queue timeline of config-3 LM steps: INSFM_DIAG=stamps makes k_lin_points,
-k_schur, k_tl_cgp, k_cg_finish and k_publish record device-clock (100 MHz) entry / exit stamps; this prints, per step
-and as medians, the step span and the regions between the stamped kernels:
-
-  lin        k_lin_points                          boundary   k_publish exit -> next k_lin_points entry
-  lin>schur  k_lin_points exit -> k_schur entry     schur      k_schur
-  pre-CG     k_schur exit -> k_tl_cgp entry (k_cg_factor, [k_cg_scale], k_tl_basis, dispatch)
-  cgp        k_tl_cgp                              post-CG    k_tl_cgp exit -> k_cg_finish entry
-  tail       k_cg_finish entry -> k_publish exit (back-substitution, cost, k_final, k_publish)
-
-The gaps are measured without a tracer; the kernels inside pre-CG and tail are not stamped (their busy time is the
-sum of their standalone durations).  The unstamped rate of the same run is printed beside.
+"""Tracer-free main-queue timeline of config-3 LM steps: INSFM_DIAG=stamps makes the main-queue
+kernels of a step -- k_lin_points, k_schur, k_cg_factor, k_tl_basis, k_tl_cgp, k_cg_finish, k_backsub_rc, k_cost,
+k_final, k_publish -- record device-clock (100 MHz) entry / exit stamps (engine.STAMP_KERNELS); this prints, per step
+and as medians, the step span (k_lin_points entry to the next one), each kernel's duration, the main queue's busy
+time (the sum of the stamped kernels: the kernels a lagged trial runs on the main queue are all stamped) and the
+gaps between consecutive kernels.  Steps with more than one trial (a rejected trial relaunches k_schur .. k_publish,
+and the stamps keep the last launch) are left out of the medians.  The stamped run's wall time per step is printed
+beside (each stamped kernel's workgroups add one atomic; bench.py gives the unstamped rate).
 
     INSFM_DIAG=stamps python tools/stamp_probe.py [--steps 20] [--warmup 3]
 """
@@ -25,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from instantsfm_amd.engine import BundleAdjuster  # noqa: E402
+from instantsfm_amd.engine import STAMP_KERNELS, BundleAdjuster  # noqa: E402
 from instantsfm_amd.synth import make_config  # noqa: E402
 
 
@@ -49,28 +45,48 @@ def main():
     pts.copy_(p0)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    iters = []
+    iters, trials = [], []
     for _ in range(a.steps):
-        iters.append(eng.step(cams, pts)[1]["pcg_iters"])
+        stt = eng.step(cams, pts)[1]
+        iters.append(stt["pcg_iters"])
+        trials.append(stt["trials"])
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / a.steps * 1e3
     st = eng.debug_stamps()[-a.steps:].astype(np.float64) / 100.0  # microseconds
-    LIN, SCH, CGP, FIN, PUB = range(5)
+    names = list(STAMP_KERNELS)
+    order = ["k_lin_points", "k_schur", "k_cg_factor", "k_tl_basis", "k_tl_cgp", "k_cg_finish", "k_backsub_rc",
+             "k_cost", "k_final", "k_publish"]
+    ix = [names.index(n) for n in order]
     rows = []
     for k in range(len(st) - 1):
         s, n = st[k], st[k + 1]
-        r = {"span": n[LIN, 0] - s[LIN, 0], "lin": s[LIN, 1] - s[LIN, 0], "lin>schur": s[SCH, 0] - s[LIN, 1],
-             "schur": s[SCH, 1] - s[SCH, 0], "pre-CG": s[CGP, 0] - s[SCH, 1], "cgp": s[CGP, 1] - s[CGP, 0],
-             "post-CG": s[FIN, 0] - s[CGP, 1], "tail": s[PUB, 1] - s[FIN, 0], "boundary": n[LIN, 0] - s[PUB, 1],
-             "pcg": iters[k]}
+        t0, t1 = s[ix[0], 0], n[ix[0], 0]
+        r = {"span": t1 - t0, "trials": trials[k], "pcg": iters[k]}
+        busy, prev_end = 0.0, None
+        for name, i in zip(order, ix):
+            b, e = s[i]
+            if not (t0 <= b < t1):  # not launched in this step
+                r[name] = float("nan")
+                continue
+            r[name] = e - b
+            busy += e - b
+            if prev_end is not None:
+                r["gap>" + name] = b - prev_end
+            prev_end = e
+        r["gap>next"] = t1 - prev_end
+        r["busy"] = busy
+        r["busy_frac"] = busy / r["span"]
         rows.append(r)
-        print(f"step {k:2d}: " + " ".join(f"{q} {v:.1f}" if q != "pcg" else f"pcg {v}" for q, v in r.items()),
+        print(f"step {k:2d}: " + " ".join(f"{q} {v:.1f}" if isinstance(v, float) else f"{q} {v}" for q, v in r.items()),
               flush=True)
-    med = {q: float(np.median([r[q] for r in rows])) for q in rows[0] if q != "pcg"}
-    stamped = sum(med[q] for q in ("lin", "schur", "cgp"))
-    print(json.dumps({"wall_ms_per_step_stamped_run": round(wall, 4), "median_us": {q: round(v, 2) for q, v in med.items()},
-                      "stamped_kernels_busy_frac": round(stamped / med["span"], 4),
-                      "gaps_us": {q: round(med[q], 2) for q in ("lin>schur", "post-CG", "boundary")}}), flush=True)
+    keep = [r for r in rows if r["trials"] == 1]
+    keys = [q for q in rows[0] if q not in ("trials", "pcg")]
+    med = {q: float(np.nanmedian([r.get(q, np.nan) for r in keep])) for q in keys}
+    gaps = {q: round(v, 2) for q, v in med.items() if q.startswith("gap>")}
+    print(json.dumps({"wall_ms_per_step_stamped_run": round(wall, 4),
+                      "steps_used": len(keep), "median_us": {q: round(v, 2) for q, v in med.items()},
+                      "main_queue_busy_frac_median": round(med["busy_frac"], 4),
+                      "gaps_us_median": gaps, "gaps_us_sum_of_medians": round(sum(gaps.values()), 2)}), flush=True)
     eng.close()
 
 
