@@ -29,6 +29,10 @@ S[tl]="tl|400|python -u -m pytest -x -q --timeout 120 --timeout-method thread te
 S[gloo2]="gloo2|400|INSFM_DIST_BACKEND=gloo python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 > $R/gpurun_out/gloo2.json"
 S[pmc_cgp_f]="pmc_cgp_f|150|cd /tmp && rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/gpurun_out/pmc_cgp_fetch -o run -- python3 $R/tools/cgp_pmc_probe.py > $R/gpurun_out/cgp_probe_fetch.json"
 S[pmc_cgp_w]="pmc_cgp_w|150|cd /tmp && rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/gpurun_out/pmc_cgp_write -o run -- python3 $R/tools/cgp_pmc_probe.py > $R/gpurun_out/cgp_probe_write.json"
+S[par]="par|600|python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py"
+S[ab_rd]="ab_rd|500|tools/ab_env.sh 3 schur_y"
+S[rdq]="rdq|300|INSFM_DIAG=create python -u bench.py --no-cpu --no-solve > $R/gpurun_out/rdq.json 2> $R/gpurun_out/rdq.err; grep -h 'Schur build' $R/gpurun_out/rdq.err; python3 -c \"import json; d=json.loads([l for l in open('$R/gpurun_out/rdq.json') if l.startswith('{')][-1]); print(d['value'], d['kernel_us'], d['phase_ms_per_step'])\""
+S[ab_cu]="ab_cu|600|tools/ab_env.sh 2 side_cu16 && tools/ab_env.sh 2 side_cu32 && tools/ab_env.sh 2 side_cu64"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done
