@@ -185,6 +185,7 @@ __device__ __forceinline__ double uni(double v) {
 // counted so far (one per iteration of earlier launches); oseg bit 0: also write this solve's coarse segments tl.Oseg
 // (the E build behind the CG then skips k_tl_erow), bit 1 (tests, INSFM_DIAG=cgp_fault): the last workgroup leaves
 // at iteration 2 as if a barrier had timed out;
+// dcout (non-null): the camera step dc = L^-T x~ written at the end (k_cg_finish's arithmetic);
 // trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
 // of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
 // barriers (workgroup 0).
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                                                           const double* __restrict__ Einv, int maxit, double tol2_rel,
                                                           double* wx, unsigned long long* yg, unsigned tag0,
                                                           unsigned* sync, unsigned epoch0, int oseg, double* runs,
-                                                          double* trace, long long* stp) {
+                                                          double* trace, double* __restrict__ dcout, long long* stp) {
     static_assert(NB % 8 == 0, "k_tl_cgp gathers eight blocks per load instruction");
     const StampScope stamp_(stp);
     constexpr int D = 8, MC = 9, BS = D * MC, LPL = (kCoarseMax + 63) / 64, LNC = (kCoarseMax / MC + 63) / 64;
@@ -901,6 +902,13 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         double* dst = lane < 8 ? cg.r[0] : lane < 16 ? tl.u : lane < 24 ? cg.w[0] : lane < 32 ? cg.w[1]
                     : lane < 40 ? cg.r[1] : lane < 48 ? cg.s[0] : lane < 56 ? cg.p : cg.x;
         dst[own] = V[lane];
+        // (round 5) the camera step dc_i = L_i^-T x~_i in k_cg_finish's order of additions, so that launch and its
+        // gap are gone from the solve's tail
+        if (dcout && lane < D) {
+            double sdc = 0.0;
+            for (int q = lane; q < D; ++q) sdc += Lirow[rl][q * D + lane] * V[VX + q];
+            dcout[(size_t)row * D + lane] = sdc;
+        }
     }
 }
 

@@ -1597,6 +1597,7 @@ struct insfm_ba {
     int cgp_slots = 0;            // workgroups of k_tl_cgp the device holds at once
     bool cg_async = false;        // lm_step: a k_tl_cgp solve's status is read after the trial's k_publish
     bool cgp_pending = false;     // a k_tl_cgp launch whose status the host has not read yet (cgp_complete)
+    bool dc_by_cgp = false;       // this solve's k_tl_cgp writes dc itself (cg_tail launches no k_cg_finish)
     bool cgp_lost = false;        // the last k_tl_cgp timed out at a grid barrier (another process holds CUs)
     double* cgp_trace = nullptr;  // INSFM_DIAG=cgp_trace: [64][4] of the last solve, printed to stderr
     // row-partitioned multi-rank CG (ba_xpart.h; insfm_ba_cg_window / insfm_ba_cg_attach)
@@ -2326,7 +2327,7 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
         hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->S,
                            h->cgp_src, h->Li, h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
                            h->cgp_tag, h->cgp_sync,
-                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace,
+                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace, h->dc,
                            stamp_ptr(h, kStCgp));
     };
     if (h->cgp_det) {
@@ -2441,6 +2442,7 @@ int cgp_complete(insfm_ba* h, int* st) {
 // convergence exit at the device status flag.  Returns 0 with st[0..2] = {status, iterations, coarse used}.
 int run_tl_cg(insfm_ba* h, int* st) {
     const int D = h->D, maxit = h->d.pcg_max_iter;
+    h->dc_by_cgp = h->cgp_nb != 0;
     const double tol2 = h->d.pcg_tol * h->d.pcg_tol;
     volatile int* pg = h->prog_host;
     pg[0] = pg[1] = pg[2] = pg[3] = 0;
@@ -2624,6 +2626,7 @@ int cg_tail(insfm_ba* h, int* st) {
             return INSFM_BA_EHIP;
         }
     }
+    if (h->dc_by_cgp) return h->cgp_pending ? 0 : st[1];  // (k_tl_cgp wrote dc; an abort's launch-path repeat clears it)
     rc = with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
         k_cg_finish<DV><<<cdiv((long long)h->C * DV, kThreads), kThreads, 0, h->stream>>>(h->C, h->Li, h->cg.x,
