@@ -34,6 +34,7 @@ S[ab_rd]="ab_rd|500|tools/ab_env.sh 3 schur_y"
 S[rdq]="rdq|300|INSFM_DIAG=create python -u bench.py --no-cpu --no-solve > $R/gpurun_out/rdq.json 2> $R/gpurun_out/rdq.err; grep -h 'Schur build' $R/gpurun_out/rdq.err; python3 -c \"import json; d=json.loads([l for l in open('$R/gpurun_out/rdq.json') if l.startswith('{')][-1]); print(d['value'], d['kernel_us'], d['phase_ms_per_step'])\""
 S[ab_cu]="ab_cu|600|tools/ab_env.sh 2 side_cu16 && tools/ab_env.sh 2 side_cu32 && tools/ab_env.sh 2 side_cu64"
 S[ab_fork]="ab_fork|500|tools/ab_env.sh 4 lin_fork_early"
+S[benchdef]="benchdef|400|python -u bench.py > $R/gpurun_out/bench_default.json"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done
