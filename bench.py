@@ -178,7 +178,7 @@ def run_gp(args):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     final_loss, rmse = eng.cost(*par)
-    tl = args.precond == 1
+    tl = args.precond >= 1
     us_cg = eng.debug_time_kernel(3 if tl else 0, 100)
     us_schur = eng.debug_time_kernel(1, 5)
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, 3
@@ -653,7 +653,7 @@ def main():
     ap.add_argument("--no-solve", action="store_true", help="skip the end-to-end TorchBA.Solve split")
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
-    ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 0 block-Jacobi (the reference's)")
+    ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 2 two-level with the A-DEF2 coarse correction, 0 block-Jacobi (the reference's)")
     ap.add_argument("--cluster-size", type=int, default=14, help="two-level: target cameras per coarse cluster")
     ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes", "mapper"), default="ba")
     ap.add_argument("--mapper-images", type=int, default=500, help="--path mapper: images in the database")
@@ -750,7 +750,7 @@ def main():
         if conv_step is not None and k + 1 == conv_step:
             rmse_conv = eng.cost(ci, pi)[1]
     eng.set_timing(False)
-    tl = args.precond == 1
+    tl = args.precond >= 1
     C, P, N, D = prob.n_cams, prob.n_points, prob.n_obs, eng.D
     Pl = shards[rank][1] - shards[rank][0]
     Nl = int(np.sum((prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])))

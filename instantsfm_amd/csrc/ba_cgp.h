@@ -191,7 +191,7 @@ __device__ __forceinline__ double uni(double v) {
 // barriers (workgroup 0).
 constexpr int kCgpPadSlot = INT_MIN;  // ssrc of a pad slot (a zero block)
 
-template <int NB, bool DET>
+template <int NB, bool DET, bool ADEF = false>
 __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __restrict__ nbr_ptr,
                                                           const int* __restrict__ nbr_j, const double* __restrict__ S,
                                                           const int* __restrict__ ssrc, const double* __restrict__ Li,
@@ -224,6 +224,8 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     __shared__ double prt[kCgpRows][12];               // each row's partials: r.u, w.u, ||L r||^2, Z~_i^T w (9)
     __shared__ int pcl[kCgpRows];                      // each row's cluster (-1: no row)
     __shared__ int bflag;
+    __shared__ double dvec[kCgpRows][D];               // ADEF: each row's d = -(off-diagonal part of S~ v)
+    static_assert(!(DET && ADEF), "A-DEF2 runs in the atomic (single-rank) form only");
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (wave-uniform: the row's values live in SGPRs)
     const int a8 = lane >> 3, b8 = lane & 7;           // block entry (a, b) of this lane
@@ -408,6 +410,218 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             }
         }
     }
+    if constexpr (ADEF) {
+        // ---- A-DEF2 setup (precond 2; oracle/ba_oracle.c adef2_apply): x0 = Z~ E^-1 R(r0) and r0' = r0 - S~ x0 without
+        // an exchange (S~ Z~ = A is this row's B segments scaled by L_i^-1); then d0 = -(the off-diagonal part of
+        // S~ r0') from the neighbours' r0' (one exchange), its restriction summed per cluster (atomic buffer 2), y0' =
+        // E^-1 R(d0), u0 = r0' + Z~ y0' and w0 = S~ u0 = r0' + off(S~ r0') + Z~ y0' + A y0' again without an exchange.
+        // Three grid barriers; the coarse solves under the setup tags tag0 + maxit + 1 and + 2.
+        for (int q = blockIdx.x * kCgpThreads + t; q < 3 * m + 2 * 3 * nc; q += gridDim.x * kCgpThreads)
+            st_sc1(q < 3 * m ? tl.Racc + q : tl.Gacc + (q - 3 * m), 0.0);
+        if (blockIdx.x == 0 && t == 0) {
+            cg.status[2] = use ? 1 : 0;  // reported as insfm_ba_stats.coarse_used
+            if (cg.prog) __hip_atomic_store(cg.prog + 3, use ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        // coarse rows of y = E^-1 R (R in rs, LDS) published under `tag`, then collected by every workgroup into ys
+        // (the E^-1 row loaded here each time: held across the setup's products it pushed the kernel into spills)
+        auto coarse_solve = [&](unsigned tag) -> bool {
+            if (gw < m) {
+                double ev[LPL];
+#pragma unroll
+                for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
+                double rq[LPL];
+#pragma unroll
+                for (int q = 0; q < LPL; ++q) rq[q] = rs[min(lane + 64 * q, m - 1)];
+                __builtin_amdgcn_sched_barrier(0);
+                double sy = 0.0;
+#pragma unroll
+                for (int q = 0; q < LPL; ++q)
+                    if (lane + 64 * q < m) sy += ev[q] * rq[q];
+                const double y = wave_sum(sy);
+                if (lane == 0) put_y(yg, gw, tag, y);
+            }
+            for (int g = gw + gridDim.x * kCgpWaves; g < m; g += gridDim.x * kCgpWaves) {
+                const double* er = Einv + (size_t)g * m;
+                double sy = 0.0;
+                for (int l = lane; l < m; l += 64) sy += er[l] * rs[l];
+                const double y = wave_sum(sy);
+                if (lane == 0) put_y(yg, g, tag, y);
+            }
+            return get_y(yg, ys, m, tag, sync);
+        };
+        // row a8's sum over the segments of B_ic y_c (lane (a, j): segments j, j + 8, ...), then over j
+        auto seg_ay = [&]() -> double {
+            double ay = 0.0;
+            const int ns = min(nseg, kCgpSegMax);
+            for (int sg = b8; sg < ns; sg += 8) {
+                const double* yc = ys + segc[rl][sg] * MC;
+                const double* A = &Aseg[rl][sg][a8 * MC];
+                double a9[MC], c9[MC];
+#pragma unroll
+                for (int k = 0; k < MC; ++k) { a9[k] = A[k]; c9[k] = yc[k]; }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < MC; ++k) ay += a9[k] * c9[k];
+            }
+            ay += __shfl_xor(ay, 1, 64);
+            ay += __shfl_xor(ay, 2, 64);
+            ay += __shfl_xor(ay, 4, 64);
+            return ay;
+        };
+        auto zy_entry = [&](int la) -> double {  // (Z~_i y_ci)[la]
+            double z9[MC], y9[MC];
+#pragma unroll
+            for (int k = 0; k < MC; ++k) { z9[k] = Zrow[rl][la * MC + k]; y9[k] = ys[ci * MC + k]; }
+            __builtin_amdgcn_sched_barrier(0);
+            double sz = 0.0;
+#pragma unroll
+            for (int k = 0; k < MC; ++k) sz += z9[k] * y9[k];
+            return sz;
+        };
+        const unsigned tag_s = tag0 + (unsigned)maxit + 1u, tag_s2 = tag0 + (unsigned)maxit + 2u;
+        const int la = lane & 7;
+        // x0, r0'
+        if (use) {
+            double rv[RPT];
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) rv[q] = tl.Rc[min(t + q * kCgpThreads, m - 1)];
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+            __syncthreads();
+            if (!coarse_solve(tag_s)) alive = false;
+        }
+        if (alive && has_row) {
+            double x0 = 0.0, sx = 0.0;
+            if (use) {
+                x0 = zy_entry(la);
+                sx = lscale(seg_ay());  // entry la of off(S~) x0 = L_i^-1 sum_c B_ic y0_c
+            }
+            const double r0p = V[VR + la] - x0 - sx;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane < D) { V[VR + la] = r0p; V[VX + la] = x0; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const double v0 = ltscale(V[VR + a8]);  // the neighbours read L_i^-T r0'
+            if (lane < D) st_sc1(wx + (size_t)C * D + (size_t)row * D + lane, v0);
+        }
+        if (alive) alive = cgp_barrier(sync, ++epoch, &bflag);
+        // d0 = -off(S~ r0') and its restriction
+        double off0 = 0.0;
+        if (alive) {
+            double uv8[NG];
+            {
+                int jr[NG];
+#pragma unroll
+                for (int g = 0; g < NG; ++g) jr[g] = jn[wv][8 * g + a8];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < NG; ++g) uv8[g] = ld_sc1(wx + (size_t)C * D + (size_t)jr[g] * D + b8);
+            }
+#pragma unroll
+            for (int g = 0; g < NG; ++g) wg[wv][8 * g + a8][b8] = uv8[g];
+            __syncthreads();
+            if (has_row) {
+                double ac4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int k0 = 0; k0 < NB; k0 += 16) {
+                    double w16[16];
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) w16[c] = wg[wv][k0 + c][b8];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) ac4[c & 3] += sreg[k0 + c] * w16[c];
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                double acc = (ac4[0] + ac4[1]) + (ac4[2] + ac4[3]);
+                acc += __shfl_xor(acc, 1, 64);
+                acc += __shfl_xor(acc, 2, 64);
+                acc += __shfl_xor(acc, 4, 64);
+                off0 = lscale(acc);
+                if (lane < D) dvec[rl][lane] = -off0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < MC) {
+                    double d8[D], z8[D];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) { d8[a] = dvec[rl][a]; z8[a] = Zrow[rl][a * MC + lane]; }
+                    __builtin_amdgcn_sched_barrier(0);
+                    double rr = 0.0;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) rr += z8[a] * d8[a];
+                    prt[rl][3 + lane] = rr;
+                }
+            }
+            __syncthreads();
+            if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane >= 3 && lane < 3 + MC) {
+                double v = prt[rl][lane];
+                for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
+                unsafeAtomicAdd(tl.Racc + (size_t)2 * m + (size_t)ci * MC + (lane - 3), v);
+            }
+            alive = cgp_barrier(sync, ++epoch, &bflag);
+        }
+        // u0, w0 and the partials of iteration 0
+        if (alive) {
+            if (use) {
+                double rv[RPT];
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) rv[q] = ld_sc1(tl.Racc + (size_t)2 * m + min(t + q * kCgpThreads, m - 1));
+#pragma unroll
+                for (int q = 0; q < RPT; ++q)
+                    if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+                __syncthreads();
+                if (!coarse_solve(tag_s2)) alive = false;
+            }
+            if (alive && has_row) {
+                double zy = 0.0, sa = 0.0;
+                if (use) {
+                    zy = zy_entry(la);
+                    sa = lscale(seg_ay());
+                }
+                const double r0p = V[VR + la];
+                const double u0 = r0p + zy;
+                const double w0 = r0p + off0 + zy + sa;  // S~ u0 (the diagonal block of S~ is I)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < D) { V[VU + la] = u0; V[VW + la] = w0; V[VZ + la] = 0.0; V[VQ + la] = 0.0; }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+                {
+                    double l8[D], r8[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) { l8[k] = Lrow[rl][la * D + k]; r8[k] = V[VR + k]; }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (lane < D) {
+                        g0 = r0p * u0;
+                        g1 = w0 * u0;
+                        double lr = 0.0;
+#pragma unroll
+                        for (int k = 0; k < D; ++k)
+                            if (k <= lane) lr += l8[k] * r8[k];
+                        g2 = lr * lr;
+                    }
+                    const double v0 = ltscale(V[VW + a8]);  // the neighbours read L_i^-T w0
+                    if (lane < D) st_sc1(wx + (size_t)row * D + lane, v0);
+                }
+                wave_sum3(g0, g1, g2);
+                if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
+            }
+            __syncthreads();
+            if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3) {
+                double v = prt[rl][lane];
+                for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
+                unsafeAtomicAdd(tl.Gacc + (size_t)lane * nc + ci, v);
+            }
+            alive = cgp_barrier(sync, ++epoch, &bflag);
+        }
+    } else {
     // ---- u0 = M~^-1 r0 (round 5: k_tl_pc's setup launch folded in; config 3 saved its 10-us launch and the gap
     // in front of it).  The restriction R(r0): every workgroup sums k_tl_basis's row partials of each cluster itself,
     // rows in cluster order (k_tl_pc's order, so the same doubles); the wave's own cluster's rows of y0 = E^-1 R
@@ -576,6 +790,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
         alive = cgp_barrier(sync, ++epoch, &bflag);
     }
+    }  // (ADEF)
     if (trace && blockIdx.x == 0 && t == 0) {
         trace[256] = (double)t_start;
         trace[257] = (double)wall_clock64();
@@ -654,9 +869,9 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         const double* Rv = tl.Racc + (size_t)b0 * m;
         double rv[RPT];
 #pragma unroll
-        for (int q = 0; q < RPT; ++q) rv[q] = (use && !DET) ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
+        for (int q = 0; q < RPT; ++q) rv[q] = (use && !DET && !ADEF) ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
         double ev[LPL];
-        if (use && gw < m) {
+        if (!ADEF && use && gw < m) {  // (A-DEF2: loaded with the restriction after the mid-phase barrier)
 #pragma unroll
             for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
         }
@@ -712,15 +927,15 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         }
 #pragma unroll
         for (int g = 0; g < NG; ++g) wg[wv][8 * g + a8][b8] = wv8[g];
-        if (use && !DET) {
+        if (use && !DET && !ADEF) {
 #pragma unroll
             for (int q = 0; q < RPT; ++q)
                 if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
         }
         __syncthreads();
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[580 + 3 * it] = (double)wall_clock64();
-        // coarse row gw: y = E^-1 R (k_tl_pc_cl's products and butterfly)
-        if (use && gw < m) {
+        // coarse row gw: y = E^-1 R (k_tl_pc_cl's products and butterfly; A-DEF2: after the restriction below)
+        if (!ADEF && use && gw < m) {
             double rq[LPL];
 #pragma unroll
             for (int q = 0; q < LPL; ++q) {  // (DET: entry k of R is record k / 9's value 3 + k % 9)
@@ -736,7 +951,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (lane == 0) put_y(yg, gw, tag0 + (unsigned)it, y);
         }
         // more coarse rows than waves (small grids): the rest, E^-1 rows loaded here
-        for (int g = gw + gridDim.x * kCgpWaves; use && g < m; g += gridDim.x * kCgpWaves) {
+        for (int g = gw + gridDim.x * kCgpWaves; !ADEF && use && g < m; g += gridDim.x * kCgpWaves) {
             const double* er = Einv + (size_t)g * m;
             double sy = 0.0;
             for (int l = lane; l < m; l += 64) sy += er[l] * rs[DET ? (l / 9) * 12 + 3 + l % 9 : l];
@@ -765,6 +980,66 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             acc += __shfl_xor(acc, 2, 64);
             acc += __shfl_xor(acc, 4, 64);
             sw = acc;  // row a8's sum_j S_ij v_j, unscaled (L_i^-1 is applied with the coarse part in P2)
+        }
+        if constexpr (ADEF) {
+            // A-DEF2: y = E^-1 Z~^T d, d = w - S~ w = -L_i^-1 sum_j S_ij v_j: the row's restriction of d, summed per
+            // cluster run and added to atomic buffer `b0`, one grid barrier, then the coarse rows of y
+            if (has_row) {
+                const double dneg = lscale(sw);
+                if (lane < D) dvec[rl][lane] = -dneg;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane < MC) {
+                    double d8[D], z8[D];
+#pragma unroll
+                    for (int a = 0; a < D; ++a) { d8[a] = dvec[rl][a]; z8[a] = Zrow[rl][a * MC + lane]; }
+                    __builtin_amdgcn_sched_barrier(0);
+                    double rr = 0.0;
+#pragma unroll
+                    for (int a = 0; a < D; ++a) rr += z8[a] * d8[a];
+                    prt[rl][3 + lane] = rr;
+                }
+            }
+            __syncthreads();
+            if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane >= 3 && lane < 3 + MC) {
+                double v = prt[rl][lane];
+                for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
+                unsafeAtomicAdd(tl.Racc + (size_t)b0 * m + (size_t)ci * MC + (lane - 3), v);
+            }
+            if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
+            if (use) {
+                double rq0[RPT];
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) rq0[q] = ld_sc1(Rv + min(t + q * kCgpThreads, m - 1));
+                if (gw < m) {
+#pragma unroll
+                    for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
+                }
+#pragma unroll
+                for (int q = 0; q < RPT; ++q)
+                    if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rq0[q];
+                __syncthreads();
+                if (gw < m) {
+                    double rq[LPL];
+#pragma unroll
+                    for (int q = 0; q < LPL; ++q) rq[q] = rs[min(lane + 64 * q, m - 1)];
+                    __builtin_amdgcn_sched_barrier(0);
+                    double sy = 0.0;
+#pragma unroll
+                    for (int q = 0; q < LPL; ++q)
+                        if (lane + 64 * q < m) sy += ev[q] * rq[q];
+                    const double y = wave_sum(sy);
+                    if (lane == 0) put_y(yg, gw, tag0 + (unsigned)it, y);
+                }
+                for (int g = gw + gridDim.x * kCgpWaves; g < m; g += gridDim.x * kCgpWaves) {
+                    const double* er = Einv + (size_t)g * m;
+                    double sy = 0.0;
+                    for (int l = lane; l < m; l += 64) sy += er[l] * rs[l];
+                    const double y = wave_sum(sy);
+                    if (lane == 0) put_y(yg, g, tag0 + (unsigned)it, y);
+                }
+            }
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) trace[322 + 4 * it + 0] = (double)wall_clock64();
         // ======== P2 ========
@@ -857,21 +1132,21 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                         if (k <= lane) lr += l8[k] * r8[k];
                     g2 = lr * lr;
                 }
-                if (lane < MC) {
+                if (!ADEF && lane < MC) {
 #pragma unroll
                     for (int a = 0; a < D; ++a) rr += z8[a] * w8[a];
                 }
             }
             wave_sum3(g0, g1, g2);
             if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
-            if (lane < MC) prt[rl][3 + lane] = rr;
+            if (!ADEF && lane < MC) prt[rl][3 + lane] = rr;
         }
         // DET: every wave's w stores complete before its run's partials are published (the consumers read w once they
         // hold every cluster's sums of the next iteration)
         if constexpr (DET) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // the first row of each cluster run of the workgroup adds the run's partials (rows in order) to the cluster
-        if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3 + MC) {
+        if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < (ADEF ? 3 : 3 + MC)) {
             double v = prt[rl][lane];
             for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
             if constexpr (DET) {

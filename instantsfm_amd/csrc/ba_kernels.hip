@@ -1587,6 +1587,7 @@ struct insfm_ba {
     // issued behind the CG (k_tl_cgp holds every SIMD of its CUs, so a chain beside it would crawl on the rest)
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
     bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
+    bool adef2 = false;                  // precond 2: k_tl_cgp applies the coarse correction as A-DEF2 (ba_cgp.h)
     double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
     int* cgp_src = nullptr;     // [n_nbr] S block of each CG slot: e (upper), ~e (lower, transposed), INT_MIN (pad)
     bool sn_valid = false;      // Sn holds the scaled S~ of the current solve (k_cg_scale ran for it)
@@ -2333,6 +2334,9 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     if (h->cgp_det) {
         if (h->cgp_nb == 64) go(k_tl_cgp<64, true>);
         else go(k_tl_cgp<128, true>);
+    } else if (h->adef2) {
+        if (h->cgp_nb == 64) go(k_tl_cgp<64, false, true>);
+        else go(k_tl_cgp<128, false, true>);
     } else {
         if (h->cgp_nb == 64) go(k_tl_cgp<64, false>);
         else go(k_tl_cgp<128, false>);
@@ -2378,7 +2382,8 @@ int cgp_complete(insfm_ba* h, int* st) {
     st[0] = pg[1]; st[1] = pg[2]; st[2] = pg[3];
     {  // the barriers this launch counted: one per completed iteration; an abort restarts the counters
         if (st[0] == 1 || st[0] == 2) {
-            h->cgp_epochs += (unsigned)st[1] + 2u;  // (the setup's two barriers and one per completed iteration)
+            // (the setup's two barriers and one per completed iteration; A-DEF2: three and two)
+            h->cgp_epochs += h->adef2 ? 2u * (unsigned)st[1] + 3u : (unsigned)st[1] + 2u;
         } else {
             HIPCHK(hipStreamSynchronize(h->stream));
             HIPCHK(hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream));
@@ -2475,7 +2480,7 @@ int run_tl_cg(insfm_ba* h, int* st) {
     int enq = std::min(std::max(kCgAhead + 2, h->last_cg_iters - CG_INIT_BACK), maxit + 2);
     if (h->cgp_nb) enq = maxit + 2;  // k_tl_cgp: one launch runs every iteration
     if (int rc = enqueue(0, enq)) return rc;
-    if (h->cgp_nb) h->cgp_tag += (unsigned)maxit + 2u;  // (the tags of this launch are never reused)
+    if (h->cgp_nb) h->cgp_tag += (unsigned)maxit + 3u;  // (the tags of this launch are never reused)
     if (h->cgp_defer) {  // the side chain of this solve behind the CG (run_tl_setup), from k_tl_cgp's segments
         // (INSFM_DIAG=chain_hold, timing only: no lagged chain at all -- later solves keep an older coarse inverse --
         // to measure what the chain's overlap costs the kernels it runs beside)
@@ -3485,7 +3490,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         }
     }
     tick("block pattern + covisibility");
-    if (desc->precond != 0 && desc->precond != 1) return fail(INSFM_BA_EINVAL, "precond must be 0 or 1");
+    if (desc->precond < 0 || desc->precond > 2) return fail(INSFM_BA_EINVAL, "precond must be 0, 1 or 2");
     // ---- two-level preconditioner: clusters ----
     // Target cluster size 14 by default (config 3, same box, 3 x 3 runs: K = 16 / 14 / 12 -> 703-711 / 716-720 /
     // 713-720 LM it/s, CG iterations per 10 steps 225 / 213 / 208; profiles/r3_v10/cluster_size_probe_*.log).
@@ -3498,7 +3503,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     int nc = 0;
     bool coarse_ok = false;
     std::vector<int>& lab = h->clab_host;
-    if (desc->precond == 1 && h->d.optimize_poses) {
+    if (desc->precond >= 1 && h->d.optimize_poses) {
         int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 14, C);
         nc = aggregate(g, C, K, lab);
         while (nc * MC > kCoarseMax && K < C) {
@@ -4014,6 +4019,8 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                     if ((rc = dd(&tl.Gb, cd * MC))) return fail(rc, "");
                 }
                 h->cgp_det = det;
+                // precond 2 (A-DEF2) runs in the atomic k_tl_cgp only; elsewhere the additive form of precond 1
+                h->adef2 = desc->precond == 2 && !det;
                 h->cgp_nb = nb;
                 h->cgp_grid = grid;
                 h->cgp_slots = per_cu * ncu;
@@ -4078,7 +4085,7 @@ int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks) {
 
 int insfm_ba_cg_info(const insfm_ba* h, int32_t* out) {
     if (!h || !out) return INSFM_BA_EINVAL;
-    out[0] = h->xpart ? 3 : h->cgp_nb ? (h->cgp_det ? 2 : 1) : 0;
+    out[0] = h->xpart ? 3 : h->cgp_nb ? (h->cgp_det ? 2 : (h->adef2 ? 4 : 1)) : 0;
     out[1] = h->cgp_grid;
     out[2] = h->cgp_slots;
     out[3] = h->cgp_nb;
@@ -4430,7 +4437,7 @@ int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out) {
         HIPCHK(hipEventRecord(h->ev[10], h->stream));
         if (int rc2 = launch_tl_cgp(h, maxit, tol2)) { h->cgp_defer = false; return rc2; }
         h->cgp_defer = false;
-        h->cgp_tag += (unsigned)maxit + 2u;
+        h->cgp_tag += (unsigned)maxit + 3u;
         HIPCHK(hipEventRecord(h->ev[11], h->stream));
         HIPCHK(hipEventSynchronize(h->ev[11]));
         int st[3];

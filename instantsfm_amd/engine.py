@@ -23,7 +23,8 @@ LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0
 STAMP_KERNELS = ("k_lin_points", "k_schur", "k_tl_cgp", "k_cg_finish", "k_publish", "k_cg_factor", "k_tl_basis",
                  "k_backsub_rc", "k_cost", "k_final")
 CG_PATHS = {0: "launch-per-iteration two-level CG", 1: "k_tl_cgp (persistent, atomic cluster sums)",
-            2: "k_tl_cgp (persistent, fixed-order)", 3: "row-partitioned CG"}
+            2: "k_tl_cgp (persistent, fixed-order)", 3: "row-partitioned CG",
+            4: "k_tl_cgp (persistent, atomic cluster sums, A-DEF2 coarse correction: precond 2)"}
 
 
 def device_key(device):

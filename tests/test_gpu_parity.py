@@ -554,3 +554,29 @@ def test_clusters_match_oracle_when_the_cap_grows_the_target(K):
     assert ng == no and np.array_equal(lg, lo)
     assert ng * 17 <= 768 and np.bincount(lo).min() >= 2
     eng.close()
+
+
+@pytest.mark.parametrize("cfg,steps", [(2, 4), (3, 10)])
+def test_adef2_coarse_correction_matches_oracle(cfg, steps):
+    """precond 2: k_tl_cgp applies the coarse correction as A-DEF2 (M~^-1 r = r + Z~ E^-1 Z~^T (r - S~ r), started from
+    the coarse solution x0 = Z~ E^-1 Z~^T r0; oracle/ba_oracle.c adef2_apply) against the oracle's precond 2: PCG
+    iterations per step within one (the k_tl_cgp form sums S~ x, S~ Z~ y and the restrictions in another order),
+    losses 1e-8 relative, and about half the iterations of the additive form on config 3 (oracle: 213 -> 111 over
+    10 steps)."""
+    prob = make_config(cfg)
+    eng, ora = engines(prob, precond=2)
+    assert eng.cg_info()[0] == 4, eng.cg_info()  # the A-DEF2 k_tl_cgp ran
+    cg, pg = dev(prob.cams_init), dev(prob.points_init)
+    co, po = prob.cams_init.copy(), prob.points_init.copy()
+    it_g, it_o = [], []
+    for s in range(steps):
+        lg, st = eng.step(cg, pg)
+        lo = ora.step(co, po)
+        so = ora.stats()
+        it_g.append(st["pcg_iters"])
+        it_o.append(so["pcg_iters"])
+        assert st["trials"] == so["trials"] and abs(st["pcg_iters"] - so["pcg_iters"]) <= 1, (s, st, so)
+        assert abs(lg - lo) / lo < 1e-8, (s, lg, lo)
+    assert rel(cg.cpu().numpy(), co) < 1e-7
+    if cfg == 3:
+        assert sum(it_g) < 0.6 * 213, it_g

@@ -35,6 +35,7 @@ S[rdq]="rdq|300|INSFM_DIAG=create python -u bench.py --no-cpu --no-solve > $R/gp
 S[ab_cu]="ab_cu|600|tools/ab_env.sh 2 side_cu16 && tools/ab_env.sh 2 side_cu32 && tools/ab_env.sh 2 side_cu64"
 S[ab_fork]="ab_fork|500|tools/ab_env.sh 4 lin_fork_early"
 S[benchdef]="benchdef|400|python -u bench.py > $R/gpurun_out/bench_default.json"
+S[adef]="adef|400|for i in 1 2; do timeout -k 10 150 python -u bench.py --no-cpu --no-solve --precond 2 > $R/gpurun_out/adef_\$i.json 2> $R/gpurun_out/adef_\$i.err || exit 1; timeout -k 10 150 python -u bench.py --no-cpu --no-solve > $R/gpurun_out/ad_\$i.json 2>> $R/gpurun_out/adef_\$i.err || exit 1; done; for f in adef_1 ad_1 adef_2 ad_2; do python3 -c \"import json; d=json.loads([l for l in open('$R/gpurun_out/\$f.json') if l.startswith('{')][-1]); print('\$f', d['value'], d['ms_per_step'], d['phase_ms_per_step']['cg_iterations'], d['pcg_iters'], sum(d['pcg_iters']), d['final_rmse_px'], d['kernel_us'])\"; done"
 S[solve]="solve|200|python -u tools/solve_probe.py --modes alive,solve,warm --reps 2"
 args=()
 for k in "$@"; do args+=("${S[$k]}"); done
