@@ -77,7 +77,7 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb, extra=None):
     raise ValueError(kernel)
 
 
-def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=14):
+def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=14, precond=2):
     """The oracle's LM to convergence on the same scene, repeated until >= min_seconds of CPU work (a bounded sample)."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
@@ -85,7 +85,7 @@ def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=14)
     while runs < max_runs and (runs == 0 or dt < min_seconds):
         t0 = time.perf_counter()
         cams, pts, hist, rmse = O.solve_to_convergence(prob, max_iters=max_steps, threads=threads,
-                                                       cluster_size=cluster_size)
+                                                       cluster_size=cluster_size, precond=precond)
         dt += time.perf_counter() - t0
         steps += len(hist)
         runs += 1
@@ -99,7 +99,7 @@ def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=14)
     except OSError:
         pass
     return dict(value=steps / dt, unit="LM it/s", cores=threads, kind="port",
-                sample=f"oracle/ba_oracle.c (C/OpenMP f64 restatement of the same LM incl. the two-level PCG), same "
+                sample=f"oracle/ba_oracle.c (C/OpenMP f64 restatement of the same LM incl. the two-level PCG, precond {precond}), same "
                        f"scene, {runs} runs to the reference stop rule ({len(hist)} LM steps each), {steps} steps in "
                        f"{dt:.2f} s incl. setup; CPU: {model}",
                 final_rmse_px=rmse, steps=len(hist))
@@ -653,7 +653,9 @@ def main():
     ap.add_argument("--no-solve", action="store_true", help="skip the end-to-end TorchBA.Solve split")
     ap.add_argument("--cpu-max-steps", type=int, default=30)
     ap.add_argument("--deterministic", action="store_true")
-    ap.add_argument("--precond", type=int, default=1, help="1 two-level (default), 2 two-level with the A-DEF2 coarse correction, 0 block-Jacobi (the reference's)")
+    ap.add_argument("--precond", type=int, default=2,
+                    help="2 (default, TorchBA's) two-level with the A-DEF2 coarse correction, 1 the additive two-level "
+                         "form, 0 block-Jacobi (the reference's)")
     ap.add_argument("--cluster-size", type=int, default=14, help="two-level: target cameras per coarse cluster")
     ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes", "mapper"), default="ba")
     ap.add_argument("--mapper-images", type=int, default=500, help="--path mapper: images in the database")
@@ -870,7 +872,9 @@ def main():
         "kernel_us": dict({k: round(v[2], 3) for k, v in kern.items()},
                           **({"k_tl_cgp_iterations": round(cgp[2], 2)}
                              if cgp is not None else {})),
-        "preconditioner": "two-level (block-Jacobi + camera-cluster similarity coarse space)" if tl else "block-Jacobi",
+        "preconditioner": ("block-Jacobi" if not tl else "two-level (block-Jacobi + camera-cluster similarity coarse space"
+                           + (", A-DEF2 coarse correction from the coarse initial guess)" if args.precond == 2 else ", additive)")),
+        "cg_path": eng.cg_info()[0],
         "roofline": roof,
         "roofline_next_kernels": others,
     }
@@ -891,7 +895,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_solve:
         out["solve_end_to_end"] = solve_end_to_end(prob, dev)
     if rank == 0 and not args.no_cpu:
-        cb = cpu_baseline(prob, args.cpu_max_steps, cluster_size=args.cluster_size)
+        cb = cpu_baseline(prob, args.cpu_max_steps, cluster_size=args.cluster_size, precond=args.precond)
         out["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         out["cpu_final_rmse_px"] = cb["final_rmse_px"]
         out["cpu_steps_to_converge"] = cb["steps"]

@@ -10,8 +10,9 @@
  *     (bae.autograd.function, un-vendored)  -> fused into the library's linearize kernels;
  *   - `bae.utils.pysolvers.PCG` and the cuDSS sparse solve (un-vendored)  -> explicit Schur complement on the camera
  *     blocks + PCG kernels with the same relative-residual stopping rule; preconditioner `desc.precond`: 1 (default)
- *     two-level = block-Jacobi + a camera-cluster coarse correction (similarity + intrinsic modes per cluster, the
- *     build's choice), 0 = block-Jacobi only (the closest restatement of PCG(tol=1e-5));
+ *     two-level = block-Jacobi + an additive camera-cluster coarse correction (similarity + intrinsic modes per
+ *     cluster, the build's choice), 2 = the same coarse space as an A-DEF2 deflation (TorchBA.Solve's choice),
+ *     0 = block-Jacobi only (the closest restatement of PCG(tol=1e-5));
  *   - `model.loss(input)` (pypose RobustModel, Huber kernel)  -> insfm_ba_cost().
  * Creation corresponds to the LM/model construction at bundle_adjustment.py:115-119 (packed inputs of :98-113).
  *
@@ -67,8 +68,12 @@ typedef struct {
     insfm_ba_allreduce_fn allreduce;  /* required when world_size > 1 */
     void* allreduce_ctx;
     int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
-                              plus a coarse correction on camera clusters (7 similarity modes + intrinsics per cluster).
-                              Same stopping rule (||b - S x|| <= tol ||b||), 5-10x fewer iterations. */
+                              plus an additive coarse correction on camera clusters (7 similarity modes + intrinsics per
+                              cluster), 2 = the same coarse space as an A-DEF2 deflation (x0 = Z E^-1 Z^T r0, then
+                              M^-1 r = r + Z E^-1 Z^T (r - S r) -- Tang, Nabben, Vuik & Erlangga 2009): about half the
+                              iterations of 1 (TorchBA.Solve and bench.py use 2).  The fixed-order multi-rank CG runs 2
+                              as 1 (insfm_ba_cg_info path code 2; 4 = A-DEF2 k_tl_cgp).  Same stopping rule
+                              (||b - S x|| <= tol ||b||), 5-20x fewer iterations than 0. */
     int32_t cluster_size;  /* target cameras per coarse cluster (default 14; grown until nclust*(D+1) <= 768) */
     int32_t schur_variant; /* reduced-system build: must be 0 (EINVAL otherwise).  Kept for the struct layout: the
                               round-2/3 variants 1-3 (re-derived or compact camera-point blocks) were measured slower

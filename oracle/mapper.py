@@ -106,7 +106,8 @@ def ba_solve(cameras, images, tracks, options):
     cams, pts, hist, rmse = O.solve_to_convergence(prob, max_iters=options['max_num_iterations'],
                                                    ftol=options['function_tolerance'],
                                                    huber_delta=options['thres_loss_function'],
-                                                   optimize_poses=int(bool(options['optimize_poses'])))
+                                                   optimize_poses=int(bool(options['optimize_poses'])),
+                                                   precond=options.get('precond', 2))  # (TorchBA's default)
     update(cameras, images, tracks, pk, cams, pts)
     return hist, rmse
 

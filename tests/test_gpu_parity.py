@@ -217,8 +217,9 @@ def test_torchba_solve_end_to_end(model):
     pk = pack(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS)
     ba = TorchBA(device="cuda:0")
     ba.Solve(cameras, images, tracks, BUNDLE_ADJUSTER_OPTIONS, progress=False)
+    # (the oracle runs the preconditioner the engine ran: A-DEF2 on the D = 8 persistent CG, else the additive form)
     ora = O.OracleBA(pk.model.value, pk.points_2d, pk.camera_indices, pk.point_indices, pk.camera_pps,
-                     pk.camera_params.shape[0], pk.points_3d.shape[0])
+                     pk.camera_params.shape[0], pk.points_3d.shape[0], precond=ba.precond_effective)
     c, p = pk.camera_params.copy(), pk.points_3d.copy()
     hist = []
     for _ in range(BUNDLE_ADJUSTER_OPTIONS['max_num_iterations']):
