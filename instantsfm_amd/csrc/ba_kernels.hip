@@ -65,6 +65,9 @@ constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 /
 #ifndef SCHUR_MINW
 #define SCHUR_MINW 1  // k_schur launch bound: minimum waves per SIMD (caps VGPRs: 4 -> 128)
 #endif
+#ifndef SCHUR_SLOTPRE
+#define SCHUR_SLOTPRE 1  // k_schur: a round's partner slots looked up before its LDS adds
+#endif
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
@@ -723,10 +726,23 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     }
                 }
             }
+#if SCHUR_SLOTPRE
+            // every slot of the round looked up before the first ds_add_f64: one LDS wait per round instead of one
+            // per partner (a slot read issued behind the previous partner's adds waits for them to retire)
+            int slv[UP];
+#pragma unroll
+            for (int u = 0; u < UP; ++u) slv[u] = slot[cj[u] >= 0 ? cj[u] : 0];
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (vmcnt, expcnt unconstrained): all slots read
+            __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
             for (int u = 0; u < UP; ++u) {
                 if (cj[u] >= 0) {
+#if SCHUR_SLOTPRE
+                    const int sl = slv[u];
+#else
                     const int sl = slot[cj[u]];
+#endif
                     if (sl >= 0) {
                         double* dst = acc + (size_t)sl * BS + cb;
                         const double y0 = x[u][0], y1 = x[u][1], y2 = x[u][2];
