@@ -77,7 +77,7 @@ def algorithmic_bytes(kernel, C, P, N, D, nnzb, extra=None):
     raise ValueError(kernel)
 
 
-def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=14, precond=2):
+def cpu_baseline(prob, max_steps, min_seconds=10.0, max_runs=8, cluster_size=24, precond=2):
     """The oracle's LM to convergence on the same scene, repeated until >= min_seconds of CPU work (a bounded sample)."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
@@ -656,7 +656,7 @@ def main():
     ap.add_argument("--precond", type=int, default=2,
                     help="2 (default, TorchBA's) two-level with the A-DEF2 coarse correction, 1 the additive two-level "
                          "form, 0 block-Jacobi (the reference's)")
-    ap.add_argument("--cluster-size", type=int, default=14, help="two-level: target cameras per coarse cluster")
+    ap.add_argument("--cluster-size", type=int, default=24, help="two-level: target cameras per coarse cluster")
     ap.add_argument("--path", choices=("ba", "gp", "tracks", "passes", "mapper"), default="ba")
     ap.add_argument("--mapper-images", type=int, default=500, help="--path mapper: images in the database")
     ap.add_argument("--mapper-points", type=int, default=100_000, help="--path mapper: scene points")

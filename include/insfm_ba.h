@@ -74,7 +74,7 @@ typedef struct {
                               iterations of 1 (TorchBA.Solve and bench.py use 2).  The fixed-order multi-rank CG runs 2
                               as 1 (insfm_ba_cg_info path code 2; 4 = A-DEF2 k_tl_cgp).  Same stopping rule
                               (||b - S x|| <= tol ||b||), 5-20x fewer iterations than 0. */
-    int32_t cluster_size;  /* target cameras per coarse cluster (default 14; grown until nclust*(D+1) <= 768) */
+    int32_t cluster_size;  /* target cameras per coarse cluster (default 24; grown until nclust*(D+1) <= 768) */
     int32_t schur_variant; /* reduced-system build: must be 0 (EINVAL otherwise).  Kept for the struct layout: the
                               round-2/3 variants 1-3 (re-derived or compact camera-point blocks) were measured slower
                               or even and removed. */

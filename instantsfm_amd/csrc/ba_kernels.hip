@@ -686,14 +686,16 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             }
         }
         if (has) {
+            // staged negated: the partner products below then come out with the sign S_ij needs (sign-symmetric
+            // rounding: bitwise the negation of the positive products) and need no v_xor per row
             if constexpr (GPW || RETRY) {
-                my_wh[cb * 4 + 0] = w0 * v00 + w1 * v01 + w2 * v02;
-                my_wh[cb * 4 + 1] = w0 * v01 + w1 * v11 + w2 * v12;
-                my_wh[cb * 4 + 2] = w0 * v02 + w1 * v12 + w2 * v22;
+                my_wh[cb * 4 + 0] = -(w0 * v00 + w1 * v01 + w2 * v02);
+                my_wh[cb * 4 + 1] = -(w0 * v01 + w1 * v11 + w2 * v12);
+                my_wh[cb * 4 + 2] = -(w0 * v02 + w1 * v12 + w2 * v22);
             } else {  // the first trial on the Y records: S_ij -= Y_o Y_q^T directly
-                my_wh[cb * 4 + 0] = w0;
-                my_wh[cb * 4 + 1] = w1;
-                my_wh[cb * 4 + 2] = w2;
+                my_wh[cb * 4 + 0] = -w0;
+                my_wh[cb * 4 + 1] = -w1;
+                my_wh[cb * 4 + 2] = -w2;
             }
             if (diag_chunk) {
                 const double* yp = y + 3 * (size_t)dcur.y;
@@ -748,7 +750,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                         const double y0 = x[u][0], y1 = x[u][1], y2 = x[u][2];
 #pragma unroll
                         for (int a2 = 0; a2 < D; ++a2)
-                            atomicAdd(dst + a2 * D, -(wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2));
+                            atomicAdd(dst + a2 * D, wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2);
                     }
                 }
             }
@@ -3131,7 +3133,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->world_size = 1; d->rank = 0;
     d->shard_point_begin = 0; d->shard_point_end = -1;
     d->precond = 1;
-    d->cluster_size = 14;
+    d->cluster_size = 24;
     d->exchange_chunks = 4;
 }
 
@@ -3520,7 +3522,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     bool coarse_ok = false;
     std::vector<int>& lab = h->clab_host;
     if (desc->precond >= 1 && h->d.optimize_poses) {
-        int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 14, C);
+        int K = std::min(desc->cluster_size > 0 ? desc->cluster_size : 24, C);
         nc = aggregate(g, C, K, lab);
         while (nc * MC > kCoarseMax && K < C) {
             K = (int)std::min<long long>(C, std::max<long long>(K + 1, ((long long)K * nc * MC + kCoarseMax - 1) / kCoarseMax));

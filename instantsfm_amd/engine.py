@@ -16,7 +16,7 @@ from . import _capi
 # TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.
 LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4, tr_factor=0.25,
                    tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, max_rejects=30, pcg_tol=1e-5,
-                   pcg_max_iter=500, precond=1, cluster_size=14, exchange_chunks=4)
+                   pcg_max_iter=500, precond=1, cluster_size=24, exchange_chunks=4)
 
 
 # insfm_ba_debug_stamps' kernel order (ba_common.h StampKind)

@@ -528,7 +528,7 @@ ora_t* ora_create(int model, int C, int P, int N, const double* uv, const int* c
     h->down0 = dopt[5]; h->factor = dopt[6]; h->high = dopt[7]; h->low = dopt[8]; h->cmin = dopt[9];
     h->cmax = dopt[10]; h->pcg_tol = dopt[11];
     h->max_rejects = iopt[0]; h->pcg_max_iter = iopt[1]; h->optimize_poses = iopt[2];
-    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 14;
+    h->precond = iopt[4]; h->cluster_size = iopt[5] > 0 ? iopt[5] : 24;
     h->order_seed = iopt[6]; h->order_mode = iopt[7];
 #ifdef _OPENMP
     if (iopt[3] > 0) omp_set_num_threads(iopt[3]);

@@ -123,7 +123,7 @@ def retract_pose(x7, d6):
 
 DEFAULTS = dict(huber_delta=1.0, tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4,
                 tr_factor=0.25, tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, pcg_tol=1e-5,
-                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=14,
+                max_rejects=30, pcg_max_iter=500, optimize_poses=1, threads=0, precond=1, cluster_size=24,
                 order_seed=0, order_mode=0)
 
 

@@ -105,10 +105,14 @@ def main():
         dist.destroy_process_group()
         return
     prob = make_problem(24, 900, seed=9) if args.small else make_config(args.config)
+    # the 24-camera scene in two coarse clusters, so the row-partitioned CG gives both ranks rows (it splits at cluster
+    # boundaries; the default target of 24 makes this scene one cluster); the single-GPU reference uses the same
+    ckw = {"cluster_size": 12} if args.small else {}
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
                          world_size=world, rank=rank, shard=shards[rank], deterministic=True,
-                         force_exchange=args.force_exchange, exchange_chunks=args.exchange_chunks)
+                         force_exchange=args.force_exchange, exchange_chunks=args.exchange_chunks,
+                         **ckw)
     rows = eng.partition_cg() if args.cg_partition else None
     path0 = eng.cg_info()[0]  # the CG every rank agreed on at create (engine.agree_cg_path)
     cams = torch.from_numpy(prob.cams_init.copy()).to(dev)
@@ -146,7 +150,7 @@ def main():
     if rank == 0:
         os.environ.pop("INSFM_DIAG", None)
         ref = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
-                             device=dev, deterministic=True)
+                             device=dev, deterministic=True, **ckw)
         rc = torch.from_numpy(prob.cams_init.copy()).to(dev)
         rp = torch.from_numpy(prob.points_init.copy()).to(dev)
         ref_losses = [ref.step(rc, rp)[0] for _ in range(args.steps)]

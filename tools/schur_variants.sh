@@ -15,9 +15,9 @@ for spec in "$@"; do
           instantsfm_amd/csrc/$src.hip
       fi
     done
-    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/lib_$name.so build/variants/${name}_ba_kernels.o \
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ${OUTDIR:-tools}/lib_$name.so build/variants/${name}_ba_kernels.o \
       build/obj/passes.hip.o build/obj/tracks.hip.o
-    echo "built tools/lib_$name.so ($defs)"
+    echo "built ${OUTDIR:-tools}/lib_$name.so ($defs)"
   ) &
 done
 wait
