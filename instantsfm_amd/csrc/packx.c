@@ -54,8 +54,16 @@ static PyObject* collect(PyObject* self, PyObject* args) {
     const Py_ssize_t T = PySequence_Fast_GET_SIZE(fast);
     PyObject** items = PySequence_Fast_ITEMS(fast);
     PyObject** ob = (PyObject**)PyMem_Calloc(T > 0 ? (size_t)T : 1, sizeof(PyObject*));
+    /* per track: its data pointer, element width and output offset (the copy below runs without the GIL) */
+    const void** src = (const void**)PyMem_Calloc(T > 0 ? (size_t)T : 1, sizeof(void*));
+    int64_t* dst_off = (int64_t*)PyMem_Calloc(T > 0 ? (size_t)T : 1, sizeof(int64_t));
+    unsigned char* kind = (unsigned char*)PyMem_Calloc(T > 0 ? (size_t)T : 1, 1);
     PyObject *lb = NULL, *obb = NULL, *xb = NULL, *res = NULL;
-    if (!ob) { Py_DECREF(fast); return PyErr_NoMemory(); }
+    if (!ob || !src || !dst_off || !kind) {
+        PyMem_Free(ob); PyMem_Free(src); PyMem_Free(dst_off); PyMem_Free(kind);
+        Py_DECREF(fast);
+        return PyErr_NoMemory();
+    }
     lb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(int64_t) * (size_t)T));
     xb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(double) * 3 * (size_t)T));
     if (!lb || !xb) goto done;
@@ -66,8 +74,12 @@ static PyObject* collect(PyObject* self, PyObject* args) {
         PyObject* o = PyObject_GetAttr(items[t], s_obs);
         if (!o) goto done;
         ob[t] = o;
-        if (!obs_kind(o)) goto fallback;
+        const int ok_ = obs_kind(o);
+        if (!ok_) goto fallback;
+        kind[t] = (unsigned char)ok_;
+        src[t] = PyArray_DATA((PyArrayObject*)o);
         lengths[t] = PyArray_DIM((PyArrayObject*)o, 0);
+        dst_off[t] = 2 * nvalid;
         if (lengths[t] >= min_len) nvalid += lengths[t];
         PyObject* x = PyObject_GetAttr(items[t], s_xyz);
         if (!x) goto done;
@@ -84,19 +96,23 @@ static PyObject* collect(PyObject* self, PyObject* args) {
     obb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(int64_t) * 2 * (size_t)nvalid));
     if (!obb) goto done;
     {
+        /* the copy from the 200k arrays (references held in ob[]) on all host cores, without the GIL: every track
+         * writes its own slice of the output, so the result is the sequential loop's */
         int64_t* out = (int64_t*)PyBytes_AS_STRING(obb);
+        Py_BEGIN_ALLOW_THREADS
+        #pragma omp parallel for schedule(static, 1024)
         for (Py_ssize_t t = 0; t < T; ++t) {
             if (lengths[t] < min_len) continue;
             const Py_ssize_t n = 2 * lengths[t];
-            const void* src = PyArray_DATA((PyArrayObject*)ob[t]);
-            if (obs_kind(ob[t]) == 8) {
-                memcpy(out, src, sizeof(int64_t) * (size_t)n);
+            int64_t* o = out + dst_off[t];
+            if (kind[t] == 8) {
+                memcpy(o, src[t], sizeof(int64_t) * (size_t)n);
             } else {
-                const int32_t* s = (const int32_t*)src;
-                for (Py_ssize_t k = 0; k < n; ++k) out[k] = s[k];
+                const int32_t* s32 = (const int32_t*)src[t];
+                for (Py_ssize_t k = 0; k < n; ++k) o[k] = s32[k];
             }
-            out += n;
         }
+        Py_END_ALLOW_THREADS
     }
     res = PyTuple_Pack(3, lb, obb, xb);
     goto done;
@@ -106,6 +122,9 @@ fallback:
 done:
     for (Py_ssize_t t = 0; t < T; ++t) Py_XDECREF(ob[t]);
     PyMem_Free(ob);
+    PyMem_Free(src);
+    PyMem_Free(dst_off);
+    PyMem_Free(kind);
     Py_XDECREF(lb);
     Py_XDECREF(obb);
     Py_XDECREF(xb);
