@@ -24,10 +24,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--precond", type=int, default=2, help="2: the A-DEF2 k_tl_cgp that bench.py's roofline times")
     a = ap.parse_args()
     prob = make_config(3)
     dev = torch.device("cuda:0")
-    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev)
+    eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
+                         precond=a.precond)
     cams = torch.from_numpy(prob.cams_init).to(dev)
     pts = torch.from_numpy(prob.points_init).to(dev)
     iters = [eng.step(cams, pts)[1]["pcg_iters"] for _ in range(a.steps)]
