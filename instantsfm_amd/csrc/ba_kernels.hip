@@ -50,6 +50,10 @@ constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgr
 #define SCHUR_LDS_KB 96  // k_schur row-chunk LDS target (rows with more upper blocks are split into chunks)
 #endif
 constexpr int kLdsTarget = SCHUR_LDS_KB * 1024;
+#ifndef SCHUR_LDS_KB_DET
+#define SCHUR_LDS_KB_DET 40  // deterministic mode's k_schur row-chunk LDS target (one wave per workgroup)
+#endif
+constexpr int kLdsTargetDet = SCHUR_LDS_KB_DET * 1024;
 #ifndef INSFM_SCHUR_WAVES
 #define INSFM_SCHUR_WAVES 8
 #endif
@@ -3604,12 +3608,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (nj.empty()) nj.push_back(0);
     tick("CG neighbour lists");
     // Schur work items: split long rows so a chunk fits the LDS budget
-    const size_t wsh_lds = sizeof(double) * kSchurWaves * (64 / D) * schur_ws(D);  // W^ staging, up to kSchurWaves waves
+    // Deterministic mode runs k_schur with one wave per workgroup (fixed order of the LDS adds): its workgroups stage
+    // one wave's W^ and take row chunks of <= kLdsTargetDet, so that several share a CU.  (With the 96-KB chunks of the
+    // 8-wave form one wave held a whole CU: k_schur 2.1 ms per trial on config 3 in deterministic mode.)
+    const bool det_schur = desc->deterministic != 0;
+    const size_t wsh_lds = sizeof(double) * (det_schur ? 1 : kSchurWaves) * (64 / D) * schur_ws(D);  // W^ staging
     const size_t fixed_lds = sizeof(double) * (D + 12) + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
-    // chunk target: kLdsTarget when at least 8 blocks fit under it, else the hard budget
-    const size_t tgt = (size_t)kLdsTarget >= fixed_lds + 8 * sizeof(double) * schur_bs(D) ? (size_t)kLdsTarget
-                                                                                         : (size_t)kLdsBudget;
+    // chunk target: kLdsTarget (deterministic mode kLdsTargetDet) when at least 8 blocks fit under it, else the hard
+    // budget
+    const size_t tgt0 = det_schur ? (size_t)kLdsTargetDet : (size_t)kLdsTarget;
+    const size_t tgt = tgt0 >= fixed_lds + 8 * sizeof(double) * schur_bs(D) ? tgt0 : (size_t)kLdsBudget;
     const int cap = (int)((tgt - fixed_lds) / (sizeof(double) * schur_bs(D)));
     std::vector<int4> work;
     int maxc = 1;
@@ -4404,13 +4413,10 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
             } else if (which == 0)
                 k_cg_iter<DV><<<h->C, kCgThreads, 0, h->stream>>>(1, h->C, h->d.pcg_max_iter, 0.0, h->nbr_ptr, h->nbr_j, h->Sn,
                                                                 h->Lf, h->cg);
-            else {
-                const int det = h->d.deterministic;
-                h->d.deterministic = 0;
+            else {  // the k_schur form this handle runs (deterministic mode: one wave per workgroup, its LDS layout)
                 const int rc2 = launch_schur(h, h->kind ? h->Up : h->U, h->kind ? h->gpc : h->gc, 1.0,
                                              h->kind ? -1e308 : h->d.clamp_min, h->kind ? 1e308 : h->d.clamp_max,
                                              h->kind ? 1 : h->d.rank == 0, false);
-                h->d.deterministic = det;
                 if (rc2) return rc2;
             }
         }
