@@ -9,10 +9,10 @@
  *     (bundle_adjustment.py:51-64, cost_function.py:32-208) and its TrackingTensor sparse Jacobian
  *     (bae.autograd.function, un-vendored)  -> fused into the library's linearize kernels;
  *   - `bae.utils.pysolvers.PCG` and the cuDSS sparse solve (un-vendored)  -> explicit Schur complement on the camera
- *     blocks + PCG kernels with the same relative-residual stopping rule; preconditioner `desc.precond`: 1 (default)
- *     two-level = block-Jacobi + an additive camera-cluster coarse correction (similarity + intrinsic modes per
- *     cluster, the build's choice), 2 = the same coarse space as an A-DEF2 deflation (TorchBA.Solve's choice),
- *     0 = block-Jacobi only (the closest restatement of PCG(tol=1e-5));
+ *     blocks + PCG kernels with the same relative-residual stopping rule; preconditioner `desc.precond`: 2 (default,
+ *     the product's: TorchBA.Solve, bench.py) a camera-cluster coarse space (similarity + intrinsic modes per cluster,
+ *     the build's choice) applied as an A-DEF2 deflation on top of block-Jacobi, 1 = the same coarse space as an
+ *     additive correction, 0 = block-Jacobi only (the closest restatement of PCG(tol=1e-5));
  *   - `model.loss(input)` (pypose RobustModel, Huber kernel)  -> insfm_ba_cost().
  * Creation corresponds to the LM/model construction at bundle_adjustment.py:115-119 (packed inputs of :98-113).
  *
@@ -67,12 +67,14 @@ typedef struct {
     int32_t shard_point_end;
     insfm_ba_allreduce_fn allreduce;  /* required when world_size > 1 */
     void* allreduce_ctx;
-    int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 (default) two-level: block-Jacobi
-                              plus an additive coarse correction on camera clusters (7 similarity modes + intrinsics per
-                              cluster), 2 = the same coarse space as an A-DEF2 deflation (x0 = Z E^-1 Z^T r0, then
-                              M^-1 r = r + Z E^-1 Z^T (r - S r) -- Tang, Nabben, Vuik & Erlangga 2009): about half the
-                              iterations of 1 (TorchBA.Solve and bench.py use 2).  The fixed-order multi-rank CG runs 2
-                              as 1 (insfm_ba_cg_info path code 2; 4 = A-DEF2 k_tl_cgp).  Same stopping rule
+    int32_t precond;       /* PCG preconditioner: 0 block-Jacobi (the reference's), 1 two-level: block-Jacobi plus an
+                              additive coarse correction on camera clusters (7 similarity modes + intrinsics per
+                              cluster), 2 (default) = the same coarse space as an A-DEF2 deflation (x0 = Z E^-1 Z^T r0,
+                              then M^-1 r = r + Z E^-1 Z^T (r - S r) -- Tang, Nabben, Vuik & Erlangga 2009): about half
+                              the iterations of 1.  2 runs on the persistent CG (D = 8; insfm_ba_cg_info path 4, and 5
+                              in its fixed-order form: deterministic mode, every rank of a multi-rank run); the
+                              launch-per-iteration CG (other D, ranks sharing a GPU) runs 2 as 1.  An A-DEF2 solve that
+                              breaks down is repeated with 1 (insfm_ba_cg_fallbacks).  Same stopping rule
                               (||b - S x|| <= tol ||b||), 5-20x fewer iterations than 0. */
     int32_t cluster_size;  /* target cameras per coarse cluster (default 24; grown until nclust*(D+1) <= 768) */
     int32_t schur_variant; /* reduced-system build: must be 0 (EINVAL otherwise).  Kept for the struct layout: the
@@ -97,7 +99,10 @@ typedef struct {
     double time_ms[8];      /* device time per phase (hipEvent on the library stream), filled when stats != NULL:
                                [0] linearize  [1] k_schur  [2] whole linear solve (point prep .. CG finish, incl. the
                                host polls of the CG status)  [3] back-substitution + update  [4] trial cost
-                               [5] CG iteration launches (k_cg_dots + k_cg_iter chunks, no host gaps)  [6..7] 0
+                               [5] CG iteration launches (k_cg_dots + k_cg_iter chunks, no host gaps)  [6] the
+                               two-level coarse-inverse chains that finished during the step (side stream: E build +
+                               Gauss-Jordan; overlaps the other phases)  [7] multi-rank: the chunked [S | b] exchange's
+                               span on the exchange stream (0 otherwise)
                                Only filled after insfm_ba_set_timing(h, 1): the events cost a little. */
     int32_t coarse_used;    /* two-level preconditioner: 1 if the coarse correction was active in the final trial
                                (0 with precond 0, or when the coarse matrix was not positive definite) */
@@ -155,6 +160,11 @@ int insfm_ba_cg_info(const insfm_ba* h, int32_t* out);
  * unless every rank runs the fixed-order k_tl_cgp and every GPU holds all grids placed on it).  on = 1: EINVAL unless
  * the handle already runs it. */
 int insfm_ba_set_persistent_cg(insfm_ba* h, int32_t on);
+
+/* A-DEF2 solves (precond 2) of this handle that broke down (single-reduction recurrence, status 2: possible under a
+ * lagged coarse inverse) and were repeated with the additive coarse correction (precond 1) instead of failing the LM
+ * step; a count (>= 0) or a negative error code. */
+int32_t insfm_ba_cg_fallbacks(const insfm_ba* h);
 
 /* Row-partitioned two-level CG across ranks (multi-rank handles with precond 1): each rank applies
  * the reduced camera matrix to its own rows (whole camera clusters) and writes those rows' CG partials straight into

@@ -60,7 +60,7 @@ SYMBOLS = ("insfm_build_info", "insfm_ba_default_desc", "insfm_ba_create", "insf
            "insfm_ba_destroy", "insfm_ba_last_error", "insfm_ba_debug_linearize", "insfm_ba_debug_solve",
            "insfm_ba_debug_get", "insfm_ba_nnzb", "insfm_ba_exchange_count", "insfm_ba_set_exchange",
            "insfm_ba_debug_time_kernel", "insfm_ba_set_timing", "insfm_ba_debug_clusters", "insfm_ba_debug_spd_inverse",
-           "insfm_ba_release_cache", "insfm_ba_set_ranks_per_device", "insfm_ba_cg_info", "insfm_ba_set_persistent_cg", "insfm_ba_cg_window", "insfm_ba_cg_attach", "insfm_ba_cg_partition",
+           "insfm_ba_release_cache", "insfm_ba_set_ranks_per_device", "insfm_ba_cg_info", "insfm_ba_set_persistent_cg", "insfm_ba_cg_fallbacks", "insfm_ba_cg_window", "insfm_ba_cg_attach", "insfm_ba_cg_partition",
            "insfm_ba_debug_time_xchg", "insfm_ba_debug_time_cgp", "insfm_ba_debug_stamps",
            "insfm_gp_default_desc", "insfm_gp_create", "insfm_gp_step", "insfm_gp_cost", "insfm_gp_debug_linearize",
            "insfm_gp_debug_get_ds",
@@ -158,6 +158,8 @@ def load(path=None):
     L.insfm_ba_cg_info.restype = ctypes.c_int
     L.insfm_ba_set_persistent_cg.argtypes = [vp, ctypes.c_int32]
     L.insfm_ba_set_persistent_cg.restype = ctypes.c_int
+    L.insfm_ba_cg_fallbacks.argtypes = [vp]
+    L.insfm_ba_cg_fallbacks.restype = ctypes.c_int32
     L.insfm_ba_cg_window.argtypes = [vp, ctypes.c_char_p]
     L.insfm_ba_cg_window.restype = ctypes.c_int
     L.insfm_ba_cg_attach.argtypes = [vp, ctypes.c_char_p]

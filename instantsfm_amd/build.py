@@ -111,7 +111,7 @@ def build_packx(force=False, verbose=True):
     """The packing extension: no FMA contraction (its cheirality test must round like numpy's unfused operations)."""
     if not (force or _stale(PACKX_OUT, [PACKX_SRC])):
         return PACKX_OUT
-    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-std=c99",
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-pthread", "-ffp-contract=off", "-std=gnu99",
            "-Wall", f'-DPACKX_SRC_HASH="{packx_hash()}"', f"-I{sysconfig.get_paths()['include']}",
            f"-I{_numpy_include()}", "-o", PACKX_OUT + ".tmp", PACKX_SRC]
     if verbose:

@@ -26,7 +26,9 @@
 // stays there.
 // Two variants: per-cluster atomic partial sums (single rank, non-deterministic), and DET, a fixed summation order
 // (deterministic mode and every rank of the replicated multi-rank CG): each workgroup run's partials are stored in a
-// parity buffer before the grid barrier, and after it every workgroup sums each cluster's runs itself in run order.
+// parity buffer before the grid barrier, and after it every workgroup sums each cluster's runs itself in run order
+// (det_cluster_sums).  Either variant applies the coarse correction additively (precond 1) or as A-DEF2 (ADEF,
+// precond 2; round 6 added the DET form of A-DEF2, so the multi-rank and deterministic paths run it too).
 // Host eligibility (ba_kernels.hip, create): D = 8, host-mapped progress word, rows of at most NB = 128 blocks stored in
 // cluster order (tl.sperm the identity), at most kCgpSegMax neighbour clusters per row, and every workgroup resident at
 // once (one per CU) -- for ranks sharing a GPU, all of their grids at once.
@@ -179,12 +181,52 @@ __device__ __forceinline__ double uni(double v) {
     return __hiloint2double(hi, lo);
 }
 
+// DET (fixed summation order): rs[e] for e < NS nc (c = e / NS, k = e % NS) = the sum of slot off + k of the
+// 12-slot run records of cluster c (rb + position * 12, one record at the head position of each run), taken in run
+// order -- the same doubles in every workgroup, no atomics.  Run heads: the cluster's first position, then every
+// multiple of kCgpRows inside it; the first RB heads of each entry are loaded at once.
+template <int NS>
+__device__ __forceinline__ void det_cluster_sums(const double* rb, int off, const int* clp, int nc, double* rs) {
+    constexpr int EPT = (NS * kCgpMaxClusters + kCgpThreads - 1) / kCgpThreads;
+    constexpr int RB = 6;  // run heads per cluster loaded at once (clusters with more take a second pass)
+    const int t = threadIdx.x, ne = NS * nc;
+    double x[EPT][RB];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+        const int e = min(t + q * kCgpThreads, ne - 1), c = e / NS, k = e - NS * c;
+        const int p1 = clp[c + 1];
+        int p = clp[c];
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            x[q][r] = ld_sc1(rb + (size_t)max(min(p, p1 - 1), 0) * 12 + off + k);  // (an empty first cluster: 0)
+            if (p < p1) p = (p / kCgpRows + 1) * kCgpRows;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+        const int e0 = t + q * kCgpThreads, e = min(e0, ne - 1), c = e / NS, k = e - NS * c;
+        const int p1 = clp[c + 1];
+        int p = clp[c];
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+            if (p < p1) {
+                v += x[q][r];
+                p = (p / kCgpRows + 1) * kCgpRows;
+            }
+        }
+        for (; p < p1; p = (p / kCgpRows + 1) * kCgpRows) v += ld_sc1(rb + (size_t)p * 12 + off + k);
+        if (e0 < ne) rs[e0] = v;
+    }
+}
+
 // NB: blocks per row held in registers (a multiple of 8).  wx: [2][C][8] the w exchange by iteration parity (a
 // workgroup's P2 may run while another is still gathering in P1); yg: [m][2] the tagged granules of y, tag0 the tag of
 // iteration 0 (tags never repeat on a handle); sync: kCgpSyncWords barrier words, epoch0: the barriers they have
 // counted so far (one per iteration of earlier launches); oseg bit 0: also write this solve's coarse segments tl.Oseg
 // (the E build behind the CG then skips k_tl_erow), bit 1 (tests, INSFM_DIAG=cgp_fault): the last workgroup leaves
-// at iteration 2 as if a barrier had timed out;
+// at iteration 2 as if a barrier had timed out, bit 2 (tests, INSFM_DIAG=adef2_breakdown): an A-DEF2 launch reports a
+// breakdown (status 2) at iteration 2;
 // dcout (non-null): the camera step dc = L^-T x~ written at the end (k_cg_finish's arithmetic);
 // trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
 // of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
@@ -225,7 +267,6 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     __shared__ int pcl[kCgpRows];                      // each row's cluster (-1: no row)
     __shared__ int bflag;
     __shared__ double dvec[kCgpRows][D];               // ADEF: each row's d = -(off-diagonal part of S~ v)
-    static_assert(!(DET && ADEF), "A-DEF2 runs in the atomic (single-rank) form only");
     const int t = threadIdx.x, lane = t & 63;
     const int wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (wave-uniform: the row's values live in SGPRs)
     const int a8 = lane >> 3, b8 = lane & 7;           // block entry (a, b) of this lane
@@ -416,8 +457,14 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         // S~ r0') from the neighbours' r0' (one exchange), its restriction summed per cluster (atomic buffer 2), y0' =
         // E^-1 R(d0), u0 = r0' + Z~ y0' and w0 = S~ u0 = r0' + off(S~ r0') + Z~ y0' + A y0' again without an exchange.
         // Three grid barriers; the coarse solves under the setup tags tag0 + maxit + 1 and + 2.
-        for (int q = blockIdx.x * kCgpThreads + t; q < 3 * m + 2 * 3 * nc; q += gridDim.x * kCgpThreads)
-            st_sc1(q < 3 * m ? tl.Racc + q : tl.Gacc + (q - 3 * m), 0.0);
+        // DET (deterministic mode, every rank of a replicated multi-rank CG): the cluster sums of the restrictions and
+        // of the scalar partials come from the run records (det_cluster_sums) instead of atomics -- d0's restriction in
+        // slots 3..11 of the parity-1 records (next written by iteration 1, behind three more barriers), iteration 0's
+        // scalars in slots 0..2 of parity 0.
+        if constexpr (!DET) {
+            for (int q = blockIdx.x * kCgpThreads + t; q < 3 * m + 2 * 3 * nc; q += gridDim.x * kCgpThreads)
+                st_sc1(q < 3 * m ? tl.Racc + q : tl.Gacc + (q - 3 * m), 0.0);
+        }
         if (blockIdx.x == 0 && t == 0) {
             cg.status[2] = use ? 1 : 0;  // reported as insfm_ba_stats.coarse_used
             if (cg.prog) __hip_atomic_store(cg.prog + 3, use ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -497,11 +544,13 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 x0 = zy_entry(la);
                 sx = lscale(seg_ay());  // entry la of off(S~) x0 = L_i^-1 sum_c B_ic y0_c
             }
-            const double r0p = V[VR + la] - x0 - sx;
+            const double r0 = V[VR + la];
+            const double r0p = r0 - x0 - sx;
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (lane < D) { V[VR + la] = r0p; V[VX + la] = x0; }
+            // (r0 itself parked in z, zeroed below: the stopping rule's reference ||L r0||^2 = ||b||^2 comes from it)
+            if (lane < D) { V[VR + la] = r0p; V[VX + la] = x0; V[VZ + la] = r0; }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -560,19 +609,24 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane >= 3 && lane < 3 + MC) {
                 double v = prt[rl][lane];
                 for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
-                unsafeAtomicAdd(tl.Racc + (size_t)2 * m + (size_t)ci * MC + (lane - 3), v);
+                if constexpr (DET) st_sc1(runs + (size_t)gridDim.x * kCgpRows * 12 + (size_t)pos * 12 + lane, v);
+                else unsafeAtomicAdd(tl.Racc + (size_t)2 * m + (size_t)ci * MC + (lane - 3), v);
             }
             alive = cgp_barrier(sync, ++epoch, &bflag);
         }
         // u0, w0 and the partials of iteration 0
         if (alive) {
             if (use) {
-                double rv[RPT];
+                if constexpr (DET) {
+                    det_cluster_sums<MC>(runs + (size_t)gridDim.x * kCgpRows * 12, 3, clp, nc, rs);
+                } else {
+                    double rv[RPT];
 #pragma unroll
-                for (int q = 0; q < RPT; ++q) rv[q] = ld_sc1(tl.Racc + (size_t)2 * m + min(t + q * kCgpThreads, m - 1));
+                    for (int q = 0; q < RPT; ++q) rv[q] = ld_sc1(tl.Racc + (size_t)2 * m + min(t + q * kCgpThreads, m - 1));
 #pragma unroll
-                for (int q = 0; q < RPT; ++q)
-                    if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+                    for (int q = 0; q < RPT; ++q)
+                        if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+                }
                 __syncthreads();
                 if (!coarse_solve(tag_s2)) alive = false;
             }
@@ -585,6 +639,11 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 const double r0p = V[VR + la];
                 const double u0 = r0p + zy;
                 const double w0 = r0p + off0 + zy + sa;  // S~ u0 (the diagonal block of S~ is I)
+                // the original r0 (parked in z above) for ||L r0||^2: iteration 0's rho, which the stopping rule keeps
+                // as its reference -- ||b||^2, as in the oracle (bb2) and the additive form, not ||L r0'||^2
+                double l8[D], r8[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) { l8[k] = Lrow[rl][la * D + k]; r8[k] = V[VZ + k]; }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -594,10 +653,6 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 double g0 = 0.0, g1 = 0.0, g2 = 0.0;
                 {
-                    double l8[D], r8[D];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) { l8[k] = Lrow[rl][la * D + k]; r8[k] = V[VR + k]; }
-                    __builtin_amdgcn_sched_barrier(0);
                     if (lane < D) {
                         g0 = r0p * u0;
                         g1 = w0 * u0;
@@ -613,11 +668,13 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 wave_sum3(g0, g1, g2);
                 if (lane == 0) { prt[rl][0] = g0; prt[rl][1] = g1; prt[rl][2] = g2; }
             }
+            if constexpr (DET) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (w0 before the runs' partials)
             __syncthreads();
             if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane < 3) {
                 double v = prt[rl][lane];
                 for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
-                unsafeAtomicAdd(tl.Gacc + (size_t)lane * nc + ci, v);
+                if constexpr (DET) st_sc1(runs + (size_t)pos * 12 + lane, v);  // (parity 0: iteration 0's scalars)
+                else unsafeAtomicAdd(tl.Gacc + (size_t)lane * nc + ci, v);
             }
             alive = cgp_barrier(sync, ++epoch, &bflag);
         }
@@ -808,45 +865,17 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         const int b0 = it % 3;  // partial sums of this iteration (P2 of it - 1 added them)
         double gl[3][LNC];
         if constexpr (DET) {
-            // every workgroup sums each cluster's 12 run partials of this iteration itself, in run order (the runs
-            // were stored before the grid barrier that ended the previous iteration, in its parity buffer): the same
-            // doubles in every workgroup, in a fixed order, no atomics
-            const double* rb = runs + (size_t)(it & 1) * gridDim.x * kCgpRows * 12;
-            constexpr int EPT = (12 * kCgpMaxClusters + kCgpThreads - 1) / kCgpThreads;
-            constexpr int RB = 6;  // run heads per cluster loaded at once (clusters with more take a second pass)
-            double x[EPT][RB];
-#pragma unroll
-            for (int q = 0; q < EPT; ++q) {
-                const int e = min(t + q * kCgpThreads, 12 * nc - 1), c = e / 12, k = e - 12 * c;
-                const int p1 = clp[c + 1];
-                int p = clp[c];
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {  // run heads: the cluster's first position, then every multiple of 4
-                    x[q][r] = ld_sc1(rb + (size_t)max(min(p, p1 - 1), 0) * 12 + k);  // (an empty first cluster: 0)
-                    if (p < p1) p = (p / kCgpRows + 1) * kCgpRows;
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < EPT; ++q) {
-                const int e0 = t + q * kCgpThreads, e = min(e0, 12 * nc - 1), c = e / 12, k = e - 12 * c;
-                const int p1 = clp[c + 1];
-                int p = clp[c];
-                double v = 0.0;
-#pragma unroll
-                for (int r = 0; r < RB; ++r) {
-                    if (p < p1) {
-                        v += x[q][r];
-                        p = (p / kCgpRows + 1) * kCgpRows;
-                    }
-                }
-                for (; p < p1; p = (p / kCgpRows + 1) * kCgpRows) v += ld_sc1(rb + (size_t)p * 12 + k);
-                if (e0 < 12 * nc) rs[e0] = v;
-            }
+            // every workgroup sums each cluster's run partials of this iteration itself, in run order (the runs were
+            // stored before the grid barrier that ended the previous iteration, in its parity buffer): the same doubles
+            // in every workgroup, in a fixed order, no atomics (A-DEF2: the 3 scalars; the additive form: the scalars
+            // and the restriction of w)
+            constexpr int NS = ADEF ? 3 : 12;
+            det_cluster_sums<NS>(runs + (size_t)(it & 1) * gridDim.x * kCgpRows * 12, 0, clp, nc, rs);
             __syncthreads();
 #pragma unroll
             for (int q = 0; q < LNC; ++q) {
                 const int c = min(lane + 64 * q, nc - 1);
-                gl[0][q] = rs[c * 12]; gl[1][q] = rs[c * 12 + 1]; gl[2][q] = rs[c * 12 + 2];
+                gl[0][q] = rs[c * NS]; gl[1][q] = rs[c * NS + 1]; gl[2][q] = rs[c * NS + 2];
             }
         } else {
             const double* G = tl.Gacc + (size_t)b0 * 3 * nc;
@@ -866,7 +895,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
 #pragma unroll
             for (int g = 0; g < NG; ++g) wv8[g] = ld_sc1(wsrc + (size_t)jr[g] * D);
         }
-        const double* Rv = tl.Racc + (size_t)b0 * m;
+        const double* Rv = DET ? nullptr : tl.Racc + (size_t)b0 * m;  // (DET: no atomic buffers)
         double rv[RPT];
 #pragma unroll
         for (int q = 0; q < RPT; ++q) rv[q] = (use && !DET && !ADEF) ? ld_sc1(Rv + min(t + q * kCgpThreads, m - 1)) : 0.0;
@@ -892,6 +921,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             const double den = (it == 0) ? del : del - be * gam / h_alpha;
             if (!(den > 0.0)) done = 2;
             else alpha = gam / den;
+            if (ADEF && (oseg & 4) && it == 2) done = 2;  // (INSFM_DIAG=adef2_breakdown: a breakdown, for the tests)
         }
         if (trace && blockIdx.x == 0 && t == 0 && it < 64) {  // INSFM_DIAG=cgp_trace
             trace[4 * it] = gam; trace[4 * it + 1] = del; trace[4 * it + 2] = rho; trace[4 * it + 3] = done;
@@ -1002,23 +1032,30 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
                 }
             }
             __syncthreads();
+            // (DET: slots 3..11 of this iteration's parity records; their last readers, iteration it - 2's, passed
+            // two grid barriers ago, and P1's readers of slots 0..2 of the same records do not touch them)
             if (has_row && (rl == 0 || pcl[rl - 1] != ci) && lane >= 3 && lane < 3 + MC) {
                 double v = prt[rl][lane];
                 for (int r2 = rl + 1; r2 < kCgpRows && pcl[r2] == ci; ++r2) v += prt[r2][lane];
-                unsafeAtomicAdd(tl.Racc + (size_t)b0 * m + (size_t)ci * MC + (lane - 3), v);
+                if constexpr (DET) st_sc1(runs + (size_t)(it & 1) * gridDim.x * kCgpRows * 12 + (size_t)pos * 12 + lane, v);
+                else unsafeAtomicAdd(tl.Racc + (size_t)b0 * m + (size_t)ci * MC + (lane - 3), v);
             }
             if (!(alive = cgp_barrier(sync, ++epoch, &bflag))) break;
             if (use) {
-                double rq0[RPT];
-#pragma unroll
-                for (int q = 0; q < RPT; ++q) rq0[q] = ld_sc1(Rv + min(t + q * kCgpThreads, m - 1));
                 if (gw < m) {
 #pragma unroll
                     for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
                 }
+                if constexpr (DET) {
+                    det_cluster_sums<MC>(runs + (size_t)(it & 1) * gridDim.x * kCgpRows * 12, 3, clp, nc, rs);
+                } else {
+                    double rq0[RPT];
 #pragma unroll
-                for (int q = 0; q < RPT; ++q)
-                    if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rq0[q];
+                    for (int q = 0; q < RPT; ++q) rq0[q] = ld_sc1(Rv + min(t + q * kCgpThreads, m - 1));
+#pragma unroll
+                    for (int q = 0; q < RPT; ++q)
+                        if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rq0[q];
+                }
                 __syncthreads();
                 if (gw < m) {
                     double rq[LPL];

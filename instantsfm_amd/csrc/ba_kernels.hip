@@ -1610,6 +1610,7 @@ struct insfm_ba {
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
     bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
     bool adef2 = false;                  // precond 2: k_tl_cgp applies the coarse correction as A-DEF2 (ba_cgp.h)
+    int adef2_fallbacks = 0;             // A-DEF2 solves that broke down and were repeated additively (adef2_fallback)
     double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
     int* cgp_src = nullptr;     // [n_nbr] S block of each CG slot: e (upper), ~e (lower, transposed), INT_MIN (pad)
     bool sn_valid = false;      // Sn holds the scaled S~ of the current solve (k_cg_scale ran for it)
@@ -2336,6 +2337,19 @@ void launch_tl_iter_x(insfm_ba* h, int it, int maxit, double tol2) {
     pspmv(it);
 }
 
+// The k_tl_cgp instantiation for NB blocks per row (64 / 128), the fixed-order form (det) and A-DEF2 (adef).
+using CgpKernel = void (*)(int, const int*, const int*, const double*, const int*, const double*, const double*, CgBufs,
+                           TlBufs, const double*, int, double, double*, unsigned long long*, unsigned, unsigned*, unsigned,
+                           int, double*, double*, double*, long long*);
+CgpKernel cgp_kernel(int nb, bool det, bool adef) {
+    if (nb == 64) {
+        if (det) return adef ? k_tl_cgp<64, true, true> : k_tl_cgp<64, true, false>;
+        return adef ? k_tl_cgp<64, false, true> : k_tl_cgp<64, false, false>;
+    }
+    if (det) return adef ? k_tl_cgp<128, true, true> : k_tl_cgp<128, true, false>;
+    return adef ? k_tl_cgp<128, false, true> : k_tl_cgp<128, false, false>;
+}
+
 // The whole two-level CG of a solve on the persistent k_tl_cgp (D = 8, h->cgp_nb > 0): one launch for the coarse
 // solve of r0 (u0 = M~^-1 r0, formerly k_tl_pc's setup launch), the setup's operator product and every iteration.
 int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
@@ -2346,23 +2360,15 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
     // INSFM_DIAG=cgp_fault (tests): the first launch of the process aborts at iteration 2
     static std::atomic<int> faults{diag("cgp_fault") ? 1 : 0};
     const bool fault = faults.load() > 0 && faults.fetch_sub(1) > 0;
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream, h->C, h->nbr_ptr, h->nbr_j, h->S,
-                           h->cgp_src, h->Li, h->Lf, h->cg, h->tl, h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
-                           h->cgp_tag, h->cgp_sync,
-                           h->cgp_epochs, (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0), h->cgp_runs, h->cgp_trace, h->dc,
-                           stamp_ptr(h, kStCgp));
-    };
-    if (h->cgp_det) {
-        if (h->cgp_nb == 64) go(k_tl_cgp<64, true>);
-        else go(k_tl_cgp<128, true>);
-    } else if (h->adef2) {
-        if (h->cgp_nb == 64) go(k_tl_cgp<64, false, true>);
-        else go(k_tl_cgp<128, false, true>);
-    } else {
-        if (h->cgp_nb == 64) go(k_tl_cgp<64, false>);
-        else go(k_tl_cgp<128, false>);
-    }
+    // INSFM_DIAG=adef2_breakdown (tests): the first A-DEF2 launch of the process reports a breakdown at iteration 2
+    static std::atomic<int> bkdn{diag("adef2_breakdown") ? 1 : 0};
+    const bool breakdown = h->adef2 && bkdn.load() > 0 && bkdn.fetch_sub(1) > 0;
+    hipLaunchKernelGGL(cgp_kernel(h->cgp_nb, h->cgp_det, h->adef2), dim3(h->cgp_grid), dim3(kCgpThreads), 0, h->stream,
+                       h->C, h->nbr_ptr, h->nbr_j, (const double*)h->S, (const int*)h->cgp_src, (const double*)h->Li,
+                       (const double*)h->Lf, h->cg, h->tl, (const double*)h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
+                       h->cgp_tag, h->cgp_sync, h->cgp_epochs,
+                       (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0) | (breakdown ? 4 : 0), h->cgp_runs, h->cgp_trace, h->dc,
+                       stamp_ptr(h, kStCgp));
     return launch_err(h, "k_tl_cgp");
 }
 
@@ -2861,6 +2867,31 @@ int cgp_collective_fallback(insfm_ba* h, int st0) {
     return reissue_chain(h);
 }
 
+// An A-DEF2 solve that broke down (k_tl_cgp status 2).  Its soundness rests on the coarse start x0 making
+// Z~^T r exactly zero, which holds only with the solve's own coarse inverse; under the lag rule E^-1 is the previous
+// solve's, the preconditioner is not symmetric on the iterates, and the single-reduction recurrence can break down.
+// The trial's solve is then repeated with the additive coarse correction (precond 1, symmetric for any SPD E^-1) on
+// the same handle: r0 = L^-1 b again from the completed S / b (k_cg_factor without U / g_c: the same L, L^-1 and r0),
+// the basis and the restriction of r0 (k_tl_basis), one additive k_tl_cgp launch.  Every rank of a replicated
+// multi-rank CG sees the same status (bitwise-equal fixed-order arithmetic), so every rank repeats it.
+int adef2_fallback(insfm_ba* h, int it_failed, int* st) {
+    std::fprintf(stderr, "[insfm] A-DEF2 PCG breakdown at iteration %d: the trial's solve is repeated with the additive "
+                         "coarse correction\n", it_failed);
+    ++h->adef2_fallbacks;
+    HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
+    int rc = with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg,
+                                                                       nullptr, nullptr, 1.0, 0.0, 0.0);
+        return launch_err(h, "k_cg_factor");
+    });
+    if (rc || (rc = run_tl_basis(h, h->cams_cur, h->stream))) return rc;
+    h->adef2 = false;
+    rc = run_tl_cg(h, st);
+    h->adef2 = true;
+    return rc;
+}
+
 // lm_step's accept rule for the trial being costed (k_publish copies an accepted trial into the caller's buffers)
 struct TrialAccept {
     double last;     // the loss before the step
@@ -2972,6 +3003,8 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
     const double last = h->loss;
     h->hmarks.clear();
     hmark(h, "step");
+    if (h->stamps)  // (this step's slot of the ring: a kernel not launched in the step reads 0, not a stamp of 1024 ago)
+        HIPCHK(hipMemsetAsync(stamp_ptr(h, 0), 0, sizeof(long long) * kStKinds * 2, h->stream));
     rec(h, 0);
     if ((rc = run_linearize(h, h->cams_cur, h->pts_cur))) return rc;
     hmark(h, "linearize enqueued");
@@ -3020,6 +3053,16 @@ int lm_step(insfm_ba* h, insfm_ba_stats* st) {
                 if ((rc = ensure_sn(h)) || (rc = run_tl_basis(h, h->cams_cur, h->stream)) || (rc = reissue_chain(h)) ||
                     (rc = run_tl_cg(h, st)))
                     return rc;
+                it = cg_tail(h, st);
+                if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
+                if (it < 0) return it;
+                if ((rc = solve_tail(h, f, h->cams_cur, h->pts_cur, h->dc))) return rc;
+                if ((rc = run_cost(h, h->cams_new, h->pts_new, true, h->scl_new, &ta))) return rc;
+            } else if (cst[0] == 2 && h->adef2) {
+                // A-DEF2 breakdown: this trial's solve again with the additive coarse correction (adef2_fallback),
+                // then its back-substitution and cost (k_publish rejected the first: its CG did not converge)
+                int* st = reinterpret_cast<int*>(h->host_res + 8);
+                if ((rc = adef2_fallback(h, cst[1], st))) return rc;
                 it = cg_tail(h, st);
                 if (it == INSFM_BA_ESOLVER) { failed = 1; h->loss = last; break; }
                 if (it < 0) return it;
@@ -3136,7 +3179,7 @@ void insfm_ba_default_desc(insfm_ba_desc* d) {
     d->pcg_tol = 1e-5;
     d->world_size = 1; d->rank = 0;
     d->shard_point_begin = 0; d->shard_point_end = -1;
-    d->precond = 1;
+    d->precond = 2;
     d->cluster_size = 24;
     d->exchange_chunks = 4;
 }
@@ -4011,16 +4054,16 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
         // rank of a replicated multi-rank CG) the fixed-order variant
         // (INSFM_DIAG=cgp_det: the fixed-order variant on a non-deterministic handle too, for A/B runs)
         const bool det = tl.Racc == nullptr || diag("cgp_det");
+        // precond 2 (A-DEF2) in either form (round 6: the fixed-order DET form too); the launch path runs the additive
+        // form of precond 1
+        const bool adef = desc->precond == 2;
         if (D == 8 && h->prog_host && nb && in_order && maxseg <= kCgpSegMax && !diag("no_cgp")) {
             int dev = 0, ncu = 0, per_cu = 0;
             hipError_t ce = hipGetDevice(&dev);
             if (ce == hipSuccess) ce = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
             if (ce == hipSuccess)
-                ce = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &per_cu,
-                    det ? (nb == 64 ? (const void*)k_tl_cgp<64, true> : (const void*)k_tl_cgp<128, true>)
-                        : (nb == 64 ? (const void*)k_tl_cgp<64, false> : (const void*)k_tl_cgp<128, false>),
-                    kCgpThreads, 0);
+                ce = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)cgp_kernel(nb, det, adef), kCgpThreads,
+                                                                  0);
             if (ce == hipSuccess && per_cu >= 1 && grid <= ncu) {
                 if ((rc = hand((void**)&h->cgp_wx, sizeof(double) * 2 * cd))) return fail(rc, "");
                 if ((rc = hand((void**)&h->cgp_yg, sizeof(unsigned long long) * 2 * kCoarseMax))) return fail(rc, "");
@@ -4046,8 +4089,7 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                     if ((rc = dd(&tl.Gb, cd * MC))) return fail(rc, "");
                 }
                 h->cgp_det = det;
-                // precond 2 (A-DEF2) runs in the atomic k_tl_cgp only; elsewhere the additive form of precond 1
-                h->adef2 = desc->precond == 2 && !det;
+                h->adef2 = adef;
                 h->cgp_nb = nb;
                 h->cgp_grid = grid;
                 h->cgp_slots = per_cu * ncu;
@@ -4112,11 +4154,16 @@ int insfm_ba_set_ranks_per_device(insfm_ba* h, int32_t ranks) {
 
 int insfm_ba_cg_info(const insfm_ba* h, int32_t* out) {
     if (!h || !out) return INSFM_BA_EINVAL;
-    out[0] = h->xpart ? 3 : h->cgp_nb ? (h->cgp_det ? 2 : (h->adef2 ? 4 : 1)) : 0;
+    out[0] = h->xpart ? 3 : h->cgp_nb ? (h->cgp_det ? (h->adef2 ? 5 : 2) : (h->adef2 ? 4 : 1)) : 0;
     out[1] = h->cgp_grid;
     out[2] = h->cgp_slots;
     out[3] = h->cgp_nb;
     return INSFM_BA_OK;
+}
+
+int32_t insfm_ba_cg_fallbacks(const insfm_ba* h) {
+    if (!h) return INSFM_BA_EINVAL;
+    return h->adef2_fallbacks;
 }
 
 int32_t insfm_ba_debug_stamps(insfm_ba* h, int64_t* host_out, int32_t max_steps) {

@@ -7,16 +7,121 @@
  *   collect(track_vals, min_len)  reads every Track's `observations` / `xyz` arrays in place (numpy C API) in one loop;
  *   finish(...)                   does the registered-image filter, the feature gather, the cheirality test
  *                                 (z of rotate_quat > 0.1, the same operations in the same order as numpy, no FMA
- *                                 contraction) and the torch.unique compaction, on all host cores.
+ *                                 contraction) and the torch.unique compaction, on the host cores.
  * collect returns None when an object is not the plain ndarray layout it expects (a Python list, another dtype or
- * shape); pack() then takes the numpy path, which gives the same result. */
+ * shape); pack() then takes the numpy path, which gives the same result.
+ *
+ * The parallel parts run on a small pthread pool whose idle workers block on a condition variable.  (Until round 5
+ * they were OpenMP regions: libgomp's idle workers spin for a while after every region (GOMP_SPINCOUNT), and on a host
+ * share of 16 cores that spinning slowed the GIL-held Python work right after the pack -- the engine creation and the
+ * 200k `track.xyz` assignments of the write-back -- by up to 2x) */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
 #include <numpy/arrayobject.h>
-#include <omp.h>
+#include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+/* ---- blocking worker pool -------------------------------------------------------------------------------------
+ * par_run(fn, ctx) calls fn(ctx, t, T) for t in [0, T) -- t = 0 on the caller -- and returns when all have finished.
+ * T = PACKX_THREADS, else OMP_NUM_THREADS (the GPU box sets it to its share of host cores), else the CPUs of the
+ * process's affinity mask; at most kMaxThreads.  The workers start on first use and live for the process; between
+ * jobs they sleep on a condition variable (no spinning).  Jobs come from one thread at a time (the GIL holder). */
+enum { kMaxThreads = 32 };
+typedef void (*par_fn)(void* ctx, int t, int T);
+static struct {
+    pthread_mutex_t m;
+    pthread_cond_t go, done;
+    int T, started;
+    long long gen, gen0;  /* job generation; its value when the workers started */
+    int pending;
+    par_fn fn;
+    void* ctx;
+} g_pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0, 0, 0, NULL, NULL};
+
+static int pool_threads(void) {
+    const char* e = getenv("PACKX_THREADS");
+    if (!e || !*e) e = getenv("OMP_NUM_THREADS");
+    int v = e && *e ? atoi(e) : 0;
+    if (v <= 0) {
+        cpu_set_t cs;
+        v = sched_getaffinity(0, sizeof(cs), &cs) == 0 ? CPU_COUNT(&cs) : 1;
+    }
+    return v < 1 ? 1 : (v > kMaxThreads ? kMaxThreads : v);
+}
+
+static void* pool_worker(void* arg) {
+    const int t = (int)(intptr_t)arg;
+    pthread_mutex_lock(&g_pool.m);
+    long long seen = g_pool.gen0;  /* (a job issued before this worker got here is still run) */
+    pthread_mutex_unlock(&g_pool.m);
+    for (;;) {
+        pthread_mutex_lock(&g_pool.m);
+        while (g_pool.gen == seen) pthread_cond_wait(&g_pool.go, &g_pool.m);
+        seen = g_pool.gen;
+        par_fn fn = g_pool.fn;
+        void* ctx = g_pool.ctx;
+        const int T = g_pool.T;
+        pthread_mutex_unlock(&g_pool.m);
+        fn(ctx, t, T);
+        pthread_mutex_lock(&g_pool.m);
+        if (--g_pool.pending == 0) pthread_cond_signal(&g_pool.done);
+        pthread_mutex_unlock(&g_pool.m);
+    }
+    return NULL;
+}
+
+/* A forked child has none of the parent's workers: it starts its own on first use. */
+static void pool_after_fork(void) {
+    pthread_mutex_init(&g_pool.m, NULL);
+    pthread_cond_init(&g_pool.go, NULL);
+    pthread_cond_init(&g_pool.done, NULL);
+    g_pool.started = 0;
+    g_pool.pending = 0;
+}
+
+/* The pool size (starting the workers on first use; a worker that cannot be started shrinks the pool). */
+static int pool_size(void) {
+    static int atfork = 0;
+    if (!atfork) atfork = pthread_atfork(NULL, NULL, pool_after_fork) == 0;
+    if (!g_pool.started) {
+        g_pool.started = 1;
+        g_pool.gen0 = g_pool.gen;
+        const int want = pool_threads();
+        int n = 1;
+        for (int t = 1; t < want; ++t) {
+            pthread_t th;
+            pthread_attr_t at;
+            pthread_attr_init(&at);
+            pthread_attr_setdetachstate(&at, PTHREAD_CREATE_DETACHED);
+            const int rc = pthread_create(&th, &at, pool_worker, (void*)(intptr_t)t);
+            pthread_attr_destroy(&at);
+            if (rc != 0) break;
+            ++n;
+        }
+        g_pool.T = n;
+    }
+    return g_pool.T;
+}
+
+static void par_run(par_fn fn, void* ctx) {
+    const int T = pool_size();
+    if (T == 1) { fn(ctx, 0, 1); return; }
+    pthread_mutex_lock(&g_pool.m);
+    g_pool.fn = fn;
+    g_pool.ctx = ctx;
+    g_pool.pending = T - 1;
+    ++g_pool.gen;
+    pthread_cond_broadcast(&g_pool.go);
+    pthread_mutex_unlock(&g_pool.m);
+    fn(ctx, 0, T);
+    pthread_mutex_lock(&g_pool.m);
+    while (g_pool.pending > 0) pthread_cond_wait(&g_pool.done, &g_pool.m);
+    pthread_mutex_unlock(&g_pool.m);
+}
 
 static PyObject *s_obs = NULL, *s_xyz = NULL;  /* interned attribute names */
 
@@ -39,6 +144,33 @@ static int xyz_kind(PyObject* o) {
     if (PyArray_NDIM(a) != 1 || PyArray_DIM(a, 0) != 3 || !PyArray_IS_C_CONTIGUOUS(a) || !PyArray_ISNOTSWAPPED(a)) return 0;
     const int t = PyArray_TYPE(a);
     return t == NPY_FLOAT64 ? 8 : (t == NPY_FLOAT32 ? 4 : 0);
+}
+
+struct copy_ctx {
+    Py_ssize_t T;
+    long long min_len;
+    const int64_t* lengths;
+    const int64_t* dst_off;
+    const void** src;
+    const unsigned char* kind;
+    int64_t* out;
+};
+
+/* worker t of T: tracks [T_tracks * t / T, T_tracks * (t + 1) / T) */
+static void copy_obs(void* p, int t, int T) {
+    const struct copy_ctx* c = (const struct copy_ctx*)p;
+    const Py_ssize_t a = (Py_ssize_t)((long long)c->T * t / T), b = (Py_ssize_t)((long long)c->T * (t + 1) / T);
+    for (Py_ssize_t k = a; k < b; ++k) {
+        if (c->lengths[k] < c->min_len) continue;
+        const Py_ssize_t n = 2 * c->lengths[k];
+        int64_t* o = c->out + c->dst_off[k];
+        if (c->kind[k] == 8) {
+            memcpy(o, c->src[k], sizeof(int64_t) * (size_t)n);
+        } else {
+            const int32_t* s32 = (const int32_t*)c->src[k];
+            for (Py_ssize_t q = 0; q < n; ++q) o[q] = s32[q];
+        }
+    }
 }
 
 /* collect(track_vals, min_len) -> (lengths int64[T], obs int64[n, 2] of the tracks with >= min_len observations,
@@ -96,22 +228,11 @@ static PyObject* collect(PyObject* self, PyObject* args) {
     obb = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(sizeof(int64_t) * 2 * (size_t)nvalid));
     if (!obb) goto done;
     {
-        /* the copy from the 200k arrays (references held in ob[]) on all host cores, without the GIL: every track
-         * writes its own slice of the output, so the result is the sequential loop's */
-        int64_t* out = (int64_t*)PyBytes_AS_STRING(obb);
+        /* the copy from the 200k arrays (references held in ob[]) on the pool, without the GIL: every track writes its
+         * own slice of the output, so the result is the sequential loop's */
+        struct copy_ctx cc = {(Py_ssize_t)T, min_len, lengths, dst_off, src, kind, (int64_t*)PyBytes_AS_STRING(obb)};
         Py_BEGIN_ALLOW_THREADS
-        #pragma omp parallel for schedule(static, 1024)
-        for (Py_ssize_t t = 0; t < T; ++t) {
-            if (lengths[t] < min_len) continue;
-            const Py_ssize_t n = 2 * lengths[t];
-            int64_t* o = out + dst_off[t];
-            if (kind[t] == 8) {
-                memcpy(o, src[t], sizeof(int64_t) * (size_t)n);
-            } else {
-                const int32_t* s32 = (const int32_t*)src[t];
-                for (Py_ssize_t k = 0; k < n; ++k) o[k] = s32[k];
-            }
-        }
+        par_run(copy_obs, &cc);
         Py_END_ALLOW_THREADS
     }
     res = PyTuple_Pack(3, lb, obb, xb);
@@ -150,6 +271,84 @@ static int get_buf(PyObject* o, Py_buffer* b, char kind, const char* what) {
         return -1;
     }
     return 0;
+}
+
+/* finish's three passes over the observations; worker t of T takes observations [n t / T, n (t + 1) / T) */
+struct fin_ctx {
+    const int64_t *obs, *foff, *tid;
+    const uint8_t* reg;
+    const double *feat, *pts, *pose;
+    int64_t n, nI, nF;
+    int stride;
+    int* bad;
+    uint8_t* ok;
+    char *pc, *pp;
+    int64_t *cnt, *cmap, *pmap, *oci, *opi;
+    double* o2d;
+    int32_t *oc32, *op32;
+};
+
+static void fin_check(void* p, int t, int T) {
+    const struct fin_ctx* c = (const struct fin_ctx*)p;
+    const int64_t a = c->n * t / T, b = c->n * (t + 1) / T;
+    int bad = 0;
+    for (int64_t k = a; k < b; ++k) {
+        const int64_t im = c->obs[2 * k];
+        if (im < 0 || im >= c->nI) { bad |= 1; continue; }
+        if (c->reg[im]) {
+            const int64_t f = c->foff[im] + c->obs[2 * k + 1];
+            if (c->obs[2 * k + 1] < 0 || f >= c->foff[im + 1] || f >= c->nF) bad |= 2;
+        }
+    }
+    c->bad[t] = bad;
+}
+
+static void fin_cheirality(void* p, int t, int T) {
+    const struct fin_ctx* c = (const struct fin_ctx*)p;
+    const int64_t a = c->n * t / T, b = c->n * (t + 1) / T;
+    int64_t cn = 0;
+    for (int64_t k = a; k < b; ++k) {
+        const int64_t im = c->obs[2 * k];
+        uint8_t keep = 0;
+        if (c->reg[im]) {
+            const double* X = c->pts + 3 * c->tid[k];
+            const double* Q = c->pose + (int64_t)c->stride * im;
+            const double px = X[0], py = X[1], pz = X[2];
+            const double qx = Q[3], qy = Q[4], qz = Q[5], w = Q[6];
+            const double uvx = qy * pz - qz * py;
+            const double uvy = qz * px - qx * pz;
+            const double uvz = qx * py - qy * px;
+            const double z = pz + 2.0 * (w * uvz + (qx * uvy - qy * uvx)) + Q[2];
+            keep = z > 0.1;
+        }
+        c->ok[k] = keep;
+        /* the flags are written only when not yet set: every thread marks the same ~1000 image bytes, and
+         * unconditional stores would ping-pong their cache lines between cores */
+        if (keep) {
+            if (!c->pc[im]) c->pc[im] = 1;
+            if (!c->pp[c->tid[k]]) c->pp[c->tid[k]] = 1;
+            ++cn;
+        }
+    }
+    c->cnt[t + 1] = cn;
+}
+
+static void fin_write(void* p, int t, int T) {
+    const struct fin_ctx* c = (const struct fin_ctx*)p;
+    const int64_t a = c->n * t / T, b = c->n * (t + 1) / T;
+    int64_t w = c->cnt[t];
+    for (int64_t k = a; k < b; ++k) {
+        if (!c->ok[k]) continue;
+        const int64_t im = c->obs[2 * k];
+        const double* fp = c->feat + 2 * (c->foff[im] + c->obs[2 * k + 1]);
+        c->o2d[2 * w] = fp[0];
+        c->o2d[2 * w + 1] = fp[1];
+        c->oci[w] = c->cmap[im];
+        c->opi[w] = c->pmap[c->tid[k]];
+        c->oc32[w] = (int32_t)c->cmap[im];
+        c->op32[w] = (int32_t)c->pmap[c->tid[k]];
+        ++w;
+    }
 }
 
 /* finish(obs int64[n,2], lengths int64[T], min_len, registered uint8[I], features float64[F,2], foff int64[I+1],
@@ -206,57 +405,30 @@ static PyObject* finish(PyObject* self, PyObject* args) {
                 for (int64_t q = 0; q < len[t]; ++q) tid[k++] = t;
             }
         }
+        const int nth = pool_size();
+        struct fin_ctx fc;
+        memset(&fc, 0, sizeof(fc));
+        fc.obs = obs; fc.reg = reg; fc.feat = feat; fc.foff = foff; fc.pts = pts; fc.pose = pose; fc.tid = tid;
+        fc.n = n; fc.nI = nI; fc.nF = nF; fc.stride = stride;
         int bad = 0;
-        #pragma omp parallel for schedule(static) reduction(|:bad)
-        for (int64_t k = 0; k < n; ++k) {
-            const int64_t im = obs[2 * k];
-            if (im < 0 || im >= nI) { bad |= 1; continue; }
-            if (reg[im]) {
-                const int64_t f = foff[im] + obs[2 * k + 1];
-                if (obs[2 * k + 1] < 0 || f >= foff[im + 1] || f >= nF) bad |= 2;
-            }
+        {
+            int badv[kMaxThreads] = {0};
+            fc.bad = badv;
+            par_run(fin_check, &fc);
+            for (int t = 0; t < nth; ++t) bad |= badv[t];
         }
         if (bad) {
             PyErr_SetString(PyExc_IndexError, (bad & 1) ? "finish: image id out of range" : "finish: feature id out of range");
             goto done;
         }
-        const int nth = omp_get_max_threads();
         cnt = (int64_t*)PyMem_Calloc((size_t)nth + 1, sizeof(int64_t));
         pc = (char*)PyMem_Calloc((size_t)(nI > 0 ? nI : 1), 1);
         pp = (char*)PyMem_Calloc((size_t)(nT > 0 ? nT : 1), 1);
         uint8_t* ok = (uint8_t*)PyMem_Malloc((size_t)(n > 0 ? n : 1));
         if (!cnt || !pc || !pp || !ok) { PyMem_Free(ok); PyErr_NoMemory(); goto done; }
         /* cheirality: z of rotate_quat(points[tid], pose[img]) exactly as _rotated_z's numpy expression */
-        #pragma omp parallel num_threads(nth)
-        {
-            const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
-            const int64_t a = n * t / T_, b = n * (t + 1) / T_;
-            int64_t c = 0;
-            for (int64_t k = a; k < b; ++k) {
-                const int64_t im = obs[2 * k];
-                uint8_t keep = 0;
-                if (reg[im]) {
-                    const double* X = pts + 3 * tid[k];
-                    const double* Q = pose + (int64_t)stride * im;
-                    const double px = X[0], py = X[1], pz = X[2];
-                    const double qx = Q[3], qy = Q[4], qz = Q[5], w = Q[6];
-                    const double uvx = qy * pz - qz * py;
-                    const double uvy = qz * px - qx * pz;
-                    const double uvz = qx * py - qy * px;
-                    const double z = pz + 2.0 * (w * uvz + (qx * uvy - qy * uvx)) + Q[2];
-                    keep = z > 0.1;
-                }
-                ok[k] = keep;
-                /* the flags are written only when not yet set: every thread marks the same ~1000 image bytes, and
-                 * unconditional stores would ping-pong their cache lines between cores */
-                if (keep) {
-                    if (!pc[im]) pc[im] = 1;
-                    if (!pp[tid[k]]) pp[tid[k]] = 1;
-                    ++c;
-                }
-            }
-            cnt[t + 1] = c;
-        }
+        fc.ok = ok; fc.pc = pc; fc.pp = pp; fc.cnt = cnt;
+        par_run(fin_cheirality, &fc);
         for (int t = 0; t < nth; ++t) cnt[t + 1] += cnt[t];
         const int64_t m = cnt[nth];
         /* compaction maps */
@@ -280,29 +452,13 @@ static PyObject* finish(PyObject* self, PyObject* args) {
         int64_t* up = (int64_t*)PyByteArray_AS_STRING(bup);
         for (int64_t i = 0, r = 0; i < nI; ++i) { cmap[i] = r; if (pc[i]) uc[r++] = i; }
         for (int64_t i = 0, r = 0; i < nT; ++i) { pmap[i] = r; if (pp[i]) up[r++] = i; }
-        double* o2d = (double*)PyByteArray_AS_STRING(b2d);
-        int64_t* oci = (int64_t*)PyByteArray_AS_STRING(bci);
-        int64_t* opi = (int64_t*)PyByteArray_AS_STRING(bpi);
-        int32_t* oc32 = (int32_t*)PyByteArray_AS_STRING(bc32);
-        int32_t* op32 = (int32_t*)PyByteArray_AS_STRING(bp32);
-        #pragma omp parallel num_threads(nth)
-        {
-            const int t = omp_get_thread_num(), T_ = omp_get_num_threads();
-            const int64_t a = n * t / T_, b = n * (t + 1) / T_;
-            int64_t w = cnt[t];
-            for (int64_t k = a; k < b; ++k) {
-                if (!ok[k]) continue;
-                const int64_t im = obs[2 * k];
-                const double* fp = feat + 2 * (foff[im] + obs[2 * k + 1]);
-                o2d[2 * w] = fp[0];
-                o2d[2 * w + 1] = fp[1];
-                oci[w] = cmap[im];
-                opi[w] = pmap[tid[k]];
-                oc32[w] = (int32_t)cmap[im];
-                op32[w] = (int32_t)pmap[tid[k]];
-                ++w;
-            }
-        }
+        fc.cmap = cmap; fc.pmap = pmap;
+        fc.o2d = (double*)PyByteArray_AS_STRING(b2d);
+        fc.oci = (int64_t*)PyByteArray_AS_STRING(bci);
+        fc.opi = (int64_t*)PyByteArray_AS_STRING(bpi);
+        fc.oc32 = (int32_t*)PyByteArray_AS_STRING(bc32);
+        fc.op32 = (int32_t*)PyByteArray_AS_STRING(bp32);
+        par_run(fin_write, &fc);
         PyMem_Free(cmap); PyMem_Free(pmap); PyMem_Free(ok);
         res = PyTuple_Pack(7, b2d, bci, bpi, buc, bup, bc32, bp32);
         Py_DECREF(b2d); Py_DECREF(bci); Py_DECREF(bpi); Py_DECREF(buc); Py_DECREF(bup);

@@ -13,10 +13,13 @@ import torch
 
 from . import _capi
 
-# TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.
+# TrustRegion / LM / PCG options TorchBA passes (bundle_adjustment.py:116-119) + pypose defaults it relies on.  The
+# preconditioner is the product's (TorchBA.Solve, bench.py): precond 2, the A-DEF2 coarse correction wherever the
+# persistent CG runs (k_tl_cgp, D = 8: single rank, deterministic mode and every rank of a multi-rank run), the additive
+# form of precond 1 elsewhere (effective_precond).
 LM_DEFAULTS = dict(tr_radius=1e4, tr_max=1e10, tr_min=1e-6, tr_up=2.0, tr_down=0.5 ** 4, tr_factor=0.25,
                    tr_high=0.5, tr_low=1e-3, clamp_min=1e-6, clamp_max=1e32, max_rejects=30, pcg_tol=1e-5,
-                   pcg_max_iter=500, precond=1, cluster_size=24, exchange_chunks=4)
+                   pcg_max_iter=500, precond=2, cluster_size=24, exchange_chunks=4)
 
 
 # insfm_ba_debug_stamps' kernel order (ba_common.h StampKind)
@@ -24,7 +27,19 @@ STAMP_KERNELS = ("k_lin_points", "k_schur", "k_tl_cgp", "k_cg_finish", "k_publis
                  "k_backsub_rc", "k_cost", "k_final")
 CG_PATHS = {0: "launch-per-iteration two-level CG", 1: "k_tl_cgp (persistent, atomic cluster sums)",
             2: "k_tl_cgp (persistent, fixed-order)", 3: "row-partitioned CG",
-            4: "k_tl_cgp (persistent, atomic cluster sums, A-DEF2 coarse correction: precond 2)"}
+            4: "k_tl_cgp (persistent, atomic cluster sums, A-DEF2 coarse correction: precond 2)",
+            5: "k_tl_cgp (persistent, fixed-order, A-DEF2 coarse correction: precond 2)"}
+# the persistent-CG paths (k_tl_cgp) and the fixed-order ones a replicated multi-rank CG may keep
+CGP_PATHS = (1, 2, 4, 5)
+CGP_DET_PATHS = (2, 5)
+
+
+def effective_precond(requested, path):
+    """The preconditioner a handle runs: A-DEF2 (2) only on the persistent CG's A-DEF2 paths (4, 5); a request for 2
+    runs the additive form (1) on the launch path; 0 and 1 as requested."""
+    if path in (4, 5):
+        return 2
+    return min(int(requested), 1)
 
 
 def device_key(device):
@@ -47,7 +62,8 @@ def cg_path_decision(allv):
     most shared GPU, keep k_tl_cgp).  The same list on every rank gives the same answer on every rank."""
     keys = [a[0] for a in allv]
     rpd = max(keys.count(k) for k in keys)
-    keep = all(a[1] == 2 for a in allv) and all(keys.count(a[0]) * a[2] <= a[3] for a in allv)
+    paths = {a[1] for a in allv}
+    keep = len(paths) == 1 and paths <= set(CGP_DET_PATHS) and all(keys.count(a[0]) * a[2] <= a[3] for a in allv)
     return rpd, keep
 
 
@@ -56,7 +72,8 @@ def agree_cg_path(handle, device, group=None):
     (the persistent k_tl_cgp and the launch path sum S~ m in different orders, so mixed paths would give dc that differ
     in rounding and replicated cameras that drift apart silently).  Every rank all-gathers its device key and
     insfm_ba_cg_info (its own eligibility: grid, slots, INSFM_DIAG, the host-mapped progress word ...); k_tl_cgp stays
-    only if every rank runs its fixed-order form and every GPU holds the grids of all ranks placed on it at once.
+    only if every rank runs the same fixed-order form (additive or A-DEF2) and every GPU holds the grids of all ranks
+    placed on it at once.
     Returns (ranks on the most shared GPU, the agreed path code)."""
     import torch.distributed as dist
     L = _capi.load()
@@ -66,7 +83,7 @@ def agree_cg_path(handle, device, group=None):
     allv = [None] * dist.get_world_size(group)
     dist.all_gather_object(allv, me, group=group)
     rpd, keep = cg_path_decision(allv)
-    if not keep and int(info[0]) in (1, 2):
+    if not keep and int(info[0]) in CGP_PATHS:
         _capi.check(handle, L.insfm_ba_set_persistent_cg(handle, 0))
     _capi.check(handle, L.insfm_ba_cg_info(handle, info))
     return rpd, int(info[0])
@@ -351,15 +368,19 @@ class BundleAdjuster:
         return tuple(int(x) for x in info)
 
     def debug_time_cgp(self, reps=10):
-        """The persistent CG (k_tl_cgp) of the last solve re-run `reps` times: (us per k_tl_cgp launch, us per k_tl_pc
-        setup launch, PCG iterations per solve); None when this handle does not run k_tl_cgp
-        (insfm_ba_debug_time_cgp)."""
+        """The persistent CG (k_tl_cgp) of the last solve re-run `reps` times: (us per k_tl_cgp launch, reserved (always
+        0: the setup launch it once timed now runs inside k_tl_cgp), PCG iterations per solve); None when this handle
+        does not run k_tl_cgp (insfm_ba_debug_time_cgp)."""
         out = (ctypes.c_double * 3)()
         rc = _capi.load().insfm_ba_debug_time_cgp(self._h, int(reps), out)
         if rc == _capi.INSFM_BA_EINVAL:
             return None
         _capi.check(self._h, rc)
         return float(out[0]), float(out[1]), float(out[2])
+
+    def adef2_fallbacks(self):
+        """A-DEF2 solves of this handle that broke down and were repeated additively (insfm_ba_cg_fallbacks)."""
+        return int(_capi.check(self._h, _capi.load().insfm_ba_cg_fallbacks(self._h)))
 
     def nnzb(self):
         return int(_capi.load().insfm_ba_nnzb(self._h))
@@ -385,7 +406,8 @@ class BundleAdjuster:
 
 # TorchGP.Optimize's LM (global_positioning.py:158-161): TrustRegion(radius=1e3, max=1e8, up=2, down=1/16), PCG(1e-5),
 # Huber(GLOBAL_POSITIONER_OPTIONS['thres_loss_function'] = 0.1), reject=30.
-GP_DEFAULTS = dict(LM_DEFAULTS, tr_radius=1e3, tr_max=1e8)
+# (the additive two-level form: global positioning has D = 3 and runs the launch-per-iteration CG)
+GP_DEFAULTS = dict(LM_DEFAULTS, tr_radius=1e3, tr_max=1e8, precond=1)
 
 
 class GlobalPositioner(BundleAdjuster):

@@ -9,7 +9,7 @@ import time
 import numpy as np
 import torch
 
-from ..engine import BundleAdjuster
+from ..engine import BundleAdjuster, effective_precond
 from ..scene.defs import CameraModelId, IMPLEMENTED_MODELS, get_camera_model_info
 
 
@@ -311,11 +311,10 @@ class TorchBA:
                              huber_delta=opts['thres_loss_function'], deterministic=opts.get('deterministic', False),
                              precond=opts.get('precond', 2),
                              **{k: opts[k] for k in ('pcg_max_iter', 'pcg_tol') if k in opts})
-        # the preconditioner the engine runs: A-DEF2 (precond 2) where the persistent CG has that form (D = 8,
-        # non-deterministic), else the additive two-level form (insfm_ba_cg_info path codes, engine.CG_PATHS)
+        # the preconditioner the engine runs: A-DEF2 (precond 2) where the persistent CG runs (D = 8), else the
+        # additive two-level form (insfm_ba_cg_info path codes, engine.CG_PATHS / effective_precond)
         self.cg_path = eng.cg_info()[0]
-        want = opts.get('precond', 2)
-        self.precond_effective = 2 if self.cg_path == 4 else min(want, 1)
+        self.precond_effective = effective_precond(opts.get('precond', 2), self.cg_path)
         dev = torch.device(self.device)
         cams_t = torch.from_numpy(packed.camera_params).to(dev).contiguous()
         pts_t = torch.from_numpy(packed.points_3d).to(dev).contiguous()

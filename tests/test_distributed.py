@@ -123,6 +123,10 @@ def test_ranks_per_device(buses, expect):
     ([(1, 2, 250, 256), (2, 0, 250, 256)], (1, False)),      # one rank ineligible (e.g. INSFM_DIAG=no_cgp there)
     ([(1, 2, 250, 256), (2, 2, 250, 240)], (1, False)),      # one GPU with fewer CUs (a partition mode)
     ([(1, 1, 250, 256), (2, 2, 250, 256)], (1, False)),      # a rank on the atomic (non-deterministic) form
+    ([(1, 5, 250, 256), (2, 5, 250, 256)], (1, True)),       # the fixed-order A-DEF2 form everywhere (round 6)
+    ([(1, 5, 50, 256), (1, 5, 50, 256)], (2, True)),
+    ([(1, 5, 250, 256), (2, 2, 250, 256)], (1, False)),      # A-DEF2 on one rank, additive on another
+    ([(1, 4, 250, 256), (2, 4, 250, 256)], (1, False)),      # the atomic A-DEF2 form is not replicable
 ])
 def test_cg_path_decision(infos, expect):
     """engine.cg_path_decision: the replicated multi-rank CG keeps k_tl_cgp only when every rank runs its

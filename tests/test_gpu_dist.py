@@ -40,12 +40,16 @@ def _run(nproc, backend, extra, timeout=600, diag=None):
 def test_two_ranks_match_single_gpu(extra):
     """[S | b] exchanged in 4 row chunks behind the Schur build (the async callback, default) or in one all-reduce."""
     out = _run(2, "gloo", extra)
+    if "clusters" in out:  # (the ranks and the reference run the same coarse space)
+        assert out["labels_equal"] and out["clusters"] == out["ref_clusters"], out
     assert out["loss_rel"] < 1e-9, out
     assert out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
     assert out["cams_equal_across_ranks"], out
     if extra[0] == "--small":  # two 6-workgroup persistent grids fit on the shared GPU: the replicated fixed-order
         assert out["ranks_per_device"] == 2, out  # k_tl_cgp on both ranks, one launch per solve, bitwise-equal ranks
         assert out["cg_launches"] == out["trials"], out
+        # the product default precond 2 as the fixed-order A-DEF2 k_tl_cgp on both ranks and on the reference
+        assert all(list(p) == [5, 5] for p in out["cg_paths"]) and out["ref_cg_path"] == 5, out
     assert abs(out["rmse"] - out["ref_rmse"]) < 1e-6, out
     if "scales_rel" in out:
         assert out["scales_rel"] < 1e-7, out
@@ -54,12 +58,14 @@ def test_two_ranks_match_single_gpu(extra):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("nproc", [2, 4])
 def test_config2_replicated_persistent_cg(nproc):
-    """the production multi-rank CG -- every rank runs the replicated fixed-order k_tl_cgp (config 2:
-    50-workgroup grids, which fit 2 and 4 times on the one MI355X of the test box) with the chunked exchange: one CG
-    launch per trial on every rank, bitwise-equal cameras across ranks, loss 1e-9 / parameters 1e-7 against one GPU."""
+    """the production multi-rank CG -- every rank runs the replicated fixed-order k_tl_cgp
+    with the A-DEF2 coarse correction (path 5; config 2: 50-workgroup grids, which fit 2 and 4 times on the one MI355X
+    of the test box) with the chunked exchange: one CG launch per trial on every rank, bitwise-equal cameras across
+    ranks, loss 1e-9 / parameters 1e-7 against one GPU running the same (deterministic A-DEF2) form."""
     out = _run(nproc, "gloo", ["--config", "2", "--steps", "3"])
     assert out["ranks_per_device"] == nproc, out
-    assert all(list(p) == [2, 2] for p in out["cg_paths"]), out  # fixed-order k_tl_cgp agreed, kept through the steps
+    assert all(list(p) == [5, 5] for p in out["cg_paths"]), out  # fixed-order A-DEF2 k_tl_cgp agreed, kept
+    assert out["ref_cg_path"] == 5 and out["precond_effective"] == 2, out
     assert out["cg_launches"] == out["trials"], out
     assert out["cams_equal_across_ranks"], out
     assert out["loss_rel"] < 1e-9, out
@@ -84,7 +90,7 @@ def test_cgp_abort_on_one_rank_is_collective():
     the persistent CG and repeats the solve on the launch path from r0.  The run completes, the ranks stay bitwise
     equal, and it matches one GPU."""
     out = _run(2, "gloo", ["--config", "2", "--steps", "3", "--diag-rank", "1", "--diag", "cgp_fault"])
-    assert all(list(p) == [2, 0] for p in out["cg_paths"]), out  # k_tl_cgp agreed at create, launch path after the abort
+    assert all(list(p) == [5, 0] for p in out["cg_paths"]), out  # k_tl_cgp agreed at create, launch path after the abort
     assert out["cams_equal_across_ranks"], out
     assert out["loss_rel"] < 1e-9 and out["cams_rel"] < 1e-7 and out["points_rel"] < 1e-7, out
 
@@ -114,9 +120,11 @@ def test_rccl_exchange_one_rank(chunks):
     """The RCCL ("nccl") branches of the exchange callbacks (engine.make_allreduce_callback and, with chunks > 1, the
     asynchronous make_allreduce_async_callback on the library's exchange stream) on a device tensor: one rank with the
     callbacks forced on, so every all-reduce of the camera system runs through RCCL; the result must equal the plain
-    single-GPU run (a 1-rank sum is the identity)."""
+    single-GPU run (a 1-rank sum is the identity) bitwise: the exchange handle and the plain handle run the same
+    arithmetic at the default cluster target (here one coarse cluster)."""
     out = _run(1, "nccl", ["--small", "--steps", "4", "--force-exchange", "--exchange-chunks", str(chunks)], timeout=280)
     assert out["backend"] == "nccl" and out["world"] == 1
+    assert out["clusters"] == out["ref_clusters"] == 1 and out["labels_equal"], out
     assert out["exchange_calls"] >= 4 * 3, out  # per step: [U|g_c], [S|b] per trial, the 5 result scalars
     assert out["loss_rel"] < 1e-12 and out["cams_rel"] < 1e-12 and out["points_rel"] < 1e-12, out
 
@@ -128,10 +136,16 @@ def test_partitioned_cg_matches_replicated(extra):
     CG partials into every rank's IPC exchange window; 2 ranks sharing the one MI355X) against the replicated CG on the
     same shards: bitwise the same losses and parameters on every rank, and the usual agreement with one GPU.  The
     partitioned CG is the launch-per-iteration path, so the replicated reference runs that path too (INSFM_DIAG=no_cgp:
-    the persistent k_tl_cgp sums S~ m in another order)."""
+    the persistent k_tl_cgp sums S~ m in another order).  The partition splits at cluster boundaries, so the 24-camera
+    scene runs at cluster target 12 (two clusters: one per rank) -- every handle of the run, the single-GPU reference
+    included (--cluster-size)."""
+    if extra[0] == "--small":
+        extra = extra + ["--cluster-size", "12"]
     rep = _run(2, "gloo", extra, diag="no_cgp")
     part = _run(2, "gloo", extra + ["--cg-partition"])
     assert part["cg_partition"] and part["rows"][0] == 0 and 0 < part["rows"][1], part
+    if extra[0] == "--small":
+        assert part["clusters"] == 2 and part["rows"][1] < 24, part  # both ranks own rows
     assert part["losses_hex"] == rep["losses_hex"], (part["losses_hex"], rep["losses_hex"])
     assert part["params_sha"] == rep["params_sha"], (part, rep)
     assert part["pcg_iters"] == rep["pcg_iters"], (part["pcg_iters"], rep["pcg_iters"])

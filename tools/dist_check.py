@@ -21,7 +21,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from instantsfm_amd.engine import BundleAdjuster, GlobalPositioner  # noqa: E402
+from instantsfm_amd.engine import LM_DEFAULTS, BundleAdjuster, GlobalPositioner, effective_precond  # noqa: E402
 from instantsfm_amd.shard import shard_ranges  # noqa: E402
 from instantsfm_amd.synth import make_config, make_gp_problem, make_problem  # noqa: E402
 
@@ -89,6 +89,8 @@ def main():
                     help="row chunks of the [S | b] exchange behind the Schur build (1: one all-reduce after it)")
     ap.add_argument("--diag-rank", type=int, default=-1, help="set INSFM_DIAG=--diag on this rank only")
     ap.add_argument("--diag", default="")
+    ap.add_argument("--cluster-size", type=int, default=0,
+                    help="coarse cluster target of every handle, the single-GPU reference included (0: the default)")
     args = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     if rank == args.diag_rank:  # (read by the library once, at its first diagnostic query)
@@ -105,9 +107,8 @@ def main():
         dist.destroy_process_group()
         return
     prob = make_problem(24, 900, seed=9) if args.small else make_config(args.config)
-    # the 24-camera scene in two coarse clusters, so the row-partitioned CG gives both ranks rows (it splits at cluster
-    # boundaries; the default target of 24 makes this scene one cluster); the single-GPU reference uses the same
-    ckw = {"cluster_size": 12} if args.small else {}
+    # every handle -- the ranks' and the single-GPU reference's -- runs the same cluster target (default or --cluster-size)
+    ckw = {"cluster_size": args.cluster_size} if args.cluster_size > 0 else {}
     shards = shard_ranges(prob.pt_idx, prob.n_points, world)
     eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points, device=dev,
                          world_size=world, rank=rank, shard=shards[rank], deterministic=True,
@@ -147,10 +148,13 @@ def main():
         cams_all = [c.cpu() for c in cams_all]
     paths = [None] * world  # (agreed at create, after the steps) per rank
     dist.all_gather_object(paths, (path0, eng.cg_info()[0]))
+    # the preconditioner the ranks ran: A-DEF2 on the persistent CG, the additive form on the launch path (ranks that
+    # share a GPU, an ineligible rank, after an abort); the single-GPU reference runs the same
+    eff = effective_precond(LM_DEFAULTS["precond"], eng.cg_info()[0])
     if rank == 0:
         os.environ.pop("INSFM_DIAG", None)
         ref = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
-                             device=dev, deterministic=True, **ckw)
+                             device=dev, deterministic=True, precond=eff, **ckw)
         rc = torch.from_numpy(prob.cams_init.copy()).to(dev)
         rp = torch.from_numpy(prob.points_init.copy()).to(dev)
         ref_losses = [ref.step(rc, rp)[0] for _ in range(args.steps)]
@@ -160,6 +164,9 @@ def main():
                    loss_rel=max(abs(a - b) / b for a, b in zip(losses, ref_losses)),
                    cams_rel=rel(cams.cpu().numpy(), rcn), points_rel=rel(full.numpy(), rpn),
                    rmse=rmse, ref_rmse=ref_rmse, exchange_calls=eng.exchange_calls[0], n_obs=int(prob.n_obs),
+                   clusters=eng.clusters()[1], ref_clusters=ref.clusters()[1], precond_effective=eff,
+                   ref_cg_path=ref.cg_info()[0],
+                   labels_equal=bool(np.array_equal(eng.clusters()[0], ref.clusters()[0])),
                    cg_partition=bool(args.cg_partition), rows=rows, pcg_iters=iters, xchg_us=xchg_us,
                    ranks_per_device=getattr(eng, "ranks_per_device", 1), cg_launches=launches, trials=trials,
                    losses_hex=[float(x).hex() for x in losses], cg_paths=paths,

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Device vs host derivation of the Schur block pattern and the co-visibility graph in insfm_ba_create
 (INSFM_DIAG=pattern_host selects the host pass; read once per process).  For a few scenes -- config 2, a scene with
-duplicated observations (two observations of one track on one camera) and one with a camera that sees nothing --
+duplicated observations (two observations of one track on one camera), one with a camera that sees nothing and the
+24-camera scene of the multi-rank tests (one coarse cluster) --
 prints one JSON line with the block count, the two-level cluster labels and the bits of three deterministic LM steps.
 Run twice by tests/test_gpu_parity.py::test_device_block_pattern_matches_host_pass and compared."""
 import hashlib
@@ -32,6 +33,8 @@ def scenes():
     keep = prob.cam_idx != 7  # camera 7 sees nothing
     prob.uv, prob.cam_idx, prob.pt_idx = (np.ascontiguousarray(a[keep]) for a in (prob.uv, prob.cam_idx, prob.pt_idx))
     yield "empty_camera", prob
+    # the multi-rank tests' 24-camera scene (tools/dist_check.py --small): one coarse cluster at the default target
+    yield "dist_small", make_problem(24, 900, seed=9)
 
 
 def main():
