@@ -316,7 +316,9 @@ typedef struct {
     double *W, *V, *gp, *U, *gc, *Vinv, *y, *S, *b, *Minv, *x, *r, *z, *p, *q, *dp;
     double *cams_new, *pts_new, *partial;
     /* stats of the last step: trials, pcg iters (last trial), total pcg iters, f */
-    double stats[8];
+    double stats[9];  /* trials, pcg last, pcg total, damping factor, damping, failed, rejects, coarse used,
+                         A-DEF2 solves of the step repeated with the additive correction (breakdown) */
+    int adef2_fallbacks;  /* (since the last ora_step) */
 } ora_t;
 
 static double det_sum_order(const double* v, size_t n, int reverse) {
@@ -1143,7 +1145,7 @@ int ora_pcg(ora_t* h, double* xout) {
      * x0 = Z~ E^-1 Z~^T r0 (with that start A-DEF2 has BNN's iterates in exact arithmetic, which keeps the
      * single-reduction recurrence sound; from x0 = 0 it broke down on config 3).  Config 3, 10 LM steps: 213 -> 111
      * iterations, the same RMSE. */
-    const int adef2 = h->precond == 2;
+    int adef2 = h->precond == 2;
     double* tdef = adef2 ? (double*)malloc(sizeof(double) * n) : NULL;
     const int pipelined = twolev;  /* the two-level path uses the pipelined recurrence (with or without a usable E) */
     double *Zt = NULL, *Einv = NULL, *Rc = NULL, *yc = NULL, *u = h->r;
@@ -1170,6 +1172,10 @@ int ora_pcg(ora_t* h, double* xout) {
         h->fresh_lin = 0;
         if (!okc) twolev = 0;
     }
+    /* A-DEF2 breakdown (the recurrence's denominator <= 0: possible under the lag rule, whose E^-1 is the previous
+     * solve's, so Z~^T r is not exactly zeroed by the coarse start): the solve is repeated from r0 with the additive
+     * correction (pass 1), as the GPU's adef2_fallback does. */
+    for (int pass = 0;; ++pass) {
     for (int i = 0; i < C; ++i) {
         const double* Li = h->Minv + (size_t)i * DD;
         for (int a = 0; a < D; ++a) {
@@ -1239,6 +1245,11 @@ int ora_pcg(ora_t* h, double* xout) {
             rho = dot(rt, rt, n, tmp);
         }
         free(mv); free(nv); free(qv); free(zv);
+        if (fail && twolev && adef2 && pass == 0) {
+            adef2 = 0;
+            h->adef2_fallbacks++;
+            continue;
+        }
         free(tdef);
         free(rt);
         free(Lfac);
@@ -1288,6 +1299,7 @@ int ora_pcg(ora_t* h, double* xout) {
         }
         rho = dot(rt, rt, n, tmp);
     }
+    free(tdef);
     free(rt);
     free(Lfac);
     if (Zt) { free(Zt); free(Einv); free(Rc); free(yc); free(u); }
@@ -1303,6 +1315,7 @@ int ora_pcg(ora_t* h, double* xout) {
         }
     }
     return k;
+    }  /* (pass) */
 }
 
 /* back-substitution: dp = Vinv (g_p - sum_o W_o^T dc_{c(o)}) */
@@ -1382,6 +1395,7 @@ int ora_step(ora_t* h, double* cams, double* pts, double* loss_out) {
     if (!h->have_loss) { h->loss = ora_cost(h, cams, pts, NULL); h->have_loss = 1; }
     double last = h->loss;
     ora_linearize(h, cams, pts);
+    h->adef2_fallbacks = 0;
     double f = 1.0;
     int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
     for (;;) {
@@ -1423,7 +1437,7 @@ int ora_step(ora_t* h, double* cams, double* pts, double* loss_out) {
         break;
     }
     h->stats[0] = trials; h->stats[1] = pcg_last; h->stats[2] = pcg_total; h->stats[3] = f;
-    h->stats[4] = h->damping; h->stats[5] = failed; h->stats[6] = rejects;
+    h->stats[4] = h->damping; h->stats[5] = failed; h->stats[6] = rejects; h->stats[8] = h->adef2_fallbacks;
     *loss_out = h->loss;
     return 0;
 }
@@ -1664,6 +1678,7 @@ int ora_gp_step(ora_t* h, double* cams, double* pts, double* scales, double* los
     if (!h->have_loss) { h->loss = ora_gp_cost(h, cams, pts, scales, NULL); h->have_loss = 1; }
     const double last = h->loss;
     ora_gp_linearize(h, cams, pts, scales);
+    h->adef2_fallbacks = 0;
     double f = 1.0;
     int rejects = 0, trials = 0, pcg_total = 0, pcg_last = 0, failed = 0;
     for (;;) {
@@ -1696,7 +1711,7 @@ int ora_gp_step(ora_t* h, double* cams, double* pts, double* scales, double* los
         break;
     }
     h->stats[0] = trials; h->stats[1] = pcg_last; h->stats[2] = pcg_total; h->stats[3] = f;
-    h->stats[4] = h->damping; h->stats[5] = failed; h->stats[6] = rejects;
+    h->stats[4] = h->damping; h->stats[5] = failed; h->stats[6] = rejects; h->stats[8] = h->adef2_fallbacks;
     *loss_out = h->loss;
     return 0;
 }

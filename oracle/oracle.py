@@ -166,10 +166,10 @@ class OracleBA:
         return loss.value
 
     def stats(self):
-        s = np.zeros(8)
+        s = np.zeros(9)
         self.L.ora_stats(self.h, _d(s))
         return dict(trials=int(s[0]), pcg_iters=int(s[1]), pcg_total=int(s[2]), damp_factor=s[3],
-                    damping=s[4], failed=int(s[5]), rejects=int(s[6]), coarse_used=int(s[7]))
+                    damping=s[4], failed=int(s[5]), rejects=int(s[6]), coarse_used=int(s[7]), adef2_fallbacks=int(s[8]))
 
     def cost(self, cams, pts):
         sq = ctypes.c_double()

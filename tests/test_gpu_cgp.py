@@ -1,7 +1,7 @@
 """The persistent register-resident CG (ba_cgp.h k_tl_cgp) against the launch-per-iteration two-level CG.
 
-Both run the same pipelined two-level recurrence (oracle/ba_oracle.c ora_pcg) in non-deterministic mode (per-cluster
-atomic partial sums); they differ only in the summation order inside S~ m, so LM trajectories agree to rounding:
+Both run the same pipelined two-level recurrence (oracle/ba_oracle.c ora_pcg) with the additive coarse correction
+(precond 1: the launch path has no A-DEF2 form) in non-deterministic mode (per-cluster atomic partial sums); they differ only in the summation order inside S~ m, so LM trajectories agree to rounding:
 losses within 1e-8 relative, PCG iteration counts within one per step.  INSFM_DIAG is read once per process, so each
 path runs in its own process (tools/cgp_check.py).  The oracle parity of the path itself is test_gpu_parity.py's
 test_solve_parity / test_step_parity (non-deterministic D = 8 cases run k_tl_cgp where it is eligible).
@@ -56,6 +56,23 @@ def test_cgp_deterministic_variant():
         s1, s2, sb = a[name], a[name + "#1"], b[name]
         assert s1["launches"] == s1["trials"], s1
         assert s1["losses_hex"] == s2["losses_hex"] and s1["params_sha"] == s2["params_sha"], (s1, s2)
+        for la, lb in zip(s1["losses"], sb["losses"]):
+            assert abs(la - lb) <= 1e-8 * abs(lb), (name, la, lb)
+        assert all(abs(x - y) <= 1 for x, y in zip(s1["iters"], sb["iters"])), (s1["iters"], sb["iters"])
+
+
+def test_cgp_deterministic_adef2_bitwise():
+    """the fixed-order A-DEF2 k_tl_cgp (path 5, the product default precond 2 in deterministic mode
+    and on every rank of a multi-rank run) is bitwise reproducible run to run, one launch per solve, and agrees with
+    the atomic A-DEF2 form (path 4) to rounding: losses 1e-8, PCG iterations within one per step."""
+    a = run("", "--det", "--repeat", "2", "--precond", "2", scenes="small,config2")
+    b = run("", "--precond", "2", scenes="small,config2")
+    for name in ("small", "config2"):
+        s1, s2, sb = a[name], a[name + "#1"], b[name]
+        assert s1["path"] == 5 and sb["path"] == 4, (s1, sb)
+        assert s1["launches"] == s1["trials"], s1
+        assert s1["losses_hex"] == s2["losses_hex"] and s1["params_sha"] == s2["params_sha"], (s1, s2)
+        assert not any(s1["failed"]) and not any(sb["failed"]), (s1, sb)
         for la, lb in zip(s1["losses"], sb["losses"]):
             assert abs(la - lb) <= 1e-8 * abs(lb), (name, la, lb)
         assert all(abs(x - y) <= 1 for x, y in zip(s1["iters"], sb["iters"])), (s1["iters"], sb["iters"])

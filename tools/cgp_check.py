@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--det", action="store_true", help="deterministic mode (the fixed-order k_tl_cgp variant)")
     ap.add_argument("--repeat", type=int, default=1, help="run each scene this many times (bitwise reproducibility)")
+    ap.add_argument("--precond", type=int, default=1,
+                    help="1: the additive form both CG paths run (default); 2: A-DEF2 (k_tl_cgp only)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     out = dict(env=os.environ.get("INSFM_DIAG", ""), scenes={})
@@ -46,7 +48,7 @@ def main():
         if a.det:
             opts = dict(opts, deterministic=True)
         eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
-                             device=dev, **opts)
+                             device=dev, precond=a.precond, **opts)
         cg = torch.from_numpy(prob.cams_init.copy()).to(dev)
         pg = torch.from_numpy(prob.points_init.copy()).to(dev)
         eng.step(cg, pg)  # warm-up (first-touch allocations, code objects)
@@ -68,7 +70,7 @@ def main():
         key = name if name not in out["scenes"] else f"{name}#{sum(k.split('#')[0] == name for k in out['scenes'])}"
         out["scenes"][key] = dict(params_sha=hashlib.sha256(cg.cpu().numpy().tobytes() + pg.cpu().numpy().tobytes()).hexdigest(),
                                    losses_hex=[float(x).hex() for x in losses],losses=losses, iters=iters, launches=launches, trials=trials, failed=failed, nc=nc,
-                                   steps_per_s=a.steps / dt, D=eng.D)
+                                   steps_per_s=a.steps / dt, D=eng.D, path=eng.cg_info()[0])
         eng.close()
         print(json.dumps(dict(scene=key, **out["scenes"][key])), file=sys.stderr, flush=True)
     print(json.dumps(out), flush=True)
