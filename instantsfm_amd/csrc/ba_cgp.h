@@ -226,7 +226,8 @@ __device__ __forceinline__ void det_cluster_sums(const double* rb, int off, cons
 // counted so far (one per iteration of earlier launches); oseg bit 0: also write this solve's coarse segments tl.Oseg
 // (the E build behind the CG then skips k_tl_erow), bit 1 (tests, INSFM_DIAG=cgp_fault): the last workgroup leaves
 // at iteration 2 as if a barrier had timed out, bit 2 (tests, INSFM_DIAG=adef2_breakdown): an A-DEF2 launch reports a
-// breakdown (status 2) at iteration 2;
+// breakdown (status 2) at iteration 2, bit 3: the restriction of r0 comes from k_tl_basis (tl.Rc) instead of
+// k_cg_factor_basis's run records;
 // dcout (non-null): the camera step dc = L^-T x~ written at the end (k_cg_finish's arithmetic);
 // trace (diagnostics, normally null): gamma, delta, rho, done of the first 64 iterations, then wall-clock ticks (100 MHz)
 // of the launch start, the setup's end and each iteration's start, then per iteration the ticks around its two grid
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     __shared__ double vec[kCgpRows][8][D];             // the row's r u w z q s p x
     __shared__ int jn[kCgpWaves][NB];                  // neighbour of each register block
     __shared__ int segc[kCgpRows][kCgpSegMax];         // neighbour cluster of each segment
-    __shared__ int clp[DET ? kCgpMaxClusters + 1 : 1];  // DET: the clusters' cluster-ordered position ranges
+    __shared__ int clp[kCgpMaxClusters + 1];          // the clusters' cluster-ordered position ranges
     __shared__ double prt[kCgpRows][12];               // each row's partials: r.u, w.u, ||L r||^2, Z~_i^T w (9)
     __shared__ int pcl[kCgpRows];                      // each row's cluster (-1: no row)
     __shared__ int bflag;
@@ -327,8 +328,7 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     const size_t own = (size_t)(has_row ? row : 0) * D + (lane & 7);
     {
         if (lane < nseg && lane < kCgpSegMax) segc[rl][lane] = tl.seg[s0 + lane].x;
-        if constexpr (DET)
-            for (int i = t; i <= nc; i += kCgpThreads) clp[i] = tl.cl_ptr[i];
+        for (int i = t; i <= nc; i += kCgpThreads) clp[i] = tl.cl_ptr[i];
         if (has_row) {
             Lrow[rl][lane] = Lf[(size_t)row * D * D + lane];
             Lirow[rl][lane] = Li[(size_t)row * D * D + lane];
@@ -425,6 +425,15 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
     const int ci = has_row ? tl.clab[row] : 0;
     if (lane == 0) pcl[rl] = has_row ? ci : -1;
     const bool use = tl.ok[0] != 0;
+    // R(r0) into rs: the cluster sums of k_cg_factor_basis's run partials (parity-1 run records, slots 3..11, summed in
+    // run order), or with oseg bit 3 k_tl_basis's per-cluster sums tl.Rc (the separate launches; FACTOR_BASIS=0)
+    auto r0_restriction = [&]() {
+        if (oseg & 8) {
+            for (int q = t; q < m; q += kCgpThreads) rs[q] = tl.Rc[q];
+        } else {
+            det_cluster_sums<MC>(runs + (size_t)gridDim.x * kCgpRows * 12, 3, clp, nc, rs);
+        }
+    };
     const double* erow = Einv + (size_t)min(gw, m - 1) * m;  // this wave's coarse row of E^-1 (read from L2)
     double h_alpha = 1.0, h_gam = 1.0, h_bb = 1.0;
     unsigned epoch = epoch0;
@@ -527,14 +536,9 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
         };
         const unsigned tag_s = tag0 + (unsigned)maxit + 1u, tag_s2 = tag0 + (unsigned)maxit + 2u;
         const int la = lane & 7;
-        // x0, r0'
+        // x0, r0' (R(r0): k_cg_factor_basis's run partials, summed per cluster in run order)
         if (use) {
-            double rv[RPT];
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) rv[q] = tl.Rc[min(t + q * kCgpThreads, m - 1)];
-#pragma unroll
-            for (int q = 0; q < RPT; ++q)
-                if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+            r0_restriction();
             __syncthreads();
             if (!coarse_solve(tag_s)) alive = false;
         }
@@ -695,22 +699,18 @@ __global__ __launch_bounds__(kCgpThreads, 1) void k_tl_cgp(int C, const int* __r
             cg.status[2] = use ? 1 : 0;  // reported as insfm_ba_stats.coarse_used
             if (cg.prog) __hip_atomic_store(cg.prog + 3, use ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        // R(r0) = k_tl_basis's cluster sums (tl.Rc, k_tl_pc's order); wave gw forms coarse row gw of y0 = E^-1 R
-        // (k_tl_pc's products and butterfly) and publishes it as tagged granules like an iteration's y, under the
-        // setup's own tag (tag0 + maxit + 1: never an iteration's); every workgroup polls all of y0
+        // R(r0) = the cluster sums of k_cg_factor_basis's run partials (parity-1 run records, slots 3..11, summed in
+        // run order: det_cluster_sums); wave gw forms coarse row gw of y0 = E^-1 R (k_tl_pc's products and butterfly)
+        // and publishes it as tagged granules like an iteration's y, under the setup's own tag (tag0 + maxit + 1:
+        // never an iteration's); every workgroup polls all of y0
         const unsigned tag_s = tag0 + (unsigned)maxit + 1u;
         if (use) {
-            double rv[RPT];
-#pragma unroll
-            for (int q = 0; q < RPT; ++q) rv[q] = tl.Rc[min(t + q * kCgpThreads, m - 1)];
             double ev[LPL];
             if (gw < m) {
 #pragma unroll
                 for (int q = 0; q < LPL; ++q) ev[q] = erow[min(lane + 64 * q, m - 1)];
             }
-#pragma unroll
-            for (int q = 0; q < RPT; ++q)
-                if (t + q * kCgpThreads < m) rs[t + q * kCgpThreads] = rv[q];
+            r0_restriction();
             __syncthreads();
             if (gw < m) {
                 double rq[LPL];

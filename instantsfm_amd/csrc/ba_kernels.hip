@@ -72,6 +72,11 @@ constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 /
 #ifndef SCHUR_SLOTPRE
 #define SCHUR_SLOTPRE 1  // k_schur: a round's partner slots looked up before its LDS adds
 #endif
+// the persistent CG's solves form the factorization and the coarse basis in one launch (k_cg_factor_basis; 0: the
+// separate k_cg_factor and k_tl_basis launches, for A/B builds)
+#ifndef FACTOR_BASIS
+#define FACTOR_BASIS 1
+#endif
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
@@ -614,6 +619,14 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
     }
 }
 
+// SCHUR_PROBE (timing-only builds for the floor model of DESIGN.md section 8, tools/schur_variants.sh; wrong results):
+//   1  the partner products summed in a register instead of the LDS atomics (gathers + FMAs, no ds_add_f64)
+//   2  the partner walk's loads only (records + camera indices; no slot lookup, no FMA, no LDS add)
+//   3  no partner-record gathers: the own record stands in for the partner's (camera index, slot lookup, FMAs and
+//      LDS adds as usual)
+#ifndef SCHUR_PROBE
+#define SCHUR_PROBE 0
+#endif
 template <int D, int WAVES, bool GPW = false, bool RETRY = false>
 __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
@@ -650,6 +663,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
     const bool active = g < NG;
     double* my_wh = wsh + (size_t)(wv * NG + (active ? g : 0)) * WS;
     double breg = 0.0;
+    double probe_sum = 0.0;  // (SCHUR_PROBE 1 / 2: keeps the probed work alive)
     const int ob = cam_ptr[i], oe = cam_ptr[i + 1];
     // per own observation one descriptor {o, p, partner begin, partner end}: one load gives every index, and the next
     // round's descriptor is loaded while the current round runs (the round chain is latency-bound, not byte-bound)
@@ -685,7 +699,8 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         for (int u = 0; u < UP; ++u) {
             cj[u] = -1;
             if (u < n) {
-                load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
+                if (SCHUR_PROBE == 3) { x[u][0] = w0; x[u][1] = w1; x[u][2] = w2; }
+                else load_wcol<D, GPW>(W, qs + u, cb, x[u][0], x[u][1], x[u][2]);
                 cj[u] = cam[qs + u];
             }
         }
@@ -727,11 +742,18 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     cj[u] = -1;
                     if (k0 + u < n) {
                         const int q = qs + k0 + u;
-                        load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
+                        if (SCHUR_PROBE == 3) { x[u][0] = w0 + k0; x[u][1] = w1; x[u][2] = w2; }
+                        else load_wcol<D, GPW>(W, q, cb, x[u][0], x[u][1], x[u][2]);
                         cj[u] = cam[q];
                     }
                 }
             }
+#if SCHUR_PROBE == 2
+#pragma unroll
+            for (int u = 0; u < UP; ++u)
+                if (cj[u] >= 0) probe_sum += x[u][0] + x[u][1] + x[u][2] + (double)cj[u];
+            continue;
+#endif
 #if SCHUR_SLOTPRE
             // every slot of the round looked up before the first ds_add_f64: one LDS wait per round instead of one
             // per partner (a slot read issued behind the previous partner's adds waits for them to retire)
@@ -753,8 +775,10 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                         double* dst = acc + (size_t)sl * BS + cb;
                         const double y0 = x[u][0], y1 = x[u][1], y2 = x[u][2];
 #pragma unroll
-                        for (int a2 = 0; a2 < D; ++a2)
-                            atomicAdd(dst + a2 * D, wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2);
+                        for (int a2 = 0; a2 < D; ++a2) {
+                            if (SCHUR_PROBE == 1) probe_sum += wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2;
+                            else atomicAdd(dst + a2 * D, wh[a2][0] * y0 + wh[a2][1] * y1 + wh[a2][2] * y2);
+                        }
                     }
                 }
             }
@@ -762,6 +786,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         __builtin_amdgcn_wave_barrier();
     }
     if (diag_chunk && active) atomicAdd(bacc + cb, breg);
+    if (SCHUR_PROBE != 0 && probe_sum == 1.2345e-300) acc[0] = probe_sum;  // (never true: a use of the probed sums)
     __syncthreads();
     double* Sout = S + (size_t)kb * DD;
     const double* Ui = U + (size_t)i * DD;
@@ -789,20 +814,18 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
 // U / g_c (`Ul` non-null): k_schur built S_ii and b_i without the camera terms (k_lin_cams ran beside it on another
 // stream), so they are added here -- S_ii += U_i with the diagonal clamped and scaled by the damping factor, b_i =
 // g_c + b_i, the same single additions k_schur makes -- and the completed block and right-hand side are written back.
+// One camera's factorization on one wave (k_cg_factor's work for camera i).  On return lane r < D holds row r of L_i in
+// a[] (zero above the diagonal) and column r of L_i^-1 in x[], and r0 = (L_i^-1 b_i)[lane] (0 when S_ii is not positive
+// definite: *ok false, the CG status raised to 2).
 template <int D>
-__global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, double* __restrict__ S,
-                                                        double* __restrict__ b, double* __restrict__ Lf,
-                                                        double* __restrict__ Li, CgBufs cg, const double* __restrict__ Ul,
-                                                        const double* __restrict__ gcl, double f, double cmin, double cmax,
-                                                        long long* stp = nullptr) {
-    const StampScope stamp_(stp);
+__device__ __forceinline__ void factor_camera(int i, int lane, const int* __restrict__ row_ptr, double* __restrict__ S,
+                                              double* __restrict__ b, double* __restrict__ Lf, double* __restrict__ Li,
+                                              CgBufs& cg, const double* __restrict__ Ul, const double* __restrict__ gcl,
+                                              double f, double cmin, double cmax, double (&a)[D], double (&x)[D],
+                                              double& r0out, bool& okout) {
     constexpr int DD = D * D;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int i = blockIdx.x * kWaves + wv;
-    if (i >= C) return;
     const int rl = min(lane, D - 1);
     double* blk = S + (size_t)row_ptr[i] * DD;
-    double a[D];
 #pragma unroll
     for (int c = 0; c < D; ++c) a[c] = blk[rl * D + c];
     double bl = b[(size_t)i * D + rl];
@@ -839,7 +862,6 @@ __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __rest
     for (int c = 0; c < D; ++c)
         if (c > lane) a[c] = 0.0;
     // column `lane` of L^-1: x[r] = (delta_rc - sum_{k<r} L[r][k] x[k]) / L[r][r]
-    double x[D];
 #pragma unroll
     for (int r = 0; r < D; ++r) {
         double s = 0.0;  // (x[k] = 0 for k < lane: those terms leave s unchanged)
@@ -871,6 +893,82 @@ __global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __rest
         cg.w[0][idx] = 0.0; cg.w[1][idx] = 0.0;
         cg.s[0][idx] = 0.0; cg.s[1][idx] = 0.0;
         cg.p[idx] = 0.0; cg.x[idx] = 0.0;
+    }
+    okout = ok;
+    r0out = ok ? r0 : 0.0;
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_factor(int C, const int* __restrict__ row_ptr, double* __restrict__ S,
+                                                        double* __restrict__ b, double* __restrict__ Lf,
+                                                        double* __restrict__ Li, CgBufs cg, const double* __restrict__ Ul,
+                                                        const double* __restrict__ gcl, double f, double cmin, double cmax,
+                                                        long long* stp = nullptr) {
+    const StampScope stamp_(stp);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int i = blockIdx.x * kWaves + wv;
+    if (i >= C) return;
+    double a[D], x[D], r0;
+    bool ok;
+    factor_camera<D>(i, lane, row_ptr, S, b, Lf, Li, cg, Ul, gcl, f, cmin, cmax, a, x, r0, ok);
+}
+
+// k_cg_factor and k_tl_basis in one launch (round 6), for the persistent CG (k_tl_cgp): the waves take the cameras in
+// cluster order -- workgroup g the four cameras k_tl_cgp's workgroup g holds -- and after its factorization each wave
+// forms its camera's basis (k_tl_basis's tl_basis_entry: lane k < D + 1 the column k of G_i, Z~_i = L_i^T G_i, the
+// restriction partial Z~_i[:,k]^T r0_i) from the factor still in its registers.  The restriction of r0 is summed per
+// cluster run of the workgroup (rows in order) into slots 3..11 of the run records `runs` (k_tl_cgp's parity-1 records,
+// which it sums per cluster in run order, det_cluster_sums) instead of k_tl_basis's per-cluster tl.Rc: one launch and
+// its gap less per solve.
+template <int D>
+__global__ __launch_bounds__(kThreads) void k_cg_factor_basis(int C, const int* __restrict__ row_ptr, double* __restrict__ S,
+                                                              double* __restrict__ b, double* __restrict__ Lf,
+                                                              double* __restrict__ Li, CgBufs cg,
+                                                              const double* __restrict__ Ul, const double* __restrict__ gcl,
+                                                              double f, double cmin, double cmax,
+                                                              const double* __restrict__ cams, TlBufs tl,
+                                                              double* __restrict__ runs, long long* stp = nullptr) {
+    static_assert(kWaves == kCgpRows, "k_cg_factor_basis's workgroups are k_tl_cgp's");
+    const StampScope stamp_(stp);
+    constexpr int MC = D + 1, ST = D + 1;  // (a BA camera row: pose [t, q] and D - 6 intrinsics)
+    __shared__ double prt[kWaves][MC];
+    __shared__ int pcl[kWaves];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int pos = blockIdx.x * kWaves + wv;
+    const bool has = pos < C;
+    const int i = has ? tl.cl_cams[pos] : 0;
+    double rr = 0.0;
+    if (has) {
+        double a[D], x[D], r0;
+        bool ok;
+        factor_camera<D>(i, lane, row_ptr, S, b, Lf, Li, cg, Ul, gcl, f, cmin, cmax, a, x, r0, ok);
+        const int k = min(lane, MC - 1);
+        double col[D];
+        basis_column<D>(k, cams + (size_t)i * ST, tl.alone[i] != 0, col);
+        const bool st = lane < MC;
+        const int cp = tl.cpos[i];
+#pragma unroll
+        for (int aa = 0; aa < D; ++aa) {
+            double sz = 0.0;  // Z~[aa][k] = sum_{l >= aa} L[l][aa] G[l][k] (tl_basis_entry's order)
+#pragma unroll
+            for (int l = aa; l < D; ++l) sz += readlane_d(a[aa], l) * col[l];
+            if (st) {
+                tl.Zt[((size_t)i * D + aa) * MC + k] = sz;
+                if (tl.Gb) tl.Gb[((size_t)i * D + aa) * MC + k] = col[aa];
+                tl.Ztc[((size_t)cp * D + aa) * MC + k] = sz;
+            }
+            rr += sz * readlane_d(r0, aa);
+        }
+        if (st) tl.rowR[(size_t)cp * MC + k] = rr;
+        if (lane < D) tl.vc[(size_t)cp * D + lane] = r0;
+    }
+    if (lane < MC) prt[wv][lane] = rr;
+    if (lane == 0) pcl[wv] = has ? tl.clab[i] : -1;
+    __syncthreads();
+    if (has && (wv == 0 || pcl[wv - 1] != pcl[wv]) && lane < MC) {
+        double v = prt[wv][lane];
+        for (int r2 = wv + 1; r2 < kWaves && pcl[r2] == pcl[wv]; ++r2) v += prt[r2][lane];
+        runs[(size_t)pos * 12 + 3 + lane] = v;
     }
 }
 
@@ -1610,6 +1708,7 @@ struct insfm_ba {
     int cgp_nb = 0, cgp_grid = 0, cgp_slot = 0;
     bool cgp_det = false;                // fixed-order partial sums (deterministic mode, multi-rank replicated CG)
     bool adef2 = false;                  // precond 2: k_tl_cgp applies the coarse correction as A-DEF2 (ba_cgp.h)
+    bool basis_by_factor = false;        // this solve's coarse basis was formed by k_cg_factor_basis
     int adef2_fallbacks = 0;             // A-DEF2 solves that broke down and were repeated additively (adef2_fallback)
     double* cgp_runs = nullptr;               // [2][grid * 4][12] the cluster runs' partials by parity (cgp_det)
     int* cgp_src = nullptr;     // [n_nbr] S block of each CG slot: e (upper), ~e (lower, transposed), INT_MIN (pad)
@@ -2243,7 +2342,7 @@ int side_flush(insfm_ba* h) {
 int run_tl_setup(insfm_ba* h, const double* cams) {
     const int slot = (int)(h->tl_solves & 1);
     if (h->timing) harvest_chain_time(h);
-    int rc = run_tl_basis(h, cams, h->stream);
+    int rc = h->basis_by_factor ? 0 : run_tl_basis(h, cams, h->stream);  // (k_cg_factor_basis formed it)
     if (rc) return rc;
     const int use = (h->tl_solves > 0 && h->tl_fresh) ? (slot ^ 1) : slot;
     h->tl_fresh = false;
@@ -2367,7 +2466,8 @@ int launch_tl_cgp(insfm_ba* h, int maxit, double tol2) {
                        h->C, h->nbr_ptr, h->nbr_j, (const double*)h->S, (const int*)h->cgp_src, (const double*)h->Li,
                        (const double*)h->Lf, h->cg, h->tl, (const double*)h->tl.Einv, maxit, tol2, h->cgp_wx, h->cgp_yg,
                        h->cgp_tag, h->cgp_sync, h->cgp_epochs,
-                       (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0) | (breakdown ? 4 : 0), h->cgp_runs, h->cgp_trace, h->dc,
+                       (h->cgp_defer ? 1 : 0) | (fault ? 2 : 0) | (breakdown ? 4 : 0) | (h->basis_by_factor ? 0 : 8),
+                       h->cgp_runs, h->cgp_trace, h->dc,
                        stamp_ptr(h, kStCgp));
     return launch_err(h, "k_tl_cgp");
 }
@@ -2770,11 +2870,22 @@ int run_solve(insfm_ba* h, double f, const double* cams, const double* pts_local
         // the CG takes the coarse segments k_tl_cgp writes) needs no scaled copy Sn; the first solve after a
         // linearization that factorizes its own E (k_tl_erow reads Sn), the launch-path CG and the debug getters do
         const bool scale = !(h->tlon && h->cgp_nb && h->tl_solves > 0 && h->tl_fresh && !h->keep_S);
+        // the persistent CG's solves: the factorization and the coarse basis in one launch (k_cg_factor_basis)
+        h->basis_by_factor = FACTOR_BASIS && h->tlon && h->cgp_nb && !gpk;
         rc = with_D(D, [&](auto dc_) -> int {
             constexpr int DV = decltype(dc_)::value;
-            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
-                h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
-                h->d.clamp_min, h->d.clamp_max, stamp_ptr(h, kStFactor));
+            if constexpr (DV != 3) {
+                if (h->basis_by_factor) {
+                    k_cg_factor_basis<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
+                        h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr,
+                        f, h->d.clamp_min, h->d.clamp_max, cams, h->tl, h->cgp_runs + (size_t)h->cgp_grid * kCgpRows * 12,
+                        stamp_ptr(h, kStFactor));
+                }
+            }
+            if (!h->basis_by_factor)
+                k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
+                    h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, ul ? h->U : nullptr, ul ? h->gc : nullptr, f,
+                    h->d.clamp_min, h->d.clamp_max, stamp_ptr(h, kStFactor));
             if (scale)
                 k_cg_scale<DV><<<cdiv(h->nnzb, kWaves * scale_nb(DV)), kThreads, 0, h->stream>>>(
                     h->nnzb, h->blk_row, h->col, h->row_ptr, h->pos_up, h->pos_lo, h->Li, h->S, h->Sn, 0);
@@ -2867,25 +2978,41 @@ int cgp_collective_fallback(insfm_ba* h, int st0) {
     return reissue_chain(h);
 }
 
+// The persistent CG's factorization and coarse basis again on the completed S / b (no U / g_c added: the same L,
+// L^-1 and r0 = L^-1 b): k_cg_factor_basis, or (FACTOR_BASIS=0 builds) k_cg_factor and k_tl_basis.
+int refactor_for_cgp(insfm_ba* h, const double* cams) {
+    const int rc = with_D(h->D, [&](auto dc_) -> int {
+        constexpr int DV = decltype(dc_)::value;
+        if constexpr (DV != 3) {
+            if (h->basis_by_factor) {
+                k_cg_factor_basis<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(
+                    h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg, nullptr, nullptr, 1.0, 0.0, 0.0, cams, h->tl,
+                    h->cgp_runs + (size_t)h->cgp_grid * kCgpRows * 12);
+                return launch_err(h, "k_cg_factor_basis");
+            }
+        }
+        k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg,
+                                                                       nullptr, nullptr, 1.0, 0.0, 0.0);
+        return launch_err(h, "k_cg_factor");
+    });
+    if (rc) return rc;
+    return h->basis_by_factor ? 0 : run_tl_basis(h, cams, h->stream);
+}
+
 // An A-DEF2 solve that broke down (k_tl_cgp status 2).  Its soundness rests on the coarse start x0 making
 // Z~^T r exactly zero, which holds only with the solve's own coarse inverse; under the lag rule E^-1 is the previous
 // solve's, the preconditioner is not symmetric on the iterates, and the single-reduction recurrence can break down.
 // The trial's solve is then repeated with the additive coarse correction (precond 1, symmetric for any SPD E^-1) on
-// the same handle: r0 = L^-1 b again from the completed S / b (k_cg_factor without U / g_c: the same L, L^-1 and r0),
-// the basis and the restriction of r0 (k_tl_basis), one additive k_tl_cgp launch.  Every rank of a replicated
+// the same handle: r0 = L^-1 b, the basis and the restriction of r0 again from the completed S / b
+// (refactor_for_cgp), one additive k_tl_cgp launch.  Every rank of a replicated
 // multi-rank CG sees the same status (bitwise-equal fixed-order arithmetic), so every rank repeats it.
 int adef2_fallback(insfm_ba* h, int it_failed, int* st) {
     std::fprintf(stderr, "[insfm] A-DEF2 PCG breakdown at iteration %d: the trial's solve is repeated with the additive "
                          "coarse correction\n", it_failed);
     ++h->adef2_fallbacks;
     HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
-    int rc = with_D(h->D, [&](auto dc_) -> int {
-        constexpr int DV = decltype(dc_)::value;
-        k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li, h->cg,
-                                                                       nullptr, nullptr, 1.0, 0.0, 0.0);
-        return launch_err(h, "k_cg_factor");
-    });
-    if (rc || (rc = run_tl_basis(h, h->cams_cur, h->stream))) return rc;
+    int rc = refactor_for_cgp(h, h->cams_cur);
+    if (rc) return rc;
     h->adef2 = false;
     rc = run_tl_cg(h, st);
     h->adef2 = true;
@@ -4073,10 +4200,10 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
                 if (hipMemsetAsync(h->cgp_sync, 0, sizeof(unsigned) * kCgpSyncWords, h->stream) != hipSuccess)
                     return fail(INSFM_BA_EHIP, "cgp barrier words");
                 if (diag("cgp_trace") && (rc = dd(&h->cgp_trace, kCgpTraceLen))) return fail(rc, "");
-                if (det) {
-                    if ((rc = hand((void**)&h->cgp_runs, sizeof(double) * 2 * 12 * (size_t)grid * kCgpRows)))
-                        return fail(rc, "");
-                }
+                // the run records: DET's partials by parity, and (every form) the restriction of r0 that
+                // k_cg_factor_basis writes for the setup
+                if ((rc = hand((void**)&h->cgp_runs, sizeof(double) * 2 * 12 * (size_t)grid * kCgpRows)))
+                    return fail(rc, "");
                 // k_tl_cgp holds S unscaled: the S block (and orientation) of every slot, and the unscaled basis
                 {
                     std::vector<int> src((size_t)std::max<int64_t>(h->n_nbr, 1), kCgpPadSlot);
@@ -4479,9 +4606,9 @@ int insfm_ba_debug_time_kernel(insfm_ba* h, int32_t which, int32_t reps, double*
 }
 
 int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out) {
-    // the persistent CG of the last solve again, `reps` times: k_cg_factor on the completed S / b (no U / g_c added:
-    // the same L, L^-1 and r0 = L^-1 b), k_tl_basis (Z~ and the restriction of r0), then the timed part -- k_tl_pc's
-    // k_tl_cgp launch, bracketed by events -- with the coarse segments written as in a lagged solve.  out[0] us per
+    // the persistent CG of the last solve again, `reps` times: k_cg_factor_basis on the completed S / b (no U / g_c
+    // added: the same L, L^-1 and r0 = L^-1 b; Z~ and the restriction of r0), then the timed part -- the k_tl_cgp
+    // launch, bracketed by events -- with the coarse segments written as in a lagged solve.  out[0] us per
     // k_tl_cgp launch, out[1] 0 (the setup launch k_tl_pc that preceded it until round 4 is folded in), out[2]
     // iterations (mean).
     if (!h || reps <= 0 || !out || !h->cgp_nb || h->kind != 0 || !h->prog_host) return INSFM_BA_EINVAL;
@@ -4493,14 +4620,7 @@ int insfm_ba_debug_time_cgp(insfm_ba* h, int32_t reps, double* out) {
     double t_cg = 0.0, t_pc = 0.0, iters = 0.0;
     for (int r = 0; r < reps; ++r) {
         HIPCHK(hipMemsetAsync(h->cg.status, 0, sizeof(int) * 4, h->stream));
-        const int rc = with_D(h->D, [&](auto dc_) -> int {
-            constexpr int DV = decltype(dc_)::value;
-            k_cg_factor<DV><<<cdiv(h->C, kWaves), kThreads, 0, h->stream>>>(h->C, h->row_ptr, h->S, h->b, h->Lf, h->Li,
-                                                                           h->cg, nullptr, nullptr, 1.0, 0.0, 0.0);
-            return launch_err(h, "k_cg_factor");
-        });
-        if (rc) return rc;
-        if (int rc2 = run_tl_basis(h, h->cams_new, h->stream)) return rc2;  // (the last trial's cameras)
+        if (int rc = refactor_for_cgp(h, h->cams_new)) return rc;  // (the last trial's cameras)
         volatile int* pg = h->prog_host;
         pg[0] = pg[1] = pg[2] = pg[3] = 0;
         std::atomic_thread_fence(std::memory_order_seq_cst);

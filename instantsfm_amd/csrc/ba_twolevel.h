@@ -100,54 +100,69 @@ __global__ __launch_bounds__(kThreads) void k_tl_basis(int C, const double* __re
     (void)C;
 }
 
+// Column k of a BA camera's G_i (D x (D + 1)): the response of its pose [rho, phi] and intrinsics to an infinitesimal
+// similarity of the world -- 3 translations (k < 3), 3 rotations (k < 6), scale (k = 6) -- then one unit column per
+// intrinsic; a camera alone in its cluster gets [I_D | 0].  cp: the camera row [t, q_xyzw, intrinsics].
+template <int D>
+__device__ __forceinline__ void basis_column(int k, const double* __restrict__ cp, bool alone, double (&col)[D]) {
+#pragma unroll
+    for (int a = 0; a < D; ++a) col[a] = 0.0;
+    if (alone) {
+        if (k < D) col[k] = 1.0;
+        return;
+    }
+    const double t0 = cp[0], t1 = cp[1], t2 = cp[2];
+    const double qx = cp[3], qy = cp[4], qz = cp[5], w = cp[6];
+    // R = I + 2w[q]x + 2[q]x^2 (same form as the retraction / projection)
+    const double K[9] = {0, -qz, qy, qz, 0, -qx, -qy, qx, 0};
+    double R[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double kk = 0.0;
+#pragma unroll
+            for (int l = 0; l < 3; ++l) kk += K[r * 3 + l] * K[l * 3 + c];
+            R[r * 3 + c] = (r == c ? 1.0 : 0.0) + 2.0 * w * K[r * 3 + c] + 2.0 * kk;
+        }
+    const double tx[9] = {0, -t2, t1, t2, 0, -t0, -t1, t0, 0};
+    if (k < 3) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) col[a] = -R[a * 3 + k];
+    } else if (k < 6) {
+        const int kk = k - 3;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < 3; ++l) s += tx[a * 3 + l] * R[l * 3 + kk];
+            col[a] = -s;
+            col[3 + a] = -R[a * 3 + kk];
+        }
+    } else if (k == 6) {
+        col[0] = t0; col[1] = t1; col[2] = t2;
+    } else {
+        col[6 + (k - 7)] = 1.0;
+    }
+}
+
 template <int M>
 __device__ __forceinline__ void tl_basis_entry(int i, int k, const double* __restrict__ cams, const double* __restrict__ Lf,
                                                const TlBufs& tl, const double* __restrict__ r0) {
     constexpr int D = kD<M>, MC = D + 1, ST = kStride<M>;
     double col[D];
+    if constexpr (M == kGP) {  // global positioning: translation (I) and scaling about the origin (c_i)
 #pragma unroll
-    for (int a = 0; a < D; ++a) col[a] = 0.0;
-    if (tl.alone[i]) {
-        if (k < D) col[k] = 1.0;
-    } else if constexpr (M == kGP) {  // global positioning: translation (I) and scaling about the origin (c_i)
-        const double* cp = cams + (size_t)i * ST;
-        if (k < 3) col[k] = 1.0;
-        else { col[0] = cp[0]; col[1] = cp[1]; col[2] = cp[2]; }
-    } else {
-        const double* cp = cams + (size_t)i * ST;
-        const double t0 = cp[0], t1 = cp[1], t2 = cp[2];
-        const double qx = cp[3], qy = cp[4], qz = cp[5], w = cp[6];
-        // R = I + 2w[q]x + 2[q]x^2 (same form as the retraction / projection)
-        const double K[9] = {0, -qz, qy, qz, 0, -qx, -qy, qx, 0};
-        double R[9];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                double kk = 0.0;
-#pragma unroll
-                for (int l = 0; l < 3; ++l) kk += K[r * 3 + l] * K[l * 3 + c];
-                R[r * 3 + c] = (r == c ? 1.0 : 0.0) + 2.0 * w * K[r * 3 + c] + 2.0 * kk;
-            }
-        const double tx[9] = {0, -t2, t1, t2, 0, -t0, -t1, t0, 0};
-        if (k < 3) {
-#pragma unroll
-            for (int a = 0; a < 3; ++a) col[a] = -R[a * 3 + k];
-        } else if (k < 6) {
-            const int kk = k - 3;
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                double s = 0.0;
-#pragma unroll
-                for (int l = 0; l < 3; ++l) s += tx[a * 3 + l] * R[l * 3 + kk];
-                col[a] = -s;
-                col[3 + a] = -R[a * 3 + kk];
-            }
-        } else if (k == 6) {
-            col[0] = t0; col[1] = t1; col[2] = t2;
+        for (int a = 0; a < D; ++a) col[a] = 0.0;
+        if (tl.alone[i]) {
+            if (k < D) col[k] = 1.0;
         } else {
-            col[6 + (k - 7)] = 1.0;
+            const double* cp = cams + (size_t)i * ST;
+            if (k < 3) col[k] = 1.0;
+            else { col[0] = cp[0]; col[1] = cp[1]; col[2] = cp[2]; }
         }
+    } else {
+        basis_column<D>(k, cams + (size_t)i * ST, tl.alone[i] != 0, col);
     }
     const double* L = Lf + (size_t)i * D * D;
     const double* r = r0 + (size_t)i * D;

@@ -19,6 +19,7 @@
 #include <Python.h>
 #define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
 #include <numpy/arrayobject.h>
+#include <malloc.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdint.h>
@@ -500,24 +501,36 @@ static PyObject* assign_xyz(PyObject* self, PyObject* args) {
     npy_intp dims[1] = {3};
     PyArray_Descr* d8 = PyArray_DescrFromType(NPY_FLOAT64);  /* (one lookup; each view takes a reference) */
     if (!d8) { Py_DECREF(fast); return NULL; }
+    /* Every assignment releases the track's previous xyz array; when those own their 24-byte buffers (a scene whose
+     * tracks were built one array each) 200k small free()s land in glibc's fastbins, and the next allocation of a
+     * kilobyte or more merges them all at once (malloc_consolidate: ~20 ms on this container's host, ~5 ms on the GPU
+     * box, paid by whatever allocates next).  For the duration of the loop the fastbins are off (mallopt(M_MXFAST, 0)
+     * consolidates what they hold and sends later frees to the regular bins), then the default is restored. */
+    mallopt(M_MXFAST, 0);
     for (npy_intp i = 0; i < n; ++i) {
         if (idx[i] < 0 || idx[i] >= T) {
             PyErr_SetString(PyExc_IndexError, "assign_xyz: track index");
             Py_DECREF(d8);
             Py_DECREF(fast);
+            mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);
             return NULL;
         }
         Py_INCREF(d8);
         PyObject* row = PyArray_NewFromDescr(&PyArray_Type, d8, 1, dims, NULL, base + 24 * i, NPY_ARRAY_CARRAY, NULL);
-        if (!row) { Py_DECREF(d8); Py_DECREF(fast); return NULL; }
+        if (!row) { Py_DECREF(d8); Py_DECREF(fast); mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4); return NULL; }
         Py_INCREF(o_pts);
-        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) { Py_DECREF(row); Py_DECREF(d8); Py_DECREF(fast); return NULL; }
+        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) {
+            Py_DECREF(row); Py_DECREF(d8); Py_DECREF(fast);
+            mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);
+            return NULL;
+        }
         const int r = PyObject_SetAttr(items[idx[i]], s_xyz, row);
         Py_DECREF(row);
-        if (r < 0) { Py_DECREF(d8); Py_DECREF(fast); return NULL; }
+        if (r < 0) { Py_DECREF(d8); Py_DECREF(fast); mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4); return NULL; }
     }
     Py_DECREF(d8);
     Py_DECREF(fast);
+    mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);  /* (glibc's DEFAULT_MXFAST) */
     Py_RETURN_NONE;
 }
 

@@ -56,17 +56,28 @@ def _quat_xyzw_from_matrix(R):
 
 
 def _pose_matrices(cam_rows):
-    """pp.SE3(rows[:, :7]).matrix(): the 4x4 of the action p -> p + 2w(q x p) + 2 q x (q x p) + t."""
-    t = cam_rows[:, 0:3]
-    qx, qy, qz, w = (cam_rows[:, 3 + k] for k in range(4))
+    """pp.SE3(rows[:, :7]).matrix(): the 4x4 of the action p -> p + 2w(q x p) + 2 q x (q x p) + t, i.e. the rotation
+    I + 2w[q]x + 2[q]x^2 written out entry by entry ([q]x^2 = q q^T - |q|^2 I) into one preallocated array (the
+    stacked 3x3 temporaries and their matmul were most of the write-back's pose time)."""
+    c = np.ascontiguousarray(cam_rows[:, :7], dtype=np.float64).T
+    qx, qy, qz, w = c[3], c[4], c[5], c[6]
     n = cam_rows.shape[0]
-    K = np.zeros((n, 3, 3))
-    K[:, 0, 1], K[:, 0, 2] = -qz, qy
-    K[:, 1, 0], K[:, 1, 2] = qz, -qx
-    K[:, 2, 0], K[:, 2, 1] = -qy, qx
-    M = np.eye(4)[None].repeat(n, axis=0)
-    M[:, :3, :3] = np.eye(3)[None] + 2.0 * w[:, None, None] * K + 2.0 * K @ K
-    M[:, :3, 3] = t
+    M = np.empty((n, 4, 4))
+    xx, yy, zz = qx * qx, qy * qy, qz * qz
+    xy, xz, yz = qx * qy, qx * qz, qy * qz
+    wx, wy, wz = w * qx, w * qy, w * qz
+    M[:, 0, 0] = 1.0 - 2.0 * (yy + zz)
+    M[:, 0, 1] = 2.0 * (xy - wz)
+    M[:, 0, 2] = 2.0 * (xz + wy)
+    M[:, 1, 0] = 2.0 * (xy + wz)
+    M[:, 1, 1] = 1.0 - 2.0 * (xx + zz)
+    M[:, 1, 2] = 2.0 * (yz - wx)
+    M[:, 2, 0] = 2.0 * (xz - wy)
+    M[:, 2, 1] = 2.0 * (yz + wx)
+    M[:, 2, 2] = 1.0 - 2.0 * (xx + yy)
+    M[:, :3, 3] = c[:3].T
+    M[:, 3, :3] = 0.0
+    M[:, 3, 3] = 1.0
     return M
 
 
@@ -268,15 +279,19 @@ def update(cameras, images, tracks, packed, camera_params, points_3d, phases=Non
             tracks[keys[orig]].xyz = xyz
     t2 = time.perf_counter()
     mats = _pose_matrices(full[:, :7])
+    t3 = time.perf_counter()
     last = {}
     for i, image_id in enumerate(packed.unique_cameras.tolist()):
         image = images[image_id]
         image.world2cam = mats[i]
         last[image.cam_id] = i            # :33-36 set_params per image: the last image of a camera wins
+    t4 = time.perf_counter()
     for cam_id, i in last.items():
         cameras[cam_id].set_params(full[i, 7:])
     if phases is not None:
-        phases.update(d2h=t1 - t0, xyz=t2 - t1, poses=time.perf_counter() - t2)
+        t5 = time.perf_counter()
+        phases.update(d2h=t1 - t0, xyz=t2 - t1, poses=t5 - t2, poses_mats=t3 - t2, poses_images=t4 - t3,
+                      poses_set_params=t5 - t4)
 
 
 class TorchBA:
