@@ -804,6 +804,13 @@ def main():
              "launches_per_step": round(lps, 3), "device_us_per_step": round(per_step, 2),
              "timing": "hipEvents on the library stream (insfm_ba_debug_time_kernel / insfm_ba_debug_time_cgp)"}
         if kname == "k_tl_cgp":
+            # (the PMC traffic was taken at its own iteration count; its ratio to the algorithmic
+            # bytes is only meaningful at the same count)
+            tit = traffic_it.get(kname)
+            if tit and traffic_tab.get(kname):
+                nb_t = algorithmic_bytes("k_tl_cgp", C, Pl, Nl, D, nnzb, dict(ext, iters=tit))
+                e.update(algorithmic_bytes_at_traffic_iterations=int(nb_t),
+                         traffic_over_algorithmic_at_traffic_iterations=round(traffic_tab[kname] / nb_t, 3))
             e.update(iterations_per_solve=round(ext["iters"], 2), traffic_iterations=traffic_it.get(kname),
                      us_per_iteration_incl_setup_share=round(avg_us / max(ext["iters"], 1.0), 3),
                      bytes_formula="8*[(nnzb-C)*D^2 + C*D*(D+1) + C*D^2 + 16*C*D + iters*(m^2 + 2*C*D + 4*m + 2*(3*nc+m))]",
