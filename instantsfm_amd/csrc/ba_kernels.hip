@@ -51,7 +51,7 @@ constexpr int kLdsBudget = 96 * 1024;  // dynamic LDS cap for one k_schur workgr
 #endif
 constexpr int kLdsTarget = SCHUR_LDS_KB * 1024;
 #ifndef SCHUR_LDS_KB_DET
-#define SCHUR_LDS_KB_DET 40  // deterministic mode's k_schur row-chunk LDS target (one wave per workgroup)
+#define SCHUR_LDS_KB_DET 52  // deterministic mode's k_schur row-chunk LDS target (3 four-wave workgroups per CU)
 #endif
 constexpr int kLdsTargetDet = SCHUR_LDS_KB_DET * 1024;
 #ifndef INSFM_SCHUR_WAVES
@@ -80,6 +80,18 @@ constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 /
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
+// deterministic mode's k_schur: waves per workgroup; with more than one the waves take their LDS adds in turn.
+// Measured on config 3 (profiles/r6_v7/det_ab*.txt, k_schur per trial): 1 wave (round 5) 1.15 ms; 2 / 3 / 4 / 6 / 8
+// waves 1.06 / 0.97 / 0.90 / 1.68 / 1.36 ms (4 waves at 5 partners in flight: 148 VGPRs, three workgroups per CU;
+// 3 / 4 / 10 partners in flight 0.98 / 0.93 / 1.10 ms; row chunks of 40 / 52 / 64 KB 1.33 / 0.90 / 1.03 ms)
+#ifndef SCHUR_DET_WAVES
+#define SCHUR_DET_WAVES 4
+#endif
+#ifndef SCHUR_UP_DET
+#define SCHUR_UP_DET 5  // partners in flight per group in the turn-taking form
+#endif
+#define SCHUR_DET_ORD (SCHUR_DET_WAVES > 1)
+constexpr int kDetWaves = SCHUR_DET_WAVES;
 
 // ------------------------------------------------------------------------------------------------------------
 // reductions
@@ -627,7 +639,7 @@ __device__ __forceinline__ void load_wcol(const double* __restrict__ W, int o, i
 #ifndef SCHUR_PROBE
 #define SCHUR_PROBE 0
 #endif
-template <int D, int WAVES, bool GPW = false, bool RETRY = false>
+template <int D, int WAVES, bool GPW = false, bool RETRY = false, bool ORD = false>
 __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __restrict__ work, const int* __restrict__ row_ptr,
                                                       const int* __restrict__ col, int C, const int* __restrict__ cam_ptr,
                                                       const int* __restrict__ cam_obs, const int* __restrict__ ptl,
@@ -672,7 +684,12 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         const int e0 = ob + wv * NG + g;
         if (active && e0 < oe) dnext = sdesc[e0];
     }
-    for (int base = ob + wv * NG; base < oe; base += WAVES * NG) {
+    // ORD (deterministic mode): every wave runs the same number of rounds, and in each partner round the waves make
+    // their LDS adds in turn (wave 0 first, a barrier between turns), so each slot sees its additions in a fixed order
+    // -- lanes of one wave adding into one address within one instruction are ordered by the hardware -- while the
+    // waves' gathers stay in flight together
+    const int nround = ORD ? (oe - ob + WAVES * NG - 1) / (WAVES * NG) : 0;
+    for (int base = ob + wv * NG, rd = 0; ORD ? rd < nround : base < oe; base += WAVES * NG, ++rd) {
         const int e = base + g;
         const bool has = active && e < oe;
         const int4 dcur = dnext;
@@ -680,7 +697,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             const int en = e + WAVES * NG;
             if (active && en < oe) dnext = sdesc[en];
         }
-        constexpr int UP = SCHUR_UP;  // partners in flight per group
+        constexpr int UP = ORD ? SCHUR_UP_DET : SCHUR_UP;  // partners in flight per group
         const int qs = has ? dcur.z : 0, qe = has ? dcur.w : 0;
         const int n = qe - qs;
         // issue order = wait order (vmcnt retires in order): the own record first, then the first UP partner records,
@@ -735,7 +752,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         }
         // rounds while any lane of the wave has partners left: a ballot (scalar compare) instead of a shuffle max of n,
         // which cost six ds_bpermute per own-observation round on the LDS pipe the accumulation already saturates
-        for (int k0 = 0; __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
+        for (int k0 = 0; ORD ? __syncthreads_or(k0 < n) != 0 : __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
             if (k0 > 0) {
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
@@ -763,6 +780,9 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (vmcnt, expcnt unconstrained): all slots read
             __builtin_amdgcn_sched_barrier(0);
 #endif
+            // ORD: wave w adds between the w-th and the (w+1)-th of the round's WAVES barriers
+            if constexpr (ORD)
+                for (int k = 0; k < wv; ++k) __syncthreads();
 #pragma unroll
             for (int u = 0; u < UP; ++u) {
                 if (cj[u] >= 0) {
@@ -782,10 +802,16 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
                     }
                 }
             }
+            if constexpr (ORD)
+                for (int k = wv; k < WAVES; ++k) __syncthreads();
         }
         __builtin_amdgcn_wave_barrier();
     }
+    if constexpr (ORD)
+        for (int k = 0; k < wv; ++k) __syncthreads();
     if (diag_chunk && active) atomicAdd(bacc + cb, breg);
+    if constexpr (ORD)
+        for (int k = wv; k < WAVES; ++k) __syncthreads();
     if (SCHUR_PROBE != 0 && probe_sum == 1.2345e-300) acc[0] = probe_sum;  // (never true: a use of the probed sums)
     __syncthreads();
     double* Sout = S + (size_t)kb * DD;
@@ -2477,10 +2503,10 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
                  bool retry, int w0 = 0, int w1 = -1) {
     const bool det = h->d.deterministic != 0;
     if (w1 < 0) w1 = h->nwork;
-    const int nt = det ? 64 : kSchurWaves * 64;
+    const int nt = det ? kDetWaves * 64 : kSchurWaves * 64;
     if (h->kind == 1) {
         if (det)
-            k_schur<3, 1, true><<<h->nwork, nt, h->schur_lds, h->stream>>>(
+            k_schur<3, kDetWaves, true, false, SCHUR_DET_ORD><<<h->nwork, nt, h->schur_lds, h->stream>>>(
                 h->work, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam, h->W,
                 h->Vinv, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, nullptr);
         else
@@ -2496,7 +2522,7 @@ int launch_schur(insfm_ba* h, const double* Uin, const double* gcin, double sf, 
                 h->work + w0, h->row_ptr, h->col, h->C, h->cam_ptr, h->cam_obs, h->ptl, h->pt_ptr, h->ustart, h->sdesc, h->cam,
                 h->W, h->Mp, h->y, Uin, gcin, sf, smin, smax, sdiag, h->S, h->b, stamp_ptr(h, kStSchur));
         };
-        if (det) retry ? go(k_schur<DV, 1, false, true>) : go(k_schur<DV, 1>);
+        if (det) retry ? go(k_schur<DV, kDetWaves, false, true, SCHUR_DET_ORD>) : go(k_schur<DV, kDetWaves, false, false, SCHUR_DET_ORD>);
         else retry ? go(k_schur<DV, kSchurWaves, false, true>) : go(k_schur<DV, kSchurWaves>);
         return launch_err(h, "k_schur");
     });
@@ -3778,11 +3804,12 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     if (nj.empty()) nj.push_back(0);
     tick("CG neighbour lists");
     // Schur work items: split long rows so a chunk fits the LDS budget
-    // Deterministic mode runs k_schur with one wave per workgroup (fixed order of the LDS adds): its workgroups stage
-    // one wave's W^ and take row chunks of <= kLdsTargetDet, so that several share a CU.  (With the 96-KB chunks of the
-    // 8-wave form one wave held a whole CU: k_schur 2.1 ms per trial on config 3 in deterministic mode.)
+    // Deterministic mode's k_schur runs kDetWaves waves per workgroup taking their LDS adds in turn (round 6; one wave
+    // in round 5): its workgroups stage kDetWaves waves' W^ and take row chunks of <= kLdsTargetDet, so that three
+    // share a CU.  (With the 96-KB chunks of the 8-wave form one wave held a whole CU: k_schur 2.1 ms per trial on
+    // config 3 in deterministic mode.)
     const bool det_schur = desc->deterministic != 0;
-    const size_t wsh_lds = sizeof(double) * (det_schur ? 1 : kSchurWaves) * (64 / D) * schur_ws(D);  // W^ staging
+    const size_t wsh_lds = sizeof(double) * (det_schur ? kDetWaves : kSchurWaves) * (64 / D) * schur_ws(D);  // W^ staging
     const size_t fixed_lds = sizeof(double) * (D + 12) + sizeof(int) * (size_t)C + wsh_lds + 64;
     if (fixed_lds + sizeof(double) * D * D > (size_t)kLdsBudget) return fail(INSFM_BA_EINVAL, "too many cameras for LDS");
     // chunk target: kLdsTarget (deterministic mode kLdsTargetDet) when at least 8 blocks fit under it, else the hard
@@ -3961,16 +3988,17 @@ int create_impl(const insfm_ba_desc* desc, int kind, const double* obs, const in
     // the Schur kernels may need more than the default dynamic-LDS limit
     with_D(D, [&](auto dc_) -> int {
         constexpr int DV = decltype(dc_)::value;
-        (void)hipFuncSetAttribute((const void*)k_schur<DV, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, kDetWaves, false, false, SCHUR_DET_ORD>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)h->schur_lds);
-        (void)hipFuncSetAttribute((const void*)k_schur<DV, 1, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)h->schur_lds);
+        (void)hipFuncSetAttribute((const void*)k_schur<DV, kDetWaves, false, true, SCHUR_DET_ORD>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         (void)hipFuncSetAttribute((const void*)k_schur<DV, kSchurWaves, false, true>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
         if constexpr (DV == 3) {
-            (void)hipFuncSetAttribute((const void*)k_schur<3, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)h->schur_lds);
+            (void)hipFuncSetAttribute((const void*)k_schur<3, kDetWaves, true, false, SCHUR_DET_ORD>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->schur_lds);
             (void)hipFuncSetAttribute((const void*)k_schur<3, kSchurWaves, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       (int)h->schur_lds);
             (void)hipFuncSetAttribute((const void*)k_schur_gp<kSchurWaves, kGPSG>, hipFuncAttributeMaxDynamicSharedMemorySize,

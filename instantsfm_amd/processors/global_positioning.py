@@ -167,9 +167,10 @@ class TorchGP:
                                huber_delta=opts['thres_loss_function'], deterministic=opts.get('deterministic', False),
                                **{k: opts[k] for k in ('pcg_max_iter', 'pcg_tol', 'precond') if k in opts})
         dev = torch.device(self.device)
-        pos_t = torch.from_numpy(pk.camera_translations).to(dev).contiguous()
-        pts_t = torch.from_numpy(pk.points_3d).to(dev).contiguous()
-        scl_t = torch.from_numpy(pk.scales).to(dev).contiguous()
+        # (np.require: a read-only pack array -- a broadcast or a mapped buffer -- is copied, torch needs a writable one)
+        pos_t = torch.from_numpy(np.require(pk.camera_translations, requirements='W')).to(dev).contiguous()
+        pts_t = torch.from_numpy(np.require(pk.points_3d, requirements='W')).to(dev).contiguous()
+        scl_t = torch.from_numpy(np.require(pk.scales, requirements='W')).to(dev).contiguous()
         t2 = time.perf_counter()
         window_size = 4                                                                         # :172-186
         loss_history = []
