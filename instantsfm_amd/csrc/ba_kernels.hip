@@ -657,6 +657,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
     constexpr int NG = 64 / D;  // observation groups per wave
     constexpr int NT = WAVES * 64;
     extern __shared__ __attribute__((aligned(16))) double sh[];
+    __shared__ int rnd_sh[ORD ? 2 * WAVES : 1];  // (ORD) partner-round counts of the waves, by own-round parity
     const int4 wk = work[blockIdx.x];
     const int i = wk.x, kb = wk.y, ke = wk.z, nb = ke - kb;
     double* acc = sh;
@@ -680,12 +681,21 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
     // per own observation one descriptor {o, p, partner begin, partner end}: one load gives every index, and the next
     // round's descriptor is loaded while the current round runs (the round chain is latency-bound, not byte-bound)
     int4 dnext = make_int4(0, 0, 0, 0);
+    constexpr int UP = ORD ? SCHUR_UP_DET : SCHUR_UP;  // partners in flight per group
     {
         const int e0 = ob + wv * NG + g;
         if (active && e0 < oe) dnext = sdesc[e0];
+        if constexpr (ORD) {  // the first own round's partner-round count of each wave
+            const int n0 = (active && e0 < oe) ? dnext.w - dnext.z : 0;
+            int nr0 = 0;
+            while (__builtin_amdgcn_ballot_w64(nr0 * UP < n0) != 0) ++nr0;
+            if (lane == 0) rnd_sh[wv] = nr0;
+            __syncthreads();
+        }
     }
-    // ORD (deterministic mode): every wave runs the same number of rounds, and in each partner round the waves make
-    // their LDS adds in turn (wave 0 first, a barrier between turns), so each slot sees its additions in a fixed order
+    // ORD (deterministic mode): every wave runs the same number of rounds (own observations, and per own round the
+    // workgroup's partner rounds), and in each partner round the waves make their LDS adds in turn (wave 0 first, a
+    // barrier between turns), so each slot sees its additions in a fixed order
     // -- lanes of one wave adding into one address within one instruction are ordered by the hardware -- while the
     // waves' gathers stay in flight together
     const int nround = ORD ? (oe - ob + WAVES * NG - 1) / (WAVES * NG) : 0;
@@ -697,7 +707,6 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             const int en = e + WAVES * NG;
             if (active && en < oe) dnext = sdesc[en];
         }
-        constexpr int UP = ORD ? SCHUR_UP_DET : SCHUR_UP;  // partners in flight per group
         const int qs = has ? dcur.z : 0, qe = has ? dcur.w : 0;
         const int n = qe - qs;
         // issue order = wait order (vmcnt retires in order): the own record first, then the first UP partner records,
@@ -752,7 +761,20 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
         }
         // rounds while any lane of the wave has partners left: a ballot (scalar compare) instead of a shuffle max of n,
         // which cost six ds_bpermute per own-observation round on the LDS pipe the accumulation already saturates
-        for (int k0 = 0; ORD ? __syncthreads_or(k0 < n) != 0 : __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
+        // ORD: the workgroup's partner-round count, the most any wave needs.  Each wave writes the next own round's
+        // count (from the prefetched descriptor, by round parity) before this round's last barrier: the readers of
+        // that buffer slot, two rounds back, have all passed the previous round's last barrier.
+        int nrd = 0;
+        if constexpr (ORD) {
+#pragma unroll
+            for (int w2 = 0; w2 < WAVES; ++w2) nrd = max(nrd, rnd_sh[(rd & 1) * WAVES + w2]);
+            const int en = e + WAVES * NG;
+            const int nn = (active && en < oe) ? dnext.w - dnext.z : 0;
+            int nrn = 0;
+            while (__builtin_amdgcn_ballot_w64(nrn * UP < nn) != 0) ++nrn;
+            if (lane == 0) rnd_sh[((rd + 1) & 1) * WAVES + wv] = nrn;
+        }
+        for (int k0 = 0; ORD ? k0 < nrd * UP : __builtin_amdgcn_ballot_w64(k0 < n) != 0; k0 += UP) {
             if (k0 > 0) {
 #pragma unroll
                 for (int u = 0; u < UP; ++u) {
@@ -805,6 +827,7 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             if constexpr (ORD)
                 for (int k = wv; k < WAVES; ++k) __syncthreads();
         }
+        if (ORD && nrd == 0) __syncthreads();  // (a round without partners: its one barrier)
         __builtin_amdgcn_wave_barrier();
     }
     if constexpr (ORD)
