@@ -13,7 +13,8 @@ from .engine import _require_gpu
 
 
 def _dev(a, dev, dtype=None):
-    t = torch.from_numpy(np.ascontiguousarray(a if dtype is None else np.asarray(a, dtype=dtype)))
+    # (np.require: C-contiguous and writable -- a read-only input is copied, torch.from_numpy needs a writable array)
+    t = torch.from_numpy(np.require(a if dtype is None else np.asarray(a, dtype=dtype), requirements=("C", "W")))
     return t.to(dev, non_blocking=False).contiguous()
 
 
