@@ -19,7 +19,6 @@
 #include <Python.h>
 #define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
 #include <numpy/arrayobject.h>
-#include <malloc.h>
 #include <pthread.h>
 #include <sched.h>
 #include <stdint.h>
@@ -477,8 +476,16 @@ done:
     return res;
 }
 
-/* assign_xyz(track_vals, unique_points int64[n], points float64[n, 3]): track_vals[unique_points[i]].xyz = points[i]
- * (a row view of `points`, as the Python loop of update() assigns it; bundle_adjustment.py:18-36). */
+/* assign_xyz(track_vals, unique_points int64[n], points float64[n, 3]): track_vals[unique_points[i]].xyz = a float64
+ * [3] array holding points[i] (bundle_adjustment.py:18-36 assigns the row views of one array; the values are the same).
+ * When the track's current xyz is an array nothing else can see -- an exact float64 [3] ndarray that owns its
+ * writable buffer, referenced only by the track's attribute (refcount 2 with ours) and by no weak reference -- the
+ * point is written into it: no caller can tell that apart from a new array, and no allocation or free happens (a
+ * scene whose tracks were built one array each, or written back by an earlier call).  Otherwise the track gets a new
+ * array that owns its 24 bytes (so the next call can take the first path).  Round 5 assigned row views of `points`:
+ * one allocation per track for two frees when the old arrays owned their buffers, and the 200k chunks left in
+ * glibc's bins made the next allocation of a kilobyte or more sort them all (malloc_consolidate / the unsorted-bin
+ * scan: ~5 ms on the GPU box's host, 20 ms on this container's). */
 static PyObject* assign_xyz(PyObject* self, PyObject* args) {
     (void)self;
     PyObject *seq, *o_idx, *o_pts;
@@ -496,46 +503,41 @@ static PyObject* assign_xyz(PyObject* self, PyObject* args) {
     const Py_ssize_t T = PySequence_Fast_GET_SIZE(fast);
     PyObject** items = PySequence_Fast_ITEMS(fast);
     const int64_t* idx = (const int64_t*)PyArray_DATA(ai);
-    char* base = (char*)PyArray_DATA(ap);
+    const double* base = (const double*)PyArray_DATA(ap);
     const npy_intp n = PyArray_DIM(ap, 0);
     npy_intp dims[1] = {3};
-    PyArray_Descr* d8 = PyArray_DescrFromType(NPY_FLOAT64);  /* (one lookup; each view takes a reference) */
-    if (!d8) { Py_DECREF(fast); return NULL; }
-    /* Every assignment releases the track's previous xyz array; when those own their 24-byte buffers (a scene whose
-     * tracks were built one array each) 200k small free()s land in glibc's fastbins, and the next allocation of a
-     * kilobyte or more merges them all at once (malloc_consolidate: ~20 ms on this container's host, ~5 ms on the GPU
-     * box, paid by whatever allocates next).  For the duration of the loop the fastbins are off (mallopt(M_MXFAST, 0)
-     * consolidates what they hold and sends later frees to the regular bins), then the default is restored. */
-    mallopt(M_MXFAST, 0);
     for (npy_intp i = 0; i < n; ++i) {
         if (idx[i] < 0 || idx[i] >= T) {
             PyErr_SetString(PyExc_IndexError, "assign_xyz: track index");
-            Py_DECREF(d8);
             Py_DECREF(fast);
-            mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);
             return NULL;
         }
-        Py_INCREF(d8);
-        PyObject* row = PyArray_NewFromDescr(&PyArray_Type, d8, 1, dims, NULL, base + 24 * i, NPY_ARRAY_CARRAY, NULL);
-        if (!row) { Py_DECREF(d8); Py_DECREF(fast); mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4); return NULL; }
-        Py_INCREF(o_pts);
-        if (PyArray_SetBaseObject((PyArrayObject*)row, o_pts) < 0) {
-            Py_DECREF(row); Py_DECREF(d8); Py_DECREF(fast);
-            mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);
-            return NULL;
+        PyObject* cur = PyObject_GetAttr(items[idx[i]], s_xyz);
+        if (!cur) PyErr_Clear();
+        else if (PyArray_CheckExact(cur) && Py_REFCNT(cur) == 2) {
+            PyArrayObject* ca = (PyArrayObject*)cur;
+            if (PyArray_NDIM(ca) == 1 && PyArray_DIM(ca, 0) == 3 && PyArray_TYPE(ca) == NPY_FLOAT64 &&
+                PyArray_ISNOTSWAPPED(ca) && PyArray_IS_C_CONTIGUOUS(ca) && PyArray_ISWRITEABLE(ca) &&
+                PyArray_CHKFLAGS(ca, NPY_ARRAY_OWNDATA) && ((PyArrayObject_fields*)ca)->weakreflist == NULL) {
+                memcpy(PyArray_DATA(ca), base + 3 * i, 3 * sizeof(double));
+                Py_DECREF(cur);
+                continue;
+            }
         }
+        Py_XDECREF(cur);
+        PyObject* row = PyArray_SimpleNew(1, dims, NPY_FLOAT64);
+        if (!row) { Py_DECREF(fast); return NULL; }
+        memcpy(PyArray_DATA((PyArrayObject*)row), base + 3 * i, 3 * sizeof(double));
         const int r = PyObject_SetAttr(items[idx[i]], s_xyz, row);
         Py_DECREF(row);
-        if (r < 0) { Py_DECREF(d8); Py_DECREF(fast); mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4); return NULL; }
+        if (r < 0) { Py_DECREF(fast); return NULL; }
     }
-    Py_DECREF(d8);
     Py_DECREF(fast);
-    mallopt(M_MXFAST, 64 * (int)sizeof(size_t) / 4);  /* (glibc's DEFAULT_MXFAST) */
     Py_RETURN_NONE;
 }
 
 static PyMethodDef methods[] = {
-    {"assign_xyz", assign_xyz, METH_VARARGS, "track.xyz = row view of the optimized points, per packed point."},
+    {"assign_xyz", assign_xyz, METH_VARARGS, "track.xyz = the optimized point (an owned float64 [3]), per packed point."},
     {"collect", collect, METH_VARARGS, "Track observations / xyz through the buffer protocol (or None)."},
     {"finish", finish, METH_VARARGS, "Registered filter, feature gather, cheirality test and compaction."},
     {NULL, NULL, 0, NULL},

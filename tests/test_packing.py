@@ -141,3 +141,41 @@ def test_native_pack_is_built_and_matches_numpy_path():
     c = pack(cams, imgs, tracks, OPTS)
     for x, y in zip(_fields(c), _fields(b)):
         np.testing.assert_array_equal(x, y)
+
+
+def test_assign_xyz_writes_in_place_only_when_unobservable():
+    """packx.assign_xyz (update()'s track.xyz write-back, bundle_adjustment.py:18-36): an xyz array nothing else can
+    see -- an exact float64 [3] ndarray owning its writable buffer, held only by the track -- gets the point written
+    into it; any other xyz (held elsewhere, a view, weak-referenced, another dtype or shape, a subclass, a list, absent)
+    is replaced by a new owned float64 [3] array and the old object keeps its values."""
+    import weakref
+    from instantsfm_amd.processors import bundle_adjustment as BA
+    px = BA.packx()
+    assert px is not None
+    n = 9
+    tracks = [Track() for _ in range(n)]
+    held = np.array([7.0, 7.0, 7.0])
+    base = np.arange(30.0)
+    tracks[1].xyz = held                       # referenced elsewhere
+    tracks[2].xyz = base[3:6]                  # a view
+    tracks[3].xyz = np.zeros(3)
+    wr = weakref.ref(tracks[3].xyz)            # weak-referenced
+    tracks[4].xyz = np.zeros(3, np.float32)    # another dtype
+    tracks[5].xyz = np.zeros(4)                # another shape
+    tracks[6].xyz = np.zeros(3).view(np.matrix)  # a subclass
+    tracks[7].xyz = [0.0, 0.0, 0.0]            # not an array
+    del tracks[8].xyz                          # absent
+    own_id = id(tracks[0].xyz)
+    pts = np.arange(3.0 * n).reshape(n, 3) + 0.5
+    order = np.arange(n - 1, -1, -1, dtype=np.int64)   # point i -> track n - 1 - i
+    px.assign_xyz(tracks, order, pts)
+    for i in range(n):
+        x = tracks[n - 1 - i].xyz
+        assert type(x) is np.ndarray and x.dtype == np.float64 and x.shape == (3,) and x.flags.owndata
+        assert np.array_equal(x, pts[i])
+    assert id(tracks[0].xyz) == own_id        # written in place
+    assert np.array_equal(held, [7.0, 7.0, 7.0]) and tracks[1].xyz is not held
+    assert np.array_equal(base, np.arange(30.0))
+    assert wr() is None                         # replaced (not written in place) and released
+    pts[:] = 0.0                                 # the tracks own their values
+    assert np.array_equal(tracks[n - 1].xyz, np.arange(3.0) + 0.5)
