@@ -80,6 +80,15 @@ constexpr int kCostThreads = COST_THREADS;  // k_cost workgroup size (64 / 128 /
 #ifndef SCHUR_UP
 #define SCHUR_UP 10
 #endif
+#ifndef LIN_NT_STORE
+// k_lin_points: the 384-MB Y-record stream stored with the nontemporal hint (global_store_dwordx4 ... nt).  Config 3
+// (profiles/r6_v10/nt_ab.txt, same box): back-to-back launches 152-153 -> 85 us, LM step 1.046-1.050 -> 1.013-1.033
+// ms; k_schur, which reads the records next, unchanged (440-448 us).
+#define LIN_NT_STORE 1
+#endif
+#ifndef SCHUR_NT_STORE
+#define SCHUR_NT_STORE 0  // k_schur: S blocks stored with the nontemporal hint (A/B builds)
+#endif
 // deterministic mode's k_schur: waves per workgroup; with more than one the waves take their LDS adds in turn.
 // Measured on config 3 (profiles/r6_v7/det_ab*.txt, k_schur per trial): 1 wave (round 5) 1.15 ms; 2 / 3 / 4 / 6 / 8
 // waves 1.06 / 0.97 / 0.90 / 1.68 / 1.36 ms (4 waves at 5 partners in flight: 148 VGPRs, three workgroups per CU;
@@ -252,7 +261,13 @@ __device__ __forceinline__ void store_records(const double* wst, double* __restr
         for (int k2 = t; k2 < n * (WR / 2); k2 += kLinThreads) {
             const int k = 2 * k2, rec = k / WR, e = k - rec * WR;
             const double* src = wst + rec * WRP + e;
+#if LIN_NT_STORE
+            typedef double nt_d2 __attribute__((ext_vector_type(2)));
+            nt_d2 v2 = {src[0], src[1]};
+            __builtin_nontemporal_store(v2, reinterpret_cast<nt_d2*>(dst + k2));
+#else
             dst[k2] = make_double2(src[0], src[1]);
+#endif
         }
     } else {
         double* dst = Y + (size_t)base * WR;
@@ -847,7 +862,11 @@ __global__ __launch_bounds__(WAVES * 64, SCHUR_MINW) void k_schur(const int4* __
             if (a2 == bb) u = clampd(u, cmin, cmax) * f;
             v += u;
         }
+#if SCHUR_NT_STORE
+        __builtin_nontemporal_store(v, Sout + k);
+#else
         Sout[k] = v;
+#endif
     }
     if (diag_chunk && t < D) b[(size_t)i * D + t] = (add_diag ? gc[(size_t)i * D + t] : 0.0) + bacc[t];
 }

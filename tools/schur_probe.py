@@ -34,5 +34,6 @@ losses = [eng.step(cams, pts)[0] for _ in range(8)]
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / 8
 us = eng.debug_time_kernel(1, 20)
-print(f"{os.path.basename(os.environ.get('INSFM_LIB', 'default'))}{' det' if os.environ.get('DET') else ''}: k_schur {us:.1f} us, step {dt*1e3:.3f} ms, "
-      f"loss {losses[-1]:.10e}", flush=True)
+ul = eng.debug_time_kernel(5, 20)
+print(f"{os.path.basename(os.environ.get('INSFM_LIB', 'default'))}{' det' if os.environ.get('DET') else ''}: k_schur {us:.1f} us, "
+      f"k_lin_points {ul:.1f} us, step {dt*1e3:.3f} ms, loss {losses[-1]:.10e}", flush=True)
