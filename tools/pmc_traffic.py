@@ -9,7 +9,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_schur": 1.0, "k_tl_pspmv": 2.0, "k_cg_iter": 2.0, "k_tl_cgp": 1.0}
+KERNELS = {"k_schur": 1.0, "k_tl_pspmv": 2.0, "k_cg_iter": 2.0, "k_tl_cgp": 1.0, "k_lin_points": 1.0}
 
 
 def load(path, counter):
