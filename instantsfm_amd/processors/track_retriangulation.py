@@ -85,9 +85,13 @@ def complete_tracks(cameras, images, tracks, tracks_orig, TRIANGULATOR_OPTIONS, 
 
 
 def merge_tracks(cameras, images, tracks, TRIANGULATOR_OPTIONS):
-    """track_retriangulation.py:110-198 -- not on the path: it needs faiss (never imported by the reference) and its
-    only caller has it commented out (:210-212)."""
-    raise NotImplementedError("merge_tracks is unused by the reference pipeline (track_retriangulation.py:210-212)")
+    """track_retriangulation.py:110-198 -- not on the path, and not callable in the reference either: its k-NN search
+    is `faiss.IndexFlatL2` (:136), but the module never imports faiss (:1-14), so a call raises NameError there before
+    any track is touched; its only caller has the call commented out (:210-212, "current version of merge does not
+    have a good result and is not used in the pipeline").  This raises at the same point, with the reason."""
+    raise NotImplementedError("merge_tracks: the reference's version cannot run (faiss is used at "
+                              "track_retriangulation.py:136 but never imported) and its only call is commented out "
+                              "(:210-212)")
 
 
 def filter_points(cameras, images, tracks, TRIANGULATOR_OPTIONS, device="cuda:0"):
