@@ -157,6 +157,27 @@ def test_deterministic_mode_bitwise():
     assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
 
 
+def test_deterministic_schur_bitwise_config3():
+    """Deterministic mode's k_schur on the full config-3 scene (round 6: four waves per row chunk taking their LDS adds
+    in turn, several partner rounds per own round): two handles build bitwise the same S and b and solve to bitwise the
+    same camera step; S agrees with the atomic (non-deterministic) build to rounding."""
+    prob = make_config(3)
+    C, D = prob.n_cams, 8
+    out = []
+    for det in (True, True, False):
+        eng = BundleAdjuster(prob.model, prob.uv, prob.cam_idx, prob.pt_idx, prob.pp, prob.n_cams, prob.n_points,
+                             device=DEV, deterministic=det)
+        eng.debug_linearize(dev(prob.cams_init), dev(prob.points_init))
+        eng.debug_solve(1.0 + 1e-4)
+        nb = eng.nnzb()
+        out.append((eng.debug_get(5, (nb, D, D)), eng.debug_get(6, (C, D)), eng.debug_get(7, (C, D))))
+        eng.close()
+    (S1, b1, d1), (S2, b2, d2), (S3, b3, _) = out
+    assert np.array_equal(S1, S2) and np.array_equal(b1, b2) and np.array_equal(d1, d2)
+    assert np.max(np.abs(S1 - S3)) <= 1e-12 * np.max(np.abs(S3))
+    assert np.max(np.abs(b1 - b3)) <= 1e-12 * np.max(np.abs(b3))
+
+
 def test_cost_matches_oracle():
     prob = make_config(1, seed=7)
     eng, ora = engines(prob)
