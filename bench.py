@@ -26,6 +26,10 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_PEAK_TFS = 78.6   # MI355X dense FP64 (MFMA = vector rate on gfx950)
+# ds_add_f64 issue cost in k_schur's pattern (8 groups of 8 lanes, each group 8 contiguous doubles of its own block):
+# 8.5 CU clocks per wave-instruction at 8 and at 16 waves per CU (tools/lds_atomic_bench.hip mode 1,
+# profiles/r6_v20/lds_bench.txt; the microarchitecture guide gives no rate for LDS f64 atomics)
+LDS_ADD_F64_CLK = 8.5
 
 
 def w_record_doubles(D):
@@ -819,6 +823,23 @@ def main():
         if kname == "k_lin_points":
             e["timing"] = ("back-to-back launches (hipEvents): the sustained rate of its 384-MB record write; in the step "
                            "it overlaps the previous solve's coarse-inverse chain")
+        if kname == "k_schur" and avg_us > 0:
+            # the kernel's other ceiling: its LDS f64 accumulation.  Every (own observation, upper partner incl.
+            # itself) pair of a track adds one D x D block: D*D lane-adds = D*D/64 ds_add_f64 wave-instructions
+            lt = np.bincount(prob.pt_idx[(prob.pt_idx >= shards[rank][0]) & (prob.pt_idx < shards[rank][1])])
+            pairs = int(np.sum(lt * (lt + 1) // 2))
+            winstr = pairs * D * D / 64.0
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            clk_per = avg_us * 2400.0 / (winstr / ncu)  # CU clocks per wave-instruction at 2.4 GHz
+            e["roofline_lds"] = {
+                "bound": "lds", "unit": "ds_add_f64 wave-instructions per CU clock",
+                "achieved": round(1.0 / clk_per, 5), "peak": round(1.0 / LDS_ADD_F64_CLK, 5),
+                "frac": round(LDS_ADD_F64_CLK / clk_per, 4), "wave_instructions_per_launch": int(winstr),
+                "pairs_per_launch": pairs, "cus": ncu,
+                "peak_source": "tools/lds_atomic_bench.hip mode 1: 8.5 clocks per wave-instruction per CU "
+                               "(profiles/r6_v20/lds_bench.txt)",
+                "note": "the accumulation alone would take frac x the kernel time; the gather floor (loads only, "
+                        "SCHUR_PROBE=2) is ~77 % of it (DESIGN.md section 8)"}
         return e
     roof = roof_entry(name)
     roof["timing"] = roof["timing"] + "; dominant = most device time per LM step on the default path"
